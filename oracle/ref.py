@@ -1,0 +1,278 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+fp32 torch-CPU restatement of the reference's hot-path components.  Each
+function cites the reference lines it follows (paths relative to the reference
+repo).  All functions are differentiable torch code, so backward parity is
+checked through torch.autograd on the same seeded inputs.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_CLIB = None
+
+
+def clib():
+    """The plain-C restatement (oracle/liboracle.so), built by oracle/Makefile."""
+    global _CLIB
+    if _CLIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        lib = ctypes.CDLL(path)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        lib.oracle_kshift_row.restype = i64
+        lib.oracle_kshift_row.argtypes = [i64, i32, i64]
+        lib.oracle_kshift_rows.argtypes = [vp, i64, i64, i32, vp]
+        lib.oracle_kshift_fwd_f32.argtypes = [vp, i64, vp, i64, i32, i32, i32, vp]
+        lib.oracle_kshift_bwd_f32.argtypes = [vp, i64, vp, i64, i32, i32, i32, vp]
+        _CLIB = lib
+    return _CLIB
+
+
+# ---------------------------------------------------------------- embeddings
+def kshift_rows(ids: np.ndarray, P: int, K: int) -> np.ndarray:
+    """commons/layers.py:174-185 (C restatement). Returns [n, K] int64."""
+    ids = np.ascontiguousarray(ids.reshape(-1), dtype=np.int64)
+    out = np.empty((ids.size, K), dtype=np.int64)
+    clib().oracle_kshift_rows(ids.ctypes.data, ids.size, P, K, out.ctypes.data)
+    return out
+
+
+def kshift_fwd_c(ids: np.ndarray, W: np.ndarray, K: int, mode: int) -> np.ndarray:
+    """commons/layers.py:152-172 (C restatement; mode 0 scale, 1 normalize, 2 none)."""
+    shp = ids.shape
+    ids = np.ascontiguousarray(ids.reshape(-1), dtype=np.int64)
+    W = np.ascontiguousarray(W, dtype=np.float32)
+    P, D = W.shape
+    out = np.empty((ids.size, D), dtype=np.float32)
+    clib().oracle_kshift_fwd_f32(ids.ctypes.data, ids.size, W.ctypes.data, P, D, K, mode, out.ctypes.data)
+    return out.reshape(*shp, D)
+
+
+def kshift_bwd_c(ids: np.ndarray, dY: np.ndarray, P: int, K: int, mode: int) -> np.ndarray:
+    ids = np.ascontiguousarray(ids.reshape(-1), dtype=np.int64)
+    D = dY.shape[-1]
+    dY = np.ascontiguousarray(dY.reshape(-1, D), dtype=np.float32)
+    dW = np.zeros((P, D), dtype=np.float32)
+    clib().oracle_kshift_bwd_f32(ids.ctypes.data, ids.size, dY.ctypes.data, P, D, K, mode, dW.ctypes.data)
+    return dW
+
+
+def kshift_row_idx_torch(x: torch.Tensor, c: int, P: int) -> torch.Tensor:
+    """commons/layers.py:174-185, torch form (arithmetic >>, wrapping <<, torch.remainder)."""
+    if c != 0:
+        x = (x << c) | (x >> (64 - c))
+    return torch.remainder(x, P)
+
+
+def kshift_fwd_torch(ids: torch.Tensor, W: torch.Tensor, K: int, normalize: bool) -> torch.Tensor:
+    """commons/layers.py:152-172 (torch form, differentiable w.r.t. W)."""
+    P = W.shape[0]
+    x = F.embedding(kshift_row_idx_torch(ids, 0, P), W)
+    for c in range(1, K):
+        x = x + F.embedding(kshift_row_idx_torch(ids, c, P), W)
+    if normalize:
+        return F.normalize(x, p=2.0, dim=-1)
+    return x / math.sqrt(K)
+
+
+def flat_fwd(ids: torch.Tensor, W: torch.Tensor, normalize: bool, padding_idx: Optional[int] = None):
+    """commons/layers.py:56-61 (FlatEmbedding)."""
+    x = torch.remainder(ids, W.shape[0]).long()
+    x = F.embedding(x, W, padding_idx=padding_idx)
+    return F.normalize(x, p=2.0, dim=-1) if normalize else x
+
+
+def qr_fwd(ids: torch.Tensor, Wq: torch.Tensor, Wr: torch.Tensor, normalize: bool):
+    """commons/layers.py:115-123 with the build's fix (rounding_mode='floor')."""
+    div = Wq.shape[0]
+    x = torch.remainder(ids, div * div)
+    q = torch.remainder(torch.div(x, div, rounding_mode="floor"), div)
+    r = torch.remainder(x, div)
+    y = F.embedding(q, Wq) + F.embedding(r, Wr)
+    return F.normalize(y, p=2.0, dim=-1) if normalize else y
+
+
+def pattern_from_timelocal(ts: torch.Tensor, div: int, mod: int, W: torch.Tensor):
+    """commons/layers.py:39-41 (build fix of the constructor)."""
+    idx = torch.remainder(torch.floor_divide(ts.long(), div), mod)
+    return F.embedding(idx, W)
+
+
+def histogram_embedding(x: torch.Tensor, lo: float, hi: float, nbins: int, W: torch.Tensor):
+    """Build-defined HistogramEmbedding: uniform bins over [lo, hi], clamped."""
+    b = torch.floor((x - lo) / (hi - lo) * nbins).long().clamp(0, nbins - 1)
+    return F.embedding(b, W)
+
+
+# ---------------------------------------------------------- feature interaction
+def quick_gelu(x):
+    """commons/layers.py:9-11."""
+    return x * torch.sigmoid(1.702 * x)
+
+
+def mlp_quickgelu(x, weights: List[torch.Tensor], biases: List[torch.Tensor]):
+    """commons/layers.py:65-81: Linear + QuickGELU per gate, final Linear."""
+    for i, (w, b) in enumerate(zip(weights, biases)):
+        x = F.linear(x, w, b)
+        if i < len(weights) - 1:
+            x = quick_gelu(x)
+    return x
+
+
+class _CapGrad(torch.autograd.Function):
+    """commons/functional.py:4-25."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g / (torch.norm(g) + 1e-6)
+
+
+def cap_gradients(x):
+    return _CapGrad.apply(x)
+
+
+def logq_forward(ids: torch.Tensor, b: torch.Tensor, num_buckets: int, offsets) -> torch.Tensor:
+    """commons/layers.py:202-208 + 225-233: min over offsets of -log b[(id+off) % nb]."""
+    res = None
+    for i, off in enumerate(offsets):
+        h = (ids + off) % num_buckets
+        v = -b[i][h].log().reshape(*ids.shape)
+        res = v if res is None else torch.minimum(res, v)
+    return res
+
+
+# ------------------------------------------------------------------- encoder
+def layer_norm(x, w, b):
+    """commons/transformers/layers.py:142-149 (eps 1e-5)."""
+    return F.layer_norm(x, w.shape, w, b, eps=1e-5)
+
+
+def rel_pos_bias(qk: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """commons/transformers/layers.py:21-35: qk[..., q, k] += table[q - k + nk, h]."""
+    nq, nk = qk.shape[-2], qk.shape[-1]
+    pos = torch.arange(nq)[:, None] - torch.arange(nk)[None, :] + nk
+    return qk + table[pos].permute(2, 0, 1).unsqueeze(0)
+
+
+def sdpa(q, k, v, mask=None, table=None):
+    """commons/transformers/layers.py:49-61 (explicit scores)."""
+    qk = (q @ k.transpose(-2, -1)) / math.sqrt(float(q.size(-1)))
+    if table is not None:
+        qk = rel_pos_bias(qk, table)
+    if mask is not None:
+        qk = qk + mask
+    return F.softmax(qk, dim=-1) @ v
+
+
+def causal_mask(L: int) -> torch.Tensor:
+    """commons/transformers/layers.py:397-402."""
+    m = torch.ones((L, L), dtype=torch.bool).tril(diagonal=0)
+    return m.float().masked_fill(~m, -float("inf"))[None, None]
+
+
+def mha(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix="attn."):
+    """commons/transformers/layers.py:247-265 (dropout p = 0)."""
+    B, T, C = x.shape
+    qkv = F.linear(x, p[prefix + "c_attn.weight"], p.get(prefix + "c_attn.bias"))
+    q, k, v = qkv.split(C, dim=2)
+    q = q.view(B, T, H, C // H).transpose(1, 2)
+    k = k.view(B, T, H, C // H).transpose(1, 2)
+    v = v.view(B, T, H, C // H).transpose(1, 2)
+    y = sdpa(q, k, v, mask, p.get(prefix + "attn.pos_bias.bias"))
+    y = y.transpose(1, 2).contiguous().view(B, T, C)
+    return F.linear(y, p[prefix + "c_proj.weight"], p.get(prefix + "c_proj.bias"))
+
+
+def mqa(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix=""):
+    """commons/transformers/layers.py:214-234."""
+    bs, t, C = x.shape
+    E = C // H
+    q = F.linear(x, p[prefix + "q_proj.weight"], p.get(prefix + "q_proj.bias"))
+    kv = F.linear(x, p[prefix + "kv_proj.weight"], p.get(prefix + "kv_proj.bias"))
+    k, v = kv.split(E, dim=-1)
+    q = q.view(bs, t, H, E).transpose(1, 2)
+    k = k.view(bs, t, 1, E).transpose(1, 2)
+    v = v.view(bs, t, 1, E).transpose(1, 2)
+    y = sdpa(q, k, v, mask, p.get(prefix + "attn.pos_bias.bias"))
+    y = y.transpose(1, 2).contiguous().view(bs, t, C)
+    return F.linear(y, p[prefix + "out_proj.weight"], p.get(prefix + "out_proj.bias"))
+
+
+def mlp_gelu(x, p, prefix="mlp."):
+    """commons/transformers/layers.py:279-284 (GELU tanh, hidden 4d as executed)."""
+    h = F.gelu(F.linear(x, p[prefix + "c_fc.weight"], p.get(prefix + "c_fc.bias")), approximate="tanh")
+    return F.linear(h, p[prefix + "c_proj.weight"], p.get(prefix + "c_proj.bias"))
+
+
+def transformer_block(x, p: Dict[str, torch.Tensor], H: int, causal: bool, attn_mask=None):
+    """commons/transformers/layers.py:382-415 (dense path, no sparse tokens)."""
+    mask = attn_mask
+    if causal:
+        cm = causal_mask(x.size(-2))
+        mask = cm if mask is None else mask + cm
+    x = x + mha(layer_norm(x, p["ln_1.weight"], p.get("ln_1.bias")), p, H, mask)
+    x = x + mlp_gelu(layer_norm(x, p["ln_2.weight"], p.get("ln_2.bias")), p)
+    return x
+
+
+def moe_linear(x, p, num_experts: int, top_k: Optional[int], in_features: int, n_gate_layers: int):
+    """commons/transformers/layers.py:120-136."""
+    h = x
+    for i in range(n_gate_layers):
+        h = F.linear(h, p[f"expert_gates.model.{2 * i}.weight"], p.get(f"expert_gates.model.{2 * i}.bias"))
+        if i < n_gate_layers - 1:
+            h = F.gelu(h, approximate="tanh")
+    gate = h / math.sqrt(float(in_features))
+    if top_k is not None:
+        k = min(top_k, gate.size(-1))
+        v, _ = torch.topk(gate, k, dim=-1)
+        gate = torch.where(gate < v[..., -1:], torch.tensor(-float("inf")), gate)
+    gate = F.softmax(gate, dim=-1)
+    outs = []
+    for e in range(num_experts):
+        u = F.gelu(F.linear(x, p[f"experts.{e}.l1.weight"], p[f"experts.{e}.l1.bias"]), approximate="tanh")
+        outs.append(F.linear(u, p[f"experts.{e}.l2.weight"], p[f"experts.{e}.l2.bias"]))
+    return (torch.stack(outs, dim=-2) * gate.unsqueeze(-1)).sum(dim=-2)
+
+
+# ------------------------------------------------------- vector-feature layers
+def cve_rows(x, projection_mat, grid, pos_offset):
+    """commons/transformers/layers.py:464-468: bucket row indices [.., n_proj]."""
+    z = F.normalize(x, p=2.0, dim=-1) @ projection_mat
+    return torch.bucketize(z, grid) + pos_offset
+
+
+def cve_fwd(x, projection_mat, grid, pos_offset, weight):
+    """commons/transformers/layers.py:462-471 (EmbeddingBag mode='sum')."""
+    bs, T, _ = x.shape
+    idx = cve_rows(x, projection_mat, grid, pos_offset).view(-1, projection_mat.shape[1])
+    return F.embedding_bag(idx, weight, mode="sum").view(bs, T, weight.shape[1])
+
+
+def quantile_mapper(x, quantiles):
+    """commons/transformers/layers.py:484-487."""
+    return torch.bucketize(x, quantiles).to(torch.float32) / float(quantiles.numel() + 1) - 0.5
+
+
+def simhash(x, projection_mat):
+    """commons/transformers/layers.py:431-437."""
+    z = (x @ projection_mat) > 0
+    res = torch.zeros(z.shape[:-1], dtype=torch.long)
+    for i in range(z.size(-1)):
+        res = res + (z[..., i].long() << i)
+    return res

@@ -1,0 +1,131 @@
+"""ctypes binding of the C ABI declared in ``include/lthm.h``.
+
+The prototypes are parsed from the header itself, so the Python side can never
+drift from the ABI a cgo/JNI/ctypes integrator would bind.
+There is deliberately no CPU fallback: every product op calls into
+``liblthm_hip.so`` and raises if the library or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import Dict, List, Tuple
+
+import torch  # noqa: F401  (loads torch's libamdhip64 first, so the .so binds to the same HIP runtime)
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(_PKG_DIR)
+HEADER = os.path.join(REPO_ROOT, "include", "lthm.h")
+LIB_PATH = os.path.join(_PKG_DIR, "liblthm_hip.so")
+
+F32 = 0
+BF16 = 1
+DTYPE_CODE = {torch.float32: F32, torch.bfloat16: BF16}
+
+_CTYPE = {
+    "int64_t*": ctypes.c_void_p,
+    "int32_t*": ctypes.c_void_p,
+    "uint8_t*": ctypes.c_void_p,
+    "uint16_t*": ctypes.c_void_p,
+    "uint64_t*": ctypes.c_void_p,
+    "float*": ctypes.c_void_p,
+    "void*": ctypes.c_void_p,
+    "char*": ctypes.c_char_p,
+    "char**": ctypes.c_void_p,
+    "int64_t": ctypes.c_int64,
+    "uint64_t": ctypes.c_uint64,
+    "int32_t": ctypes.c_int32,
+    "uint32_t": ctypes.c_uint32,
+    "int": ctypes.c_int,
+    "float": ctypes.c_float,
+    "double": ctypes.c_double,
+    "size_t": ctypes.c_size_t,
+}
+
+
+def parse_header(path: str = HEADER) -> Dict[str, Tuple[str, List[str]]]:
+    """Return {name: (return type, [arg types])} for every prototype in lthm.h."""
+    with open(path) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    text = re.sub(r"#[^\n]*", " ", text)
+    protos = {}
+    for m in re.finditer(r"\b(int|void|int64_t|double|float)\s+(lthm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        ret, name, args = m.group(1), m.group(2), m.group(3).strip()
+        types = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = " ".join(a.replace("const ", "").split())
+                # drop the parameter name, keep pointer stars
+                tm = re.match(r"^([A-Za-z_0-9]+)\s*(\**)\s*[A-Za-z_0-9]*$", a.replace(" *", "*").replace("* ", "* "))
+                if tm is None:
+                    base = a.split()[0]
+                    stars = a.count("*")
+                else:
+                    base, stars = tm.group(1), len(tm.group(2))
+                    stars = a.count("*")
+                types.append(base + "*" * stars)
+        protos[name] = (ret, types)
+    return protos
+
+
+_LIB = None
+_PROTOS: Dict[str, Tuple[str, List[str]]] = {}
+
+
+def load() -> ctypes.CDLL:
+    global _LIB, _PROTOS
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: the HIP extension is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    protos = parse_header()
+    for name, (ret, args) in protos.items():
+        fn = getattr(lib, name)
+        fn.restype = {"int": ctypes.c_int, "void": None, "int64_t": ctypes.c_int64,
+                      "double": ctypes.c_double, "float": ctypes.c_float}[ret]
+        fn.argtypes = [_CTYPE[a] for a in args]
+    _LIB, _PROTOS = lib, protos
+    return lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hip error {rc}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def dcode(t: torch.Tensor) -> int:
+    try:
+        return DTYPE_CODE[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}; the gfx950 kernels take float32 or bfloat16")
+
+
+def require_gpu(*tensors) -> None:
+    """Fail loudly: the product path has no CPU fallback."""
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "recommendations_amd ops run only on an MI355X (gfx950) device; got a CPU tensor. "
+                "The CPU restatement lives in oracle/ and is test infrastructure only.")
+        if not t.is_contiguous():
+            raise RuntimeError("recommendations_amd ops require contiguous tensors")

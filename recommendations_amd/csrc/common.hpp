@@ -1,0 +1,175 @@
+// Shared device helpers for the LTHM gfx950 kernels.
+//
+// Everything here is written for CDNA4 (wave64, MFMA, 160 KiB LDS); there is no
+// dual-platform path.  bf16 values travel as raw uint16_t so that every load and
+// store is an explicit, vectorisable integer access (cdna_hip_programming.md G13).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lthm.h"
+
+#define LTHM_WAVE 64
+
+namespace lthm {
+
+typedef uint16_t bf16_t;
+
+// ---- bf16 <-> f32 (round-to-nearest-even, NaN stays NaN; identical to torch) ----
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// generic element load/store as f32
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  __device__ __forceinline__ static float ld(const float* p) { return *p; }
+  __device__ __forceinline__ static void st(float* p, float v) { *p = v; }
+};
+template <> struct Elem<bf16_t> {
+  __device__ __forceinline__ static float ld(const bf16_t* p) { return bf2f(*p); }
+  __device__ __forceinline__ static void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+
+// 16-byte vector of T (4 x f32 or 8 x bf16)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Load VB bytes (4/8/16) starting at p as f32 values into out[0..VB/sizeof(T))
+template <typename T, int VB>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, float* out) {
+  constexpr int N = VB / (int)sizeof(T);
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (VB == 16) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(p);
+      out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+    } else if constexpr (VB == 8) {
+      float2 v = *reinterpret_cast<const float2*>(p);
+      out[0] = v.x; out[1] = v.y;
+    } else {
+      out[0] = *reinterpret_cast<const float*>(p);
+    }
+  } else {
+    if constexpr (VB == 16) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        out[2 * i] = __uint_as_float(v[i] << 16);
+        out[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+      }
+    } else if constexpr (VB == 8) {
+      u32x2 v = *reinterpret_cast<const u32x2*>(p);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        out[2 * i] = __uint_as_float(v[i] << 16);
+        out[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+      }
+    } else {
+      uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+      out[0] = __uint_as_float(v << 16);
+      out[1] = __uint_as_float(v & 0xffff0000u);
+    }
+  }
+  (void)N;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (N == 4) {
+      *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    } else if constexpr (N == 2) {
+      *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) p[i] = v[i];
+    }
+  } else {
+    if constexpr (N == 8) {
+      u32x4 w;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+      *reinterpret_cast<u32x4*>(p) = w;
+    } else if constexpr (N == 4) {
+      u32x2 w;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+      *reinterpret_cast<u32x2*>(p) = w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) p[i] = f2bf(v[i]);
+    }
+  }
+}
+
+// ---- wave reductions (64 lanes) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reduce inside aligned groups of G lanes (G power of two <= 64)
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---- KShift row index, bit-identical to commons/layers.py:174-185 ----
+// c == 0: x mod P ; c >= 1: ((x << c) | (x >> (64 - c))) mod P with a wrapping
+// left shift, an ARITHMETIC right shift on signed int64 and Python-style
+// (non-negative) remainder (torch.remainder).
+__device__ __host__ __forceinline__ int64_t kshift_row(int64_t x, int c, int64_t P) {
+  int64_t y = x;
+  if (c != 0) {
+    uint64_t ux = (uint64_t)x;
+    uint64_t hi = ux << c;
+    uint64_t lo = (uint64_t)(x >> (64 - c));  // arithmetic shift: sign fill
+    y = (int64_t)(hi | lo);
+  }
+  int64_t r = y % P;
+  if (r < 0) r += P;
+  return r;
+}
+
+// Python-style floor division + remainder for int64 (PatternFromTimelocal, QR)
+__device__ __host__ __forceinline__ int64_t floordiv64(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+__device__ __host__ __forceinline__ int64_t pymod64(int64_t a, int64_t b) {
+  int64_t r = a % b;
+  if (r != 0 && ((r < 0) != (b < 0))) r += b;
+  return r;
+}
+
+__host__ __forceinline__ int grid_for(int64_t work, int per_block, int cap = 256 * 16) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace lthm
+
+#define LTHM_CHECK_LAUNCH() \
+  do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
+#define LTHM_REQUIRE(cond) \
+  do { if (!(cond)) return (int)hipErrorInvalidValue; } while (0)

@@ -1,0 +1,366 @@
+// KShift / Flat embedding gather+pool (forward) and LDS-dedup segmented
+// backward for gfx950.
+//
+// Reference semantics: commons/layers.py:125-185 (KShiftEmbedding),
+// commons/layers.py:44-61 (FlatEmbedding = K 1, mode NONE / NORMALIZE).
+//
+// Forward layout: one item (id, feature) is served by a group of LPR lanes;
+// lane j of the group owns bytes [j*VB, (j+1)*VB) of every table row, so each
+// of the K row reads is one fully coalesced 16-byte-per-lane access.  The K row
+// indices of an item are computed once (spread over the group's lanes) and
+// staged in LDS, so the 64-bit remainder is not repeated per lane.
+#include "common.hpp"
+
+namespace lthm {
+
+constexpr int KS_BLOCK = 256;
+constexpr int KS_ROWS_LDS = 1024;  // int64 row slots per wave
+
+__global__ __launch_bounds__(256) void kshift_rows_k(const int64_t* __restrict__ ids, int64_t n,
+                                                     int64_t P, int K, int64_t* __restrict__ rows) {
+  int64_t total = n * K;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t i = t / K;
+    int c = (int)(t - i * K);
+    rows[t] = kshift_row(ids[i], c, P);
+  }
+}
+
+template <typename TW, typename TO, int VB>
+__global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
+    const int64_t* __restrict__ ids, int64_t n_items, int F, const TW* __restrict__ W, int64_t P,
+    int D, int K, int mode, float scale, TO* __restrict__ out, float* __restrict__ norms, int LPR_LOG2) {
+  constexpr int NE = VB / (int)sizeof(TW);  // elements per lane
+  __shared__ int64_t rows_lds[KS_BLOCK / 64][KS_ROWS_LDS];
+  const int LPR = 1 << LPR_LOG2;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gl = lane & (LPR - 1);        // lane inside group
+  const int gi = lane >> LPR_LOG2;        // group (item) inside wave
+  const int IPW = 64 >> LPR_LOG2;         // items per wave
+  const int IPB = IPW * (KS_BLOCK / 64);  // items per block iteration
+
+  for (int64_t base = (int64_t)blockIdx.x * IPB; base < n_items; base += (int64_t)gridDim.x * IPB) {
+    const int64_t item = base + wave * IPW + gi;
+    const bool valid = item < n_items;
+    int64_t id = 0, rbase = 0;
+    if (valid) {
+      id = ids[item];
+      rbase = (F > 1) ? (int64_t)(item % F) * P : 0;
+    }
+    // rows for this item, spread over the group's lanes
+    for (int c = gl; c < K; c += LPR) rows_lds[wave][gi * K + c] = valid ? rbase + kshift_row(id, c, P) : 0;
+    __syncthreads();
+    float acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.f;
+    if (valid) {
+      const TW* colp = W + (size_t)gl * NE;
+      int c = 0;
+      // issue 4 row loads ahead, then add in order c = 0..K-1 (bit-exact order)
+      for (; c + 4 <= K; c += 4) {
+        float v0[NE], v1[NE], v2[NE], v3[NE];
+        const int64_t r0 = rows_lds[wave][gi * K + c], r1 = rows_lds[wave][gi * K + c + 1];
+        const int64_t r2 = rows_lds[wave][gi * K + c + 2], r3 = rows_lds[wave][gi * K + c + 3];
+        load_vec<TW, VB>(colp + r0 * D, v0);
+        load_vec<TW, VB>(colp + r1 * D, v1);
+        load_vec<TW, VB>(colp + r2 * D, v2);
+        load_vec<TW, VB>(colp + r3 * D, v3);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] = (c == 0) ? v0[e] : acc[e] + v0[e];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] += v1[e];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] += v2[e];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] += v3[e];
+      }
+      for (; c < K; ++c) {
+        float v0[NE];
+        load_vec<TW, VB>(colp + rows_lds[wave][gi * K + c] * D, v0);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] = (c == 0) ? v0[e] : acc[e] + v0[e];
+      }
+    }
+    if (mode == LTHM_KSHIFT_NORMALIZE) {
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) ss += acc[e] * acc[e];
+      for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float nrm = sqrtf(ss);
+      const float den = fmaxf(nrm, 1e-12f);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / den;
+      if (valid && norms != nullptr && gl == 0) norms[item] = nrm;
+    } else if (mode == LTHM_KSHIFT_SCALE) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / scale;
+    }
+    if (valid) store_vec<TO, NE>(out + item * D + (size_t)gl * NE, acc);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward: LDS-staged dedup + wave-segmented reduction + one f32 add per
+// unique row per workgroup.
+// ---------------------------------------------------------------------------
+constexpr int KB_NP = 2048;            // max (row, item) pairs per workgroup
+constexpr int KB_G_FLOATS = 16384;     // LDS budget for per-item gradients (64 KiB)
+
+template <typename TY, typename TO>
+__global__ __launch_bounds__(256) void kshift_bwd_dense_k(
+    const int64_t* __restrict__ ids, int64_t n_items, int F, const TY* __restrict__ dY,
+    const TO* __restrict__ out, const float* __restrict__ norms, int64_t P, int D, int K, int mode,
+    float scale, int CH, int NP2, float* __restrict__ dW) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);                   // NP2
+  float* g = reinterpret_cast<float*>(smem + (size_t)KB_NP * 8);        // CH * D
+  int* segs = reinterpret_cast<int*>(smem + (size_t)KB_NP * 8 + (size_t)KB_G_FLOATS * 4);  // NP2+1
+  __shared__ int s_nseg;
+  __shared__ int s_wsum[4];
+
+  const int tid = threadIdx.x;
+  for (int64_t base = (int64_t)blockIdx.x * CH; base < n_items; base += (int64_t)gridDim.x * CH) {
+    const int nit = (int)min((int64_t)CH, n_items - base);
+    // 1) per-item input gradient g = d(out)/d(sum) applied to dY
+    for (int t = tid; t < nit * D; t += 256) {
+      const int it = t / D;
+      const int d = t - it * D;
+      float dy = Elem<TY>::ld(dY + (base + it) * D + d);
+      float v;
+      if (mode == LTHM_KSHIFT_SCALE) v = dy / scale;
+      else v = dy;
+      g[it * D + d] = v;
+    }
+    __syncthreads();
+    if (mode == LTHM_KSHIFT_NORMALIZE) {
+      // g = (dy - y (y . dy)) / max(|x|, eps)  (eps branch: dy / eps)
+      const int wave = tid >> 6, lane = tid & 63;
+      for (int it = wave; it < nit; it += 4) {
+        float dot = 0.f;
+        for (int d = lane; d < D; d += 64) dot += Elem<TO>::ld(out + (base + it) * D + d) * g[it * D + d];
+        dot = wave_sum(dot);
+        const float nrm = norms[base + it];
+        for (int d = lane; d < D; d += 64) {
+          const float dy = g[it * D + d];
+          g[it * D + d] = (nrm > 1e-12f) ? (dy - Elem<TO>::ld(out + (base + it) * D + d) * dot) / nrm
+                                         : dy / 1e-12f;
+        }
+      }
+    }
+    // 2) (row, pair) keys
+    const int np = nit * K;
+    for (int p = tid; p < NP2; p += 256) {
+      uint64_t key = ~0ull;
+      if (p < np) {
+        const int it = p / K;
+        const int c = p - it * K;
+        const int64_t item = base + it;
+        const int64_t row = ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], c, P);
+        key = ((uint64_t)row << 12) | (uint64_t)p;
+      }
+      keys[p] = key;
+    }
+    __syncthreads();
+    // 3) bitonic sort of NP2 keys in LDS
+    for (int k = 2; k <= NP2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = tid; t < NP2 / 2; t += 256) {
+          const int i0 = 2 * t - (t & (j - 1));
+          const int i1 = i0 + j;
+          const bool up = ((i0 & k) == 0);
+          uint64_t a = keys[i0], b = keys[i1];
+          if ((a > b) == up) { keys[i0] = b; keys[i1] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    // 4) segment heads -> compact segment starts (block exclusive scan)
+    const int PER = NP2 / 256;  // NP2 >= 256 guaranteed by host
+    int flags[KB_NP / 256];
+    int cnt = 0;
+    for (int q = 0; q < PER; ++q) {
+      const int p = tid * PER + q;
+      int h = 0;
+      if (p < np) h = (p == 0) || ((keys[p] >> 12) != (keys[p - 1] >> 12));
+      flags[q] = h;
+      cnt += h;
+    }
+    // wave inclusive scan of cnt
+    const int lane = tid & 63, wave = tid >> 6;
+    int incl = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+      int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wave; ++w) woff += s_wsum[w];
+    if (tid == 255) s_nseg = woff + incl;
+    int pos = woff + incl - cnt;
+    for (int q = 0; q < PER; ++q) {
+      if (flags[q]) segs[pos++] = tid * PER + q;
+    }
+    __syncthreads();
+    const int nseg = s_nseg;
+    if (tid == 0) segs[nseg] = np;
+    __syncthreads();
+    // 5) one group of lanes per segment: ordered sum, then one f32 add per column
+    const int LPR = (D >= 64) ? 64 : D;    // lanes per segment (1 float each per pass)
+    const int gpw = 64 / LPR;
+    const int grp = (tid >> 6) * gpw + (lane / LPR);
+    const int ngrp = 4 * gpw;
+    const int gl = lane % LPR;
+    for (int s = grp; s < nseg; s += ngrp) {
+      const int s0 = segs[s], s1 = segs[s + 1];
+      const int64_t row = (int64_t)(keys[s0] >> 12);
+      for (int d = gl; d < D; d += LPR) {
+        float acc = 0.f;
+        for (int p = s0; p < s1; ++p) {
+          const int it = (int)(keys[p] & 0xfff) / K;
+          acc += g[it * D + d];
+        }
+        atomicAdd(dW + row * D + d, acc);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static int pick_vb(int D, int esz, int* lpr_log2) {
+  const int bytes = D * esz;
+  int vb = 16;
+  while (vb > esz && (bytes % vb != 0)) vb >>= 1;
+  while (bytes / vb > 64) return -1;
+  const int lpr = bytes / vb;
+  if (lpr & (lpr - 1)) return -1;
+  int l2 = 0;
+  while ((1 << l2) < lpr) ++l2;
+  *lpr_log2 = l2;
+  return vb;
+}
+
+template <typename TW, typename TO>
+static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W, int64_t P, int D, int K,
+                      int mode, void* out, float* norms, hipStream_t s) {
+  int l2 = 0;
+  const int vb = pick_vb(D, (int)sizeof(TW), &l2);
+  LTHM_REQUIRE(vb > 0);
+  // TO vector width must divide: elements per lane NE = vb / sizeof(TW)
+  const int ipw = 64 >> l2;
+  LTHM_REQUIRE(ipw * K <= KS_ROWS_LDS);
+  const int ipb = ipw * (KS_BLOCK / 64);
+  const int grid = grid_for(n_items, ipb, 256 * 32);
+  const float scale = (float)__builtin_sqrt((double)K);
+  if (vb == 16)
+    hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 16>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+  else if (vb == 8)
+    hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 8>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+  else if (vb == 4)
+    hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 4>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+  else
+    return (int)hipErrorInvalidValue;
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename TY, typename TO>
+static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY, const void* out,
+                      const float* norms, int64_t P, int D, int K, int mode, float* dW, hipStream_t s) {
+  int ch = KB_NP / K;
+  if (ch * D > KB_G_FLOATS) ch = KB_G_FLOATS / D;
+  LTHM_REQUIRE(ch >= 1);
+  int np2 = 256;
+  while (np2 < ch * K) np2 <<= 1;
+  const float scale = (float)__builtin_sqrt((double)K);
+  const size_t shmem = (size_t)KB_NP * 8 + (size_t)KB_G_FLOATS * 4 + (size_t)(KB_NP + 1) * 4;
+  const int grid = grid_for(n_items, ch, 256 * 8);
+  hipLaunchKernelGGL((kshift_bwd_dense_k<TY, TO>), dim3(grid), dim3(256), shmem, s, ids, n_items, F,
+                     (const TY*)dY, (const TO*)out, norms, P, D, K, mode, scale, ch, np2, dW);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace lthm
+
+using namespace lthm;
+
+extern "C" {
+
+int lthm_abi_version(void) { return 1; }
+
+int lthm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int lthm_kshift_rows(const int64_t* ids, int64_t n, int64_t P, int32_t K, int64_t* rows, void* stream) {
+  LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && n >= 0);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(kshift_rows_k, dim3(grid_for(n * K, 256)), dim3(256), 0, (hipStream_t)stream, ids, n,
+                     P, K, rows);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+static int kshift_fwd_impl(const int64_t* ids, int64_t n_items, int F, const void* W, int w_dtype, int64_t P,
+                           int D, int K, int mode, void* out, int out_dtype, float* norms, void* stream) {
+  LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n_items >= 0 && F >= 1);
+  LTHM_REQUIRE(mode >= 0 && mode <= 2);
+  if (n_items == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (w_dtype == LTHM_F32 && out_dtype == LTHM_F32)
+    return launch_fwd<float, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+  if (w_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
+    return launch_fwd<float, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+  if (w_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
+    return launch_fwd<bf16_t, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+  if (w_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
+    return launch_fwd<bf16_t, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+  return (int)hipErrorInvalidValue;
+}
+
+int lthm_kshift_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtype, int64_t P, int64_t row_base,
+                    int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, float* norms, void* stream) {
+  const void* Wb = W;
+  if (row_base != 0) {
+    const size_t esz = (w_dtype == LTHM_F32) ? 4 : 2;
+    Wb = (const void*)((const char*)W + (size_t)row_base * D * esz);
+  }
+  return kshift_fwd_impl(ids, n, 1, Wb, w_dtype, P, D, K, mode, out, out_dtype, norms, stream);
+}
+
+int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* W, int32_t w_dtype, int64_t P,
+                          int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, float* norms,
+                          void* stream) {
+  return kshift_fwd_impl(ids, n * (int64_t)F, F, W, w_dtype, P, D, K, mode, out, out_dtype, norms, stream);
+}
+
+int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                          const void* out, int32_t out_dtype, const float* norms, int64_t P, int32_t D, int32_t K,
+                          int32_t mode, float* dW, void* stream) {
+  LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n >= 0 && F >= 1);
+  LTHM_REQUIRE(mode >= 0 && mode <= 2);
+  LTHM_REQUIRE(mode != LTHM_KSHIFT_NORMALIZE || (out != nullptr && norms != nullptr));
+  const int64_t items = n * (int64_t)F;
+  if (items == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (dy_dtype == LTHM_F32 && out_dtype == LTHM_F32)
+    return launch_bwd<float, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+  if (dy_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
+    return launch_bwd<bf16_t, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+  if (dy_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
+    return launch_bwd<float, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+  if (dy_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
+    return launch_bwd<bf16_t, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+  return (int)hipErrorInvalidValue;
+}
+
+}  // extern "C"
