@@ -34,7 +34,7 @@ def clib():
         lib.oracle_kshift_row.argtypes = [i64, i32, i64]
         lib.oracle_kshift_rows.argtypes = [vp, i64, i64, i32, vp]
         lib.oracle_kshift_fwd_f32.argtypes = [vp, i64, vp, i64, i32, i32, i32, vp]
-        lib.oracle_kshift_bwd_f32.argtypes = [vp, i64, vp, i64, i32, i32, i32, vp]
+        lib.oracle_kshift_bwd_f64.argtypes = [vp, i64, vp, i64, i32, i32, i32, vp]
         _CLIB = lib
     return _CLIB
 
@@ -63,9 +63,9 @@ def kshift_bwd_c(ids: np.ndarray, dY: np.ndarray, P: int, K: int, mode: int) -> 
     ids = np.ascontiguousarray(ids.reshape(-1), dtype=np.int64)
     D = dY.shape[-1]
     dY = np.ascontiguousarray(dY.reshape(-1, D), dtype=np.float32)
-    dW = np.zeros((P, D), dtype=np.float32)
-    clib().oracle_kshift_bwd_f32(ids.ctypes.data, ids.size, dY.ctypes.data, P, D, K, mode, dW.ctypes.data)
-    return dW
+    acc = np.zeros((P, D), dtype=np.float64)
+    clib().oracle_kshift_bwd_f64(ids.ctypes.data, ids.size, dY.ctypes.data, P, D, K, mode, acc.ctypes.data)
+    return acc.astype(np.float32)
 
 
 def kshift_row_idx_torch(x: torch.Tensor, c: int, P: int) -> torch.Tensor:

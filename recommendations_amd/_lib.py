@@ -71,6 +71,30 @@ def parse_header(path: str = HEADER) -> Dict[str, Tuple[str, List[str]]]:
     return protos
 
 
+def parse_structs(path: str = HEADER) -> Dict[str, type]:
+    """ctypes.Structure classes for every `typedef struct name {...} name;` in lthm.h."""
+    with open(path) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"typedef\s+struct\s+(\w+)\s*\{(.*?)\}\s*(\w+)\s*;", text, flags=re.S):
+        fields = []
+        for line in m.group(2).split(";"):
+            line = " ".join(line.replace("const ", "").split())
+            if not line:
+                continue
+            typ, name = line.rsplit(" ", 1)
+            stars = name.count("*") + typ.count("*")
+            typ, name = typ.replace("*", "").strip(), name.replace("*", "")
+            fields.append((name, _CTYPE[typ + "*" * stars]))
+        out[m.group(3)] = type(m.group(3), (ctypes.Structure,), {"_fields_": fields})
+    return out
+
+
+STRUCTS = parse_structs()
+for _n in STRUCTS:
+    _CTYPE[_n + "*"] = ctypes.c_void_p
+
 _LIB = None
 _PROTOS: Dict[str, Tuple[str, List[str]]] = {}
 

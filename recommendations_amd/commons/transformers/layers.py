@@ -1,0 +1,249 @@
+"""Sequence-encoder layers — drop-in for commons/transformers/layers.py.
+
+Module names and parameter names match the reference (``ln_1.weight``,
+``attn.c_attn.weight``, ``attn.attn.pos_bias.bias``, ``mlp.c_fc.weight`` ...), so
+state_dicts interchange.  The TransformerBlock hot path is one fused autograd op
+(``TransformerBlockFn``) whose forward and backward are a fixed sequence of
+gfx950 kernels: LayerNorm, MFMA GEMMs with fused bias/GELU/residual epilogues,
+and the LDS-resident attention with the in-kernel relative-position bias.
+
+Reference behaviour reproduced "as executed" (SURVEY.md §3.5 #15): the FFN
+hidden size is 4*d whatever ``rotator_config.ff_mult`` says, and
+``SelfAttention.from_config`` always builds multi-head attention.  Activations
+are bf16 (GEMM operands), the residual stream and all accumulations fp32.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ... import kernels as K
+from ..._lib import require_gpu
+
+
+def _bf(w):
+    return None if w is None else K.cast(w.detach().contiguous(), torch.bfloat16)
+
+
+def _f(b):
+    return None if b is None else b.detach().contiguous()
+
+
+class TransformerBlockFn(torch.autograd.Function):
+    """x -> x + attn(ln_1 x) -> + mlp(ln_2 .)  [+ x again when double_residual]."""
+
+    @staticmethod
+    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal, double_residual):
+        require_gpu(x)
+        B, T, d = x.shape
+        E = d // H
+        M = B * T
+        x2 = x.contiguous().view(M, d)
+        wqkv_b, wp_b, w1_b, w2_b = _bf(wqkv), _bf(wp), _bf(w1), _bf(w2)
+        h1, mu1, rs1 = K.layernorm_fwd(x2, ln1w.detach(), _f(ln1b))
+        qkv = K.linear_fwd(h1, wqkv_b, _f(bqkv))
+        tab = None if table is None else table.detach().contiguous()
+        o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
+        x1 = K.linear_fwd(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
+        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+        pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
+        g = K.linear_fwd(h2, w1_b, _f(b1), act=K.ACT_GELU, aux_out=pre)
+        out = K.linear_fwd(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
+        ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
+                              wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
+        ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
+                   b1 is not None, b2 is not None, None if table is None else table.shape)
+        return out.view(B, T, d)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g, wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w,
+         tab) = ctx.saved_tensors
+        B, T, d, H, E, causal, dbl, has_ln1b, has_bqkv, has_bp, has_b1, has_b2, tshape = ctx.cfg
+        M = B * T
+        dy = dout.contiguous().view(M, d)
+        if dy.dtype != torch.float32:
+            dy = dy.float()
+        dyb = K.cast(dy, torch.bfloat16)
+        # MLP half
+        dw2 = K.linear_wgrad(dyb, g)
+        db2 = K.colsum(dy) if has_b2 else None
+        dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_GELU_GRAD, aux=pre)
+        dw1 = K.linear_wgrad(dpre, h2)
+        db1 = K.colsum(dpre) if has_b1 else None
+        dh2 = K.linear_dgrad(dpre, w1_b)
+        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy)
+        # attention half
+        dwp = K.linear_wgrad(dx1b, o)
+        dbp = K.colsum(dx1) if has_bp else None
+        do = K.linear_dgrad(dx1b, wp_b)
+        dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+        dwqkv = K.linear_wgrad(dqkv, h1)
+        dbqkv = K.colsum(dqkv) if has_bqkv else None
+        dh1 = K.linear_dgrad(dqkv, wqkv_b)
+        dx, _, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1, res2=dy if dbl else None,
+                                              want_bf16=False)
+        dtable = None
+        if tshape is not None:
+            dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
+            dtable[: dtab.shape[0]] = dtab
+        return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
+                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None)
+
+
+# ------------------------------------------------------------------ modules
+class RelativePositionBias(nn.Module):
+    """commons/transformers/layers.py:13-35 (table [nq + nk + 1, nh], row q - k + nk)."""
+
+    def __init__(self, nq: int, nk: int, nh: int):
+        super().__init__()
+        self.nq, self.nk, self.nh = nq, nk, nh
+        self.bias = nn.Parameter(torch.zeros((nq + nk + 1, nh)))
+
+    def check(self, nq: int, nk: int):
+        if not (nq <= self.nq):
+            raise RuntimeError("nq > self.nq")
+        if not (nk <= self.nk):
+            raise RuntimeError("nk > self.nk")
+
+
+class ScaledDotProductAttention(nn.Module):
+    """commons/transformers/layers.py:41-61; the scores are never materialised."""
+
+    def __init__(self, nq: int, nk: int, nh: int, relative_bias: bool = False):
+        super().__init__()
+        self.pos_bias = RelativePositionBias(nq, nk, nh) if relative_bias else nn.Identity()
+
+    @property
+    def table(self) -> Optional[torch.Tensor]:
+        return self.pos_bias.bias if isinstance(self.pos_bias, RelativePositionBias) else None
+
+
+class LayerNorm(nn.Module):
+    """commons/transformers/layers.py:142-149."""
+
+    def __init__(self, ndim: int, bias: bool = True):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(ndim))
+        self.bias = nn.Parameter(torch.zeros(ndim)) if bias else None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return LayerNormFn.apply(x, self.weight, self.bias)
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        require_gpu(x)
+        shp = x.shape
+        x2 = x.contiguous().view(-1, shp[-1]).float()
+        y, mu, rs = K.layernorm_fwd(x2, w.detach(), _f(b), y_dtype=torch.float32)
+        ctx.save_for_backward(x2, w, mu, rs)
+        ctx.has_b, ctx.shp = b is not None, shp
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mu, rs = ctx.saved_tensors
+        dx, _, dw, db = K.layernorm_bwd(dy.contiguous().view(x2.shape).float(), x2, w.detach(), mu, rs,
+                                        want_bf16=False, need_bias=ctx.has_b)
+        return dx.view(ctx.shp), dw, db
+
+
+class SelfAttentionConfig:
+    """Lightweight attribute config (commons/transformers/layers.py:165-174)."""
+
+    def __init__(self, n_embd: int, n_head: int, attn_dropout: float, dropout: float, bias: bool, pos_bias=None):
+        self.n_embd, self.n_head = n_embd, n_head
+        self.attn_dropout, self.dropout, self.bias, self.pos_bias = attn_dropout, dropout, bias, pos_bias
+
+
+class SelfAttention(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        assert config.n_embd % config.n_head == 0
+        self.config = config
+        if config.pos_bias is None:
+            self.attn = ScaledDotProductAttention(0, 0, 0, relative_bias=False)
+        else:
+            cw = config.pos_bias.context_window
+            self.attn = ScaledDotProductAttention(nq=cw, nk=cw, nh=config.n_head, relative_bias=True)
+
+    @classmethod
+    def from_config(cls, config):
+        # as executed by the reference (:195-199): always multi-head
+        return MultiHeadAttention(config)
+
+
+class MultiHeadAttention(SelfAttention):
+    """commons/transformers/layers.py:237-265."""
+
+    def __init__(self, config):
+        super().__init__(config)
+        self.c_attn = nn.Linear(config.n_embd, 3 * config.n_embd, bias=config.bias)
+        self.c_proj = nn.Linear(config.n_embd, config.n_embd, bias=config.bias)
+        self.attn_dropout = nn.Dropout(config.attn_dropout)
+        self.resid_dropout = nn.Dropout(config.dropout)
+        self.n_head = config.n_head
+        self.n_embd = config.n_embd
+
+
+class _MLP(nn.Module):
+    """commons/transformers/layers.py:271-284."""
+
+    def __init__(self, n_embd: int, bias: bool, dropout: float, hidden_mult: int):
+        super().__init__()
+        self.c_fc = nn.Linear(n_embd, int(hidden_mult * n_embd), bias=bias)
+        self.gelu = nn.GELU(approximate="tanh")
+        self.c_proj = nn.Linear(int(hidden_mult * n_embd), n_embd, bias=bias)
+        self.dropout = nn.Dropout(dropout)
+
+
+class TransformerBlock(nn.Module):
+    """commons/transformers/layers.py:323-420 (dense path)."""
+
+    def __init__(self, config: Any, seed: Optional[int] = None, n_cls: int = 0):
+        super().__init__()
+        self.is_causal = config.is_causal
+        attn_cfg = config.attn_config
+        self.ln_1 = LayerNorm(attn_cfg.n_embd, bias=attn_cfg.bias)
+        self.attn = SelfAttention.from_config(attn_cfg)
+        self.ln_2 = LayerNorm(attn_cfg.n_embd, bias=attn_cfg.bias)
+        if isinstance(config.rotator_config, dict) and "moe" in config.rotator_config:
+            raise NotImplementedError("MoE feed-forward: use MoELinear directly (SURVEY a14)")
+        hidden_mult = config.rotator_config if isinstance(config.rotator_config, (int, float)) else 4
+        self.mlp = _MLP(attn_cfg.n_embd, attn_cfg.bias, attn_cfg.dropout, hidden_mult)
+        self.is_sparse = getattr(config, "is_sparse_attn", False)
+        if self.is_sparse:
+            raise NotImplementedError("is_sparse_attn is disabled in every north-star config")
+        self.enable_gradient_checkpointing = getattr(config, "enable_gradient_checkpointing", False)
+        self.null_connector = nn.Identity()
+        self.register_buffer("input_mask_idx", torch.empty(0, dtype=torch.long), persistent=True)
+        self.register_buffer("input_mask_not_idx", torch.empty(0, dtype=torch.long), persistent=True)
+
+    def _args(self):
+        a, m = self.attn, self.mlp
+        return (self.ln_1.weight, self.ln_1.bias, a.c_attn.weight, a.c_attn.bias, a.c_proj.weight, a.c_proj.bias,
+                a.attn.table, self.ln_2.weight, self.ln_2.bias, m.c_fc.weight, m.c_fc.bias, m.c_proj.weight,
+                m.c_proj.bias)
+
+    def _fused(self, x, double_residual: bool):
+        if x.dim() != 3:
+            raise ValueError("TransformerBlock expects [B, T, d]")
+        if self.attn.attn.table is not None:
+            self.attn.attn.pos_bias.check(x.shape[1], x.shape[1])
+        return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal, double_residual)
+
+    def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if attn_mask is not None:
+            raise NotImplementedError("additive attn_mask: only the causal mask is fused in the kernel")
+        # Activation checkpointing is unnecessary at 288 GB HBM: the fused op keeps
+        # its bf16 activations, and recompute would give the same numbers.
+        return self._fused(x, False)
+
+    def forward_double_residual(self, x: torch.Tensor) -> torch.Tensor:
+        """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137)."""
+        return self._fused(x, True)

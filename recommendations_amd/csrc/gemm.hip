@@ -1,0 +1,305 @@
+// bf16 MFMA GEMM with fused epilogues for gfx950 (v_mfma_f32_16x16x32_bf16).
+//
+//   C[b] = epi( alpha * A[b] . B[b] )      fp32 accumulation
+//
+// Each operand is either K-CONTIGUOUS (A[m][k], B[n][k]: the Linear forward
+// Y = X W^T and dX = dY W^T layouts) or K-STRIDED (A[k][m], B[k][n]: the
+// weight-gradient dW = dY^T X layout).  K-strided tiles are staged into LDS
+// untransposed and fed to the MFMA with ds_read_b64_tr_b16 (gfx950 hardware
+// transpose read), so no operand is ever transposed in HBM.
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA
+// 16x16 tiles.  Register-staged double-buffered LDS (64 KiB), one barrier per
+// K-tile; XOR-swizzled LDS images (128-B rows for K-contiguous, the 256-B row
+// swizzle of cdna_hip_programming.md T10(b) for K-strided).
+//
+// Reference call sites served: every nn.Linear of commons/transformers/layers.py
+// (MultiHeadAttention.c_attn/c_proj :240-241, _MLP.c_fc/c_proj :274-276),
+// commons/layers.py:65-81 (MLP + QuickGELU), models/lthm/sequence/*.py Linears.
+#include "common.hpp"
+
+namespace lthm {
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  int64_t M, N, K;
+  int64_t lda, ldb, ldc;
+  int64_t sA, sB, sC;  // batch strides (elements)
+  int64_t k_per_split;
+  float alpha;
+  const float* bias;   // [N] f32 or null
+  int act;             // LTHM_ACT_*
+  const bf16_t* aux;   // pre-activation input for *_GRAD acts [M, ldaux]
+  bf16_t* aux_out;     // pre-activation store for GELU/QGELU [M, ldaux]
+  int64_t ldaux;
+  const void* res1;
+  const void* res2;
+  int64_t ldr1, ldr2;
+  int res1_dt, res2_dt;
+  int out_dt;
+  float* ws;           // split-K slabs [splits][M][N] f32 (when splits > 1)
+};
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float kb = 0.7978845608028654f, kk = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(kb * (x + kk * x * x * x)));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float kb = 0.7978845608028654f, kk = 0.044715f;
+  const float x2 = x * x;
+  const float t = tanhf(kb * (x + kk * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kb * (1.f + 3.f * kk * x2);
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float qgelu(float x) { return x * sigmoidf_(1.702f * x); }
+__device__ __forceinline__ float qgelu_grad(float x) {
+  const float s = sigmoidf_(1.702f * x);
+  return s + 1.702f * x * s * (1.f - s);
+}
+
+__device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
+  return dt == LTHM_F32 ? reinterpret_cast<const float*>(p)[i] : bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
+}
+
+__device__ __forceinline__ float epilogue(const GemmArgs& g, float v, int64_t row, int64_t col, int64_t b) {
+  if (g.bias) v += g.bias[col];
+  if (g.act == LTHM_ACT_GELU || g.act == LTHM_ACT_QGELU) {
+    if (g.aux_out) g.aux_out[b * g.M * g.ldaux + row * g.ldaux + col] = f2bf(v);
+    v = (g.act == LTHM_ACT_GELU) ? gelu_tanh(v) : qgelu(v);
+  } else if (g.act == LTHM_ACT_GELU_GRAD) {
+    v *= gelu_tanh_grad(bf2f(g.aux[b * g.M * g.ldaux + row * g.ldaux + col]));
+  } else if (g.act == LTHM_ACT_QGELU_GRAD) {
+    v *= qgelu_grad(bf2f(g.aux[b * g.M * g.ldaux + row * g.ldaux + col]));
+  }
+  if (g.res1) v += ld_any(g.res1, g.res1_dt, b * g.M * g.ldr1 + row * g.ldr1 + col);
+  if (g.res2) v += ld_any(g.res2, g.res2_dt, b * g.M * g.ldr2 + row * g.ldr2 + col);
+  return v;
+}
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, 16 KiB
+
+// byte offset in a K-contiguous image [128 rows][64 k] (128-B rows)
+__device__ __forceinline__ int kc_off(int r, int chunk) { return r * 128 + ((chunk ^ ((r >> 1) & 7)) << 4); }
+// byte offset in a K-strided image [64 k-rows][128] (256-B rows), T10(b) swizzle
+__device__ __forceinline__ int ks_off(int kr, int ch) {
+  return kr * 256 + ((ch ^ (((kr & 3) << 2) | ((kr >> 2) & 3))) << 4);
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t ld, int64_t rows, int64_t r0,
+                                          int64_t k, int64_t k1, int tid, u32x4 (&reg)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 256 * i;
+    int64_t gr, gk;
+    if constexpr (KCONTIG) {
+      gr = r0 + (idx >> 3);
+      gk = k + (idx & 7) * 8;
+    } else {
+      gk = k + (idx >> 4);
+      gr = r0 + (idx & 15) * 8;
+    }
+    if (gr < rows && gk < k1) {
+      const bf16_t* src = KCONTIG ? (P + gr * ld + gk) : (P + gk * ld + gr);
+      reg[i] = *reinterpret_cast<const u32x4*>(src);
+    } else {
+      reg[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void store_tile(unsigned char* lds, int tid, const u32x4 (&reg)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 256 * i;
+    const int off = KCONTIG ? kc_off(idx >> 3, idx & 7) : ks_off(idx >> 4, idx & 15);
+    *reinterpret_cast<u32x4*>(lds + off) = reg[i];
+  }
+}
+
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <bool KCONTIG>
+__device__ __forceinline__ bf16x8v read_frag(const unsigned char* lds, int rbase, int s, int lane) {
+  if constexpr (KCONTIG) {
+    const int r = rbase + (lane & 15);
+    const int chunk = s * 4 + (lane >> 4);
+    u32x4 v = *reinterpret_cast<const u32x4*>(lds + kc_off(r, chunk));
+    return __builtin_bit_cast(bf16x8v, v);
+  } else {
+    const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int kr = s * 32 + 8 * gq + q;
+    const int ch = (rbase >> 3) + (p >> 1);
+    const unsigned char* a0 = lds + ks_off(kr, ch) + 8 * (p & 1);
+    const unsigned char* a1 = lds + ks_off(kr + 4, ch) + 8 * (p & 1);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8v, v);
+  }
+}
+
+template <bool KA, bool KB>
+__global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs g, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tile = blockIdx.x;
+  const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
+  const int64_t b = blockIdx.y;
+  const int split = blockIdx.z;
+  const bf16_t* A = g.A + b * g.sA;
+  const bf16_t* B = g.B + b * g.sB;
+  const int64_t k0 = (int64_t)split * g.k_per_split;
+  const int64_t k1 = min(g.K, k0 + g.k_per_split);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  if (k0 < k1) {
+    load_tile<KA>(A, g.lda, g.M, m0, k0, k1, tid, ra);
+    load_tile<KB>(B, g.ldb, g.N, n0, k0, k1, tid, rb);
+    store_tile<KA>(smem, tid, ra);
+    store_tile<KB>(smem + TILE_BYTES, tid, rb);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t kt = k0; kt < k1; kt += BK) {
+    const bool has_next = kt + BK < k1;
+    if (has_next) {
+      load_tile<KA>(A, g.lda, g.M, m0, kt + BK, k1, tid, ra);
+      load_tile<KB>(B, g.ldb, g.N, n0, kt + BK, k1, tid, rb);
+    }
+    const unsigned char* sa = smem + cur * 2 * TILE_BYTES;
+    const unsigned char* sb = sa + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8v af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<KA>(sa, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<KB>(sb, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (has_next) {
+      unsigned char* nxt = smem + (cur ^ 1) * 2 * TILE_BYTES;
+      store_tile<KA>(nxt, tid, ra);
+      store_tile<KB>(nxt + TILE_BYTES, tid, rb);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue
+  const bool split_mode = g.ws != nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < g.M && col < g.N) {
+          float v = g.alpha * acc[i][j][r];
+          if (split_mode) {
+            g.ws[((int64_t)split * gridDim.y + b) * g.M * g.N + row * g.N + col] = v;
+          } else {
+            v = epilogue(g, v, row, col, b);
+            const int64_t o = b * g.sC + row * g.ldc + col;
+            if (g.out_dt == LTHM_F32) reinterpret_cast<float*>(g.C)[o] = v;
+            else reinterpret_cast<bf16_t*>(g.C)[o] = f2bf(v);
+          }
+        }
+      }
+    }
+  }
+}
+
+// split-K combine: C = epi(sum_s ws[s])
+__global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs g, int splits, int batch) {
+  const int64_t MN = g.M * g.N;
+  const int64_t total = MN * batch;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / MN;
+    const int64_t rc = t - b * MN;
+    const int64_t row = rc / g.N, col = rc - row * g.N;
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += g.ws[((int64_t)s * batch + b) * MN + rc];
+    v = epilogue(g, v, row, col, b);
+    const int64_t o = b * g.sC + row * g.ldc + col;
+    if (g.out_dt == LTHM_F32) reinterpret_cast<float*>(g.C)[o] = v;
+    else reinterpret_cast<bf16_t*>(g.C)[o] = f2bf(v);
+  }
+}
+
+}  // namespace lthm
+
+using namespace lthm;
+
+extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
+  LTHM_REQUIRE(d != nullptr);
+  LTHM_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 1);
+  LTHM_REQUIRE(d->out_dtype == LTHM_F32 || d->out_dtype == LTHM_BF16);
+  if (d->M == 0 || d->N == 0) return 0;
+  const bool ka = d->a_kcontig != 0, kb = d->b_kcontig != 0;
+  // 16-byte chunk alignment of every staged row
+  LTHM_REQUIRE(((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0);
+  LTHM_REQUIRE(d->lda % 8 == 0 && d->ldb % 8 == 0);
+  LTHM_REQUIRE(ka ? (d->K % 8 == 0) : (d->M % 8 == 0));
+  LTHM_REQUIRE(kb ? (d->K % 8 == 0) : (d->N % 8 == 0));
+  LTHM_REQUIRE(d->batch == 1 || (d->sA % 8 == 0 && d->sB % 8 == 0));
+  LTHM_REQUIRE(d->act >= 0 && d->act <= LTHM_ACT_QGELU_GRAD);
+  LTHM_REQUIRE(!(d->act == LTHM_ACT_GELU_GRAD || d->act == LTHM_ACT_QGELU_GRAD) || d->aux != nullptr);
+  int splits = d->splits < 1 ? 1 : d->splits;
+  LTHM_REQUIRE(splits == 1 || d->workspace != nullptr);
+  GemmArgs g;
+  g.A = (const bf16_t*)d->A; g.B = (const bf16_t*)d->B; g.C = d->C;
+  g.M = d->M; g.N = d->N; g.K = d->K;
+  g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
+  g.sA = d->sA; g.sB = d->sB; g.sC = d->sC;
+  int64_t kps = (d->K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  if (kps < BK) kps = BK;
+  splits = (int)((d->K + kps - 1) / kps);
+  if (splits < 1) splits = 1;
+  g.k_per_split = (splits == 1) ? (d->K > 0 ? d->K : 1) : kps;
+  g.alpha = d->alpha;
+  g.bias = d->bias; g.act = d->act; g.aux = (const bf16_t*)d->aux; g.aux_out = (bf16_t*)d->aux_out;
+  g.ldaux = d->ldaux > 0 ? d->ldaux : d->N;
+  g.res1 = d->res1; g.res2 = d->res2; g.ldr1 = d->ldr1 > 0 ? d->ldr1 : d->N; g.ldr2 = d->ldr2 > 0 ? d->ldr2 : d->N;
+  g.res1_dt = d->res1_dtype; g.res2_dt = d->res2_dtype; g.out_dt = d->out_dtype;
+  g.ws = (splits > 1) ? d->workspace : nullptr;
+  if (splits > 1) {
+    LTHM_REQUIRE(d->workspace_bytes >= (size_t)splits * d->batch * d->M * d->N * 4);
+  }
+  const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
+  dim3 grid(tiles_m * tiles_n, d->batch, splits);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t shmem = 4 * TILE_BYTES;
+  if (ka && kb) hipLaunchKernelGGL((gemm_k<true, true>), grid, dim3(256), shmem, s, g, tiles_n);
+  else if (ka && !kb) hipLaunchKernelGGL((gemm_k<true, false>), grid, dim3(256), shmem, s, g, tiles_n);
+  else if (!ka && kb) hipLaunchKernelGGL((gemm_k<false, true>), grid, dim3(256), shmem, s, g, tiles_n);
+  else hipLaunchKernelGGL((gemm_k<false, false>), grid, dim3(256), shmem, s, g, tiles_n);
+  LTHM_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int64_t total = d->M * d->N * d->batch;
+    hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, g, splits, d->batch);
+    LTHM_CHECK_LAUNCH();
+  }
+  return 0;
+}

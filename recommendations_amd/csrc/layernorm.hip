@@ -1,0 +1,185 @@
+// LayerNorm forward/backward (commons/transformers/layers.py:142-149, eps 1e-5).
+//
+// One wave per row, the row held in registers (D/64 values per lane, D <= 1024),
+// vectorised loads.  The forward writes y in bf16 (the GEMM operand) plus the
+// per-row mean / rstd; the backward fuses the residual-gradient sums of the
+// double-residual encoder (x + block(x), models/lthm/sequence/query_tower.py:
+// 132-137) and emits both the f32 residual gradient and its bf16 copy for the
+// next GEMM, plus per-block partial sums for dweight / dbias.
+#include "common.hpp"
+
+namespace lthm {
+
+template <int NPL, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_k(const float* __restrict__ x, int64_t M, int D, const float* __restrict__ w,
+                                                const float* __restrict__ b, TY* __restrict__ y, float* __restrict__ mean,
+                                                float* __restrict__ rstd, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = wave; r < M; r += nw) {
+    const float* xr = x + r * D;
+    float v[NPL];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = (c < D) ? xr[c] : 0.f;
+      s += v[i];
+    }
+    s = wave_sum(s);
+    const float mu = s / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + 64 * i;
+      const float d = (c < D) ? v[i] - mu : 0.f;
+      q += d * d;
+    }
+    q = wave_sum(q);
+    const float rs = 1.f / sqrtf(q / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        float o = (v[i] - mu) * rs * w[c];
+        if (b) o += b[c];
+        Elem<TY>::st(y + r * D + c, o);
+      }
+    }
+    if (lane == 0) {
+      mean[r] = mu;
+      rstd[r] = rs;
+    }
+  }
+}
+
+template <int NPL, typename TDY>
+__global__ __launch_bounds__(256) void ln_bwd_k(const TDY* __restrict__ dy, const float* __restrict__ x, int64_t M, int D,
+                                                const float* __restrict__ w, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, const float* __restrict__ res1,
+                                                const float* __restrict__ res2, float* __restrict__ dx,
+                                                bf16_t* __restrict__ dx_bf16, float* __restrict__ dw_part,
+                                                float* __restrict__ db_part) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t wave = blockIdx.x * 4 + wv;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float dwa[NPL], dba[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { dwa[i] = 0.f; dba[i] = 0.f; }
+  for (int64_t r = wave; r < M; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float g[NPL], xh[NPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float d = Elem<TDY>::ld(dy + r * D + c);
+        xh[i] = (x[r * D + c] - mu) * rs;
+        g[i] = d * w[c];
+        dwa[i] += d * xh[i];
+        dba[i] += d;
+      } else {
+        xh[i] = 0.f;
+        g[i] = 0.f;
+      }
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        float o = rs * (g[i] - s1 - xh[i] * s2);
+        if (res1) o += res1[r * D + c];
+        if (res2) o += res2[r * D + c];
+        dx[r * D + c] = o;
+        if (dx_bf16) dx_bf16[r * D + c] = f2bf(o);
+      }
+    }
+  }
+  // block partials for dweight / dbias
+  __shared__ float red[4][1024];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) red[wv][c] = dwa[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) dw_part[(int64_t)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) red[wv][c] = dba[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) db_part[(int64_t)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+template <int NPL>
+static int ln_fwd_launch(const float* x, int64_t M, int D, const float* w, const float* b, void* y, int ydt, float* mean,
+                         float* rstd, hipStream_t s) {
+  const int grid = grid_for(M, 4, 256 * 8);
+  if (ydt == LTHM_BF16)
+    hipLaunchKernelGGL((ln_fwd_k<NPL, bf16_t>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (bf16_t*)y, mean, rstd, 1e-5f);
+  else
+    hipLaunchKernelGGL((ln_fwd_k<NPL, float>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (float*)y, mean, rstd, 1e-5f);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int NPL>
+static int ln_bwd_launch(const void* dy, int dydt, const float* x, int64_t M, int D, const float* w, const float* mean,
+                         const float* rstd, const float* res1, const float* res2, float* dx, bf16_t* dxb, float* part,
+                         int nblk, hipStream_t s) {
+  float* dwp = part;
+  float* dbp = part + (int64_t)nblk * D;
+  if (dydt == LTHM_BF16)
+    hipLaunchKernelGGL((ln_bwd_k<NPL, bf16_t>), dim3(nblk), dim3(256), 0, s, (const bf16_t*)dy, x, M, D, w, mean, rstd, res1,
+                       res2, dx, dxb, dwp, dbp);
+  else
+    hipLaunchKernelGGL((ln_bwd_k<NPL, float>), dim3(nblk), dim3(256), 0, s, (const float*)dy, x, M, D, w, mean, rstd, res1,
+                       res2, dx, dxb, dwp, dbp);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace lthm
+
+using namespace lthm;
+
+extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y,
+                                  int32_t y_dtype, float* mean, float* rstd, void* stream) {
+  LTHM_REQUIRE(M >= 0 && D > 0 && D <= 1024 && w != nullptr);
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int npl = (D + 63) / 64;
+  if (npl <= 1) return ln_fwd_launch<1>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  if (npl <= 2) return ln_fwd_launch<2>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  if (npl <= 4) return ln_fwd_launch<4>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  if (npl <= 8) return ln_fwd_launch<8>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  return ln_fwd_launch<16>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+}
+
+extern "C" int lthm_layernorm_bwd_blocks(int64_t M) { return grid_for(M, 4, 256 * 4); }
+
+extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D, const float* w,
+                                  const float* mean, const float* rstd, const float* res1, const float* res2, float* dx,
+                                  void* dx_bf16, float* partials, void* stream) {
+  LTHM_REQUIRE(M >= 0 && D > 0 && D <= 1024 && w != nullptr && partials != nullptr);
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = grid_for(M, 4, 256 * 4);
+  const int npl = (D + 63) / 64;
+  bf16_t* xb = (bf16_t*)dx_bf16;
+  if (npl <= 1) return ln_bwd_launch<1>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+  if (npl <= 2) return ln_bwd_launch<2>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+  if (npl <= 4) return ln_bwd_launch<4>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+  if (npl <= 8) return ln_bwd_launch<8>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+  return ln_bwd_launch<16>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+}

@@ -65,3 +65,179 @@ def kshift(ids, weight, P: int, K: int, mode: int, F: int = 1, out_dtype=None):
     if out_dtype is None:
         out_dtype = weight.dtype
     return KShiftFn.apply(ids.contiguous(), weight, P, K, mode, F, out_dtype)
+
+
+# ----------------------------------------------------------------- helpers
+def cast(x: torch.Tensor, dtype) -> torch.Tensor:
+    """dtype cast in a HIP kernel (f32 <-> bf16)."""
+    require_gpu(x)
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    call("lthm_cast", ptr(x), dcode(x), ptr(out), dcode(out), x.numel(), stream())
+    return out
+
+
+def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """Sum over all leading dims of x [..., C] -> f32 [C]."""
+    require_gpu(x)
+    C = x.shape[-1]
+    rows = x.numel() // C if C else 0
+    if out is None:
+        out = torch.empty(C, dtype=torch.float32, device=x.device)
+        accumulate = False
+    call("lthm_colsum", ptr(x), dcode(x), rows, C, C, ptr(out), int(accumulate), stream())
+    return out
+
+
+# ----------------------------------------------------------------- GEMM
+ACT_NONE, ACT_GELU, ACT_QGELU, ACT_GELU_GRAD, ACT_QGELU_GRAD = 0, 1, 2, 3, 4
+_ws_cache = {}
+
+
+def _workspace(dev, nbytes: int) -> torch.Tensor:
+    t = _ws_cache.get(dev)
+    if t is None or t.numel() * 4 < nbytes:
+        t = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        _ws_cache[dev] = t
+    return t
+
+
+def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, out=None,
+         out_dtype=torch.bfloat16, ldc=None, alpha=1.0, bias=None, act=ACT_NONE, aux=None, aux_out=None,
+         res1=None, res2=None, batch=1, sA=0, sB=0, sC=0, splits=1):
+    """C = epi(alpha * A.B) on the MFMA GEMM kernel (include/lthm.h lthm_gemm)."""
+    from ._lib import STRUCTS
+    require_gpu(A, B)
+    dev = A.device
+    if out is None:
+        shape = (batch, M, N) if batch > 1 else (M, N)
+        out = torch.empty(shape, dtype=out_dtype, device=dev)
+    d = STRUCTS["lthm_gemm_desc"]()
+    d.A, d.B, d.C = ptr(A), ptr(B), ptr(out)
+    d.M, d.N, d.K = M, N, K
+    d.lda = lda if lda is not None else (K if a_kcontig else M)
+    d.ldb = ldb if ldb is not None else (K if b_kcontig else N)
+    d.ldc = ldc if ldc is not None else N
+    d.sA, d.sB, d.sC = sA, sB, (sC if sC else M * (ldc if ldc is not None else N))
+    d.batch, d.a_kcontig, d.b_kcontig = batch, int(a_kcontig), int(b_kcontig)
+    d.out_dtype = dcode(out)
+    d.alpha, d.act = alpha, act
+    d.bias = ptr(bias)
+    d.aux, d.aux_out = ptr(aux), ptr(aux_out)
+    d.ldaux = N
+    d.res1, d.res2 = ptr(res1), ptr(res2)
+    d.ldr1 = d.ldr2 = N
+    d.res1_dtype = dcode(res1) if res1 is not None else F32
+    d.res2_dtype = dcode(res2) if res2 is not None else F32
+    if splits > 1:
+        ws = _workspace(dev, splits * batch * M * N * 4)
+        d.workspace, d.workspace_bytes = ptr(ws), ws.numel() * 4
+    d.splits = splits
+    import ctypes
+    call("lthm_gemm", ctypes.addressof(d), stream())
+    return out
+
+
+def _splits_for(M: int, N: int, K: int) -> int:
+    """Split-K factor for tall reductions (weight gradients): fill ~2 waves of 256 CUs."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    if tiles >= 256 or K < 4096:
+        return 1
+    s = max(1, min(512 // tiles, K // 2048))
+    return s
+
+
+def linear_fwd(x2d, w_bf16, bias=None, act=ACT_NONE, aux_out=None, res1=None, res2=None, out_dtype=torch.bfloat16):
+    """y = act(x W^T + b) (+ res1 + res2). x2d [M, K] bf16, w [N, K] bf16."""
+    M, K_ = x2d.shape
+    N = w_bf16.shape[0]
+    return gemm(x2d, w_bf16, M, N, K_, bias=bias, act=act, aux_out=aux_out, res1=res1, res2=res2,
+                out_dtype=out_dtype)
+
+
+def linear_dgrad(dy2d, w_bf16, act_grad=ACT_NONE, aux=None, out_dtype=torch.bfloat16, res1=None):
+    """dx = (dy W) [* act'(aux)].  dy [M, N] bf16, w [N, K] bf16 (K-strided B operand)."""
+    M, N = dy2d.shape
+    K_ = w_bf16.shape[1]
+    return gemm(dy2d, w_bf16, M, K_, N, a_kcontig=True, b_kcontig=False, ldb=K_, act=act_grad, aux=aux,
+                out_dtype=out_dtype, res1=res1)
+
+
+def linear_wgrad(dy2d, x2d, out=None, accumulate=False):
+    """dW = dy^T x  -> f32 [N, K].  dy [M, N] bf16, x [M, K] bf16 (both K-strided over M)."""
+    M, N = dy2d.shape
+    K_ = x2d.shape[1]
+    res = out if (accumulate and out is not None) else None
+    s = _splits_for(N, K_, M)
+    return gemm(dy2d, x2d, N, K_, M, a_kcontig=False, b_kcontig=False, lda=N, ldb=K_, out=out,
+                out_dtype=torch.float32, res1=res, splits=s)
+
+
+# ----------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
+    require_gpu(x2d, w)
+    M, D = x2d.shape
+    y = torch.empty((M, D), dtype=y_dtype, device=x2d.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x2d.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x2d.device)
+    call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True):
+    from ._lib import load
+    M, D = x2d.shape
+    nblk = load().lthm_layernorm_bwd_blocks(M)
+    part = torch.empty((2, nblk, D), dtype=torch.float32, device=x2d.device)
+    dx = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
+    dxb = torch.empty((M, D), dtype=torch.bfloat16, device=x2d.device) if want_bf16 else None
+    call("lthm_layernorm_bwd", ptr(dy2d), dcode(dy2d), ptr(x2d), M, D, ptr(w), ptr(mean), ptr(rstd), ptr(res1),
+         ptr(res2), ptr(dx), ptr(dxb), ptr(part), stream())
+    dw = colsum(part[0])
+    db = colsum(part[1]) if need_bias else None
+    return dx, dxb, dw, db
+
+
+# ----------------------------------------------------------------- attention
+def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs):
+    from ._lib import STRUCTS
+    d = STRUCTS["lthm_attn_desc"]()
+    d.q, d.k, d.v = ptr(q), ptr(k), ptr(v)
+    d.q_tok_stride, d.k_tok_stride, d.v_tok_stride = q_ts, kv_ts, kv_ts
+    d.q_head_stride, d.k_head_stride, d.v_head_stride = E, kv_hs, kv_hs
+    d.q_batch_stride, d.k_batch_stride, d.v_batch_stride = T * q_ts, T * kv_ts, T * kv_ts
+    d.out, d.o_tok_stride, d.o_head_stride, d.o_batch_stride = ptr(out), H * E, E, T * H * E
+    d.table = ptr(table)
+    d.table_rows = table.shape[0] if table is not None else 0
+    d.lse = ptr(lse)
+    d.B, d.T, d.H, d.E, d.causal = B, T, H, E, int(causal)
+    return d
+
+
+def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True):
+    """qkv bf16 [B*T, 3*H*E] (c_attn output) -> out bf16 [B*T, H*E], lse f32 [B, H, T]."""
+    import ctypes
+    C = H * E
+    out = torch.empty((B * T, C), dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
+    q = qkv
+    k = qkv[:, C:]
+    v = qkv[:, 2 * C:]
+    d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
+    call("lthm_attn_fwd", ctypes.addressof(d), stream())
+    return out, lse
+
+
+def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
+    """-> dqkv bf16 [B*T, 3C], dtable f32 [2T+1, H] (or None)."""
+    import ctypes
+    C = H * E
+    dqkv = torch.empty_like(qkv)
+    part = torch.empty((B, 2 * T + 1, H), dtype=torch.float32, device=qkv.device) if table is not None else None
+    d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
+    d.dout, d.dq, d.dk, d.dv = ptr(dout), ptr(dqkv), ptr(dqkv[:, C:]), ptr(dqkv[:, 2 * C:])
+    d.dtable_part = ptr(part)
+    call("lthm_attn_bwd", ctypes.addressof(d), stream())
+    dtab = None
+    if part is not None:
+        dtab = colsum(part.view(B, (2 * T + 1) * H)).view(2 * T + 1, H)
+    return dqkv, dtab
