@@ -73,6 +73,14 @@ int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* 
                           const float* norms, int64_t P, int32_t D, int32_t K,
                           int32_t mode, float* dW, void* stream);
 
+/* Same, plus the touched-row list for the sparse row-wise optimizers: the first
+ * add to a row sets flags[row] (int32 [F*P], caller keeps it zeroed) and appends
+ * the row to list (int64 [>= n*F*K]) at atomic index *count (int64, zeroed). */
+int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void* dY,
+                           int32_t dy_dtype, const void* out, int32_t out_dtype,
+                           const float* norms, int64_t P, int32_t D, int32_t K, int32_t mode,
+                           float* dW, int32_t* flags, int64_t* list, int64_t* count, void* stream);
+
 /* ------------------------------------------------------------------------- */
 /* GEMM: every nn.Linear on the path (commons/transformers/layers.py:240-241,   */
 /* :274-276; commons/layers.py:65-81; models/lthm/sequence/ Linears)          */
@@ -183,6 +191,172 @@ int lthm_attn_fwd(const lthm_attn_desc* desc, void* stream);
 int lthm_attn_bwd(const lthm_attn_desc* desc, void* stream);
 
 /* ------------------------------------------------------------------------- */
+/* LTHM towers (models/lthm/sequence/ encoder, product and query towers)     */
+/* ------------------------------------------------------------------------- */
+#define LTHM_MAX_CVE 8
+
+/* history flip, right padding -> left padding (encoder.py:52-54, 60-61) */
+int lthm_flip_tokens(const int64_t* in, int64_t* out, int64_t B, int32_t T, void* stream);
+
+/* ProductTower.forward (product_tower.py:43-62) with its 6 CosineVectorEmbedding
+ * modules (commons/transformers/layers.py:443-471) fused per token. */
+typedef struct lthm_ptower_desc {
+  const int64_t* ids;
+  const void* x;
+  int32_t x_dtype;
+  int32_t Din;
+  int64_t n;
+  int32_t Dout;
+  int32_t n_mod;
+  const float* w_map;
+  const float* b_map;
+  const float* proj;
+  const float* grids;
+  const void* tables;
+  const void* hist;
+  int32_t tab_dtype;
+  int32_t proj_total;
+  int32_t grid_total;
+  int32_t cve_rows;
+  int32_t norm_bins;
+  float norm_threshold;
+  int32_t cve_only;       /* 1: plain CosineVectorEmbedding(s): sum of bags only, one normalisation */
+  int32_t emb_dtype;      /* dtype of emb_out: LTHM_F32 or LTHM_BF16 */
+  int32_t mod_nproj[8];
+  int32_t mod_nbins[8];
+  int32_t mod_row_off[8];
+  int32_t mod_proj_off[8];
+  int32_t mod_grid_off[8];
+  void* emb_out;
+  uint16_t* rows_out;
+  void* xn_out;
+  uint8_t* mask_out;
+} lthm_ptower_desc;
+
+int lthm_product_tower_fwd(const lthm_ptower_desc* desc, void* stream);
+
+/* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i (0xffff = skip).
+ * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows. */
+int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,
+                         int64_t n, int32_t R, int32_t D, float* dW, void* stream);
+/* QuantileMapper (commons/transformers/layers.py:477-487) on x [B, F]:
+ * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
+int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,
+                      float* out, void* stream);
+
+/* QueryTower input assembly (query_tower.py:89-111): action + time embeddings,
+ * pad substitution, zero/CLS token, reversed position embedding. */
+typedef struct lthm_tokens_desc {
+  const void* P;
+  int32_t p_dtype;
+  int32_t d;
+  const int64_t* labels;
+  const int64_t* ts;
+  const uint8_t* mask;
+  int64_t B;
+  int32_t T_full;
+  int32_t trim;
+  const float* act;
+  const float* hod;
+  const float* how;
+  const float* dow;
+  const float* wpe;
+  const float* pad;
+  const float* ctx;
+  int32_t off_act;
+  int32_t off_hod;
+  int32_t off_how;
+  int32_t off_dow;
+  int32_t off_wpe;
+  int32_t off_pad;
+  int64_t div_hod;
+  int64_t mod_hod;
+  int64_t div_how;
+  int64_t mod_how;
+  int64_t div_dow;
+  int64_t mod_dow;
+  float* x0;
+  uint16_t* rows_out;
+} lthm_tokens_desc;
+
+int lthm_tokens_fwd(const lthm_tokens_desc* desc, void* stream);
+/* dP (bf16 [B, T, d]) = unmasked dx0[:, 1:], dctx (f32 [B, d], may be NULL) = dx0[:, 0] */
+int lthm_tokens_bwd(const lthm_tokens_desc* desc, const float* dx0, void* dP, float* dctx, void* stream);
+/* out = bf16(x + table[outcome mod n_outcomes]) (query_tower.py:118-122); rows_out [B*(T+1)] */
+int lthm_outcome_fwd(const float* x, const int64_t* labels, int64_t B, int32_t T_full, int32_t trim,
+                     int64_t future, const float* table, int32_t n_outcomes, int32_t D, void* out,
+                     uint16_t* rows, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* In-batch contrastive loss (models/lthm/sequence/wrapper.py:114-245)        */
+/* ------------------------------------------------------------------------- */
+/* F.normalize of rows: out bf16 [rows, D], norms f32 [rows] (wrapper.py:118-119) */
+int lthm_rownorm(const void* x, int32_t x_dtype, int64_t rows, int32_t D, void* out_bf16, float* norms,
+                 void* stream);
+/* backward of lthm_rownorm: dx = (g - y (y.g)) / |x|; writes dx_bf16 and/or dx_f32 */
+int lthm_rownorm_bwd(const void* x, int32_t x_dtype, const float* norms, const float* g, int64_t rows,
+                     int32_t D, void* dx_bf16, float* dx_f32, void* stream);
+
+typedef struct lthm_contrastive_desc {
+  const void* out_n;      /* bf16 [B, T+1, n_heads, De] normalised next_token_emb */
+  const void* in_n;       /* bf16 [B, T, De] normalised current_token_emb */
+  const uint8_t* mask;    /* [B, mask_stride] pad mask (already offset by the trim) */
+  int64_t mask_stride;
+  int64_t B;
+  int32_t T;
+  int32_t n_heads;
+  int32_t head;
+  int32_t De;
+  int32_t mb_size;        /* train_mini_batch_size (32) */
+  int32_t n_mb;
+  int32_t n_max;          /* >= mb_size * T, <= 4096 */
+  float tau;              /* softmax_temperature */
+  const int32_t* offsets; /* [n_mb, n_heads] lookahead offset per mini-batch and head */
+  float* lse;             /* [n_mb, n_max] per-row buffers (this head) */
+  float* pos;
+  int32_t* cnt;
+  int32_t* rank;
+  float* diag;
+  float* w;               /* row weights, written by the forward, read by the backward */
+  const float* gscale;    /* device scalar: upstream gradient of the loss (backward) */
+  float* d_out;           /* f32 [B, T+1, n_heads, De] (rows of this head written) */
+  float* d_in;            /* f32 [B, T, De] (accumulated over heads) */
+} lthm_contrastive_desc;
+
+/* Forward for one head over all mini-batches.  stats [n_mb, nstat] f32:
+ * {mean CE, used rows, mean negatives, min negatives, mean rank, median rank,
+ *  offset, hit@ks[0..nk)}; loss_scale multiplies the row weights (1 / n_mb). */
+int lthm_contrastive_fwd(const lthm_contrastive_desc* desc, float* stats, int32_t nstat, const int32_t* ks,
+                         int32_t nk, float loss_scale, void* stream);
+int lthm_contrastive_bwd(const lthm_contrastive_desc* desc, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Optimizers and gradient transforms                                        */
+/* ------------------------------------------------------------------------- */
+/* torch.optim.AdamW step on a flat fp32 tensor (wrapper.py:263-275); optional bf16
+ * shadow of the updated parameter; grad_scale multiplies g (clipping). */
+int lthm_adamw(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+               float eps, float weight_decay, int64_t step, float grad_scale, void* bf16_shadow,
+               int32_t zero_grad, void* stream);
+/* torch.optim.Adagrad step (embedding_module_gen.py:97,137) */
+int lthm_adagrad(float* p, float* g, float* state_sum, int64_t n, float lr, float lr_decay, float eps,
+                 float weight_decay, int64_t step, int32_t zero_grad, void* stream);
+/* row-wise (lazy) AdamW / Adagrad over the touched rows of a [R, D] table; each
+ * consumed gradient row is re-zeroed and its flag cleared.  max_rows bounds *count. */
+int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                      float* g, float* m, float* v, int32_t* flags, float lr, float beta1, float beta2,
+                      float eps, float weight_decay, int64_t step, void* bf16_shadow, void* stream);
+int lthm_sparse_adagrad(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                        float* g, float* state_sum, int32_t* flags, float lr, float lr_decay, float eps,
+                        int64_t step, void* bf16_shadow, void* stream);
+/* *out_accum += sum(x^2) */
+int lthm_sumsq(const void* x, int32_t dtype, int64_t n, float* out_accum, void* stream);
+/* max_norm <= 0: y = x / (sqrt(*sumsq) + add_eps)   (cap_gradients, commons/functional.py:23)
+ * max_norm  > 0: y = x * min(1, max_norm / (sqrt(*sumsq) + 1e-6))   (clip_grad_norm_) */
+int lthm_scale_by_norm(const void* x, void* y, int32_t dtype, int64_t n, const float* sumsq, float add_eps,
+                       float max_norm, void* stream);
+
+/* ------------------------------------------------------------------------- */
 /* streaming helpers                                                         */
 /* ------------------------------------------------------------------------- */
 int lthm_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, int64_t n, void* stream);
@@ -190,6 +364,11 @@ int lthm_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, in
 int lthm_colsum(const void* in, int32_t dtype, int64_t rows, int64_t cols, int64_t ld, float* out,
                 int32_t accumulate, void* stream);
 int lthm_fill_f32(float* p, float value, int64_t n, void* stream);
+/* first column of mask [B, T] (uint8, 1 = pad) holding a non-pad entry (T if none) -> *out
+ * (the history trim of query_tower.py:73-86) */
+int lthm_trim_first_valid(const uint8_t* mask, int64_t B, int32_t T, int32_t* out, void* stream);
+/* y = act(x) (dy == NULL) or y = dy * act'(x); act = LTHM_ACT_GELU / LTHM_ACT_QGELU */
+int lthm_activation(const void* x, const void* dy, void* y, int32_t dtype, int64_t n, int32_t act, void* stream);
 
 #ifdef __cplusplus
 }

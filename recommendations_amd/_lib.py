@@ -86,7 +86,11 @@ def parse_structs(path: str = HEADER) -> Dict[str, type]:
             typ, name = line.rsplit(" ", 1)
             stars = name.count("*") + typ.count("*")
             typ, name = typ.replace("*", "").strip(), name.replace("*", "")
-            fields.append((name, _CTYPE[typ + "*" * stars]))
+            ct = _CTYPE[typ + "*" * stars]
+            am = re.match(r"^(\w+)\[(\d+)\]$", name)
+            if am:
+                name, ct = am.group(1), ct * int(am.group(2))
+            fields.append((name, ct))
         out[m.group(3)] = type(m.group(3), (ctypes.Structure,), {"_fields_": fields})
     return out
 

@@ -82,3 +82,209 @@ class _ZeroRowGrad(torch.autograd.Function):
         g = g.clone()
         g[ctx.row].zero_()
         return g, None
+
+
+# ------------------------------------------------------------------ sparse (row-wise) KShift
+class _SparseKShiftFn(torch.autograd.Function):
+    """Forward as K.KShiftFn; backward accumulates into the module's persistent
+    dense f32 gradient and appends the touched rows for the row-wise optimizer
+    (no [P, D] gradient tensor is materialised per step)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, mod, gather_w):
+        from .._lib import call, dcode, ptr, require_gpu, stream
+        require_gpu(ids, weight)
+        F_, P, Kk, mode = mod._F, mod._num_embeddings, mod._num_shifts, mod._mode
+        D = weight.shape[1]
+        out_dtype = mod._out_dtype or torch.float32
+        out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
+        norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if mode == K.KSHIFT_NORMALIZE else None
+        call("lthm_kshift_fwd_multi", ptr(ids), ids.numel() // F_, F_, ptr(gather_w), dcode(gather_w), P, D, Kk, mode,
+             ptr(out), dcode(out), ptr(norms), stream())
+        ctx.mod = mod
+        ctx.save_for_backward(ids, out if mode == K.KSHIFT_NORMALIZE else None, norms)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        ids, out, norms = ctx.saved_tensors
+        mod = ctx.mod
+        mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
+        K.kshift_bwd_sparse(ids, gy.contiguous(), out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
+                            mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count)
+        mod.sparse_pending += ids.numel() * mod._num_shifts
+        return None, None, None, None
+
+
+class TableBatchedKShiftEmbedding(nn.Module):
+    """F KShift tables of P rows stored as one [F*P, D] weight (TorchRec-style
+    table batching): ids [..., F] -> [..., F, D].  ``sparse=True`` keeps a
+    persistent gradient + touched-row list for ``optim.SparseRowAdamW``;
+    ``gather_dtype=torch.bfloat16`` gathers from a bf16 shadow of the fp32
+    master that the optimizer keeps in sync (half the HBM bytes per lookup)."""
+
+    def __init__(self, num_features: int, num_embeddings: int, emb_dim: int, num_shifts: int = 8,
+                 normalize_output: bool = False, sparse: bool = True, gather_dtype=torch.float32, out_dtype=None):
+        super().__init__()
+        self._F = num_features
+        self._num_embeddings = num_embeddings
+        self._num_shifts = num_shifts
+        self._mode = K.KSHIFT_NORMALIZE if normalize_output else K.KSHIFT_SCALE
+        self._out_dtype = out_dtype
+        self._gather_dtype = gather_dtype
+        self.weight = nn.Parameter(torch.randn(num_features * num_embeddings, emb_dim))
+        self.sparse = sparse
+        self._shadow = None
+        self._shadow_version = -1
+        self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
+        self.sparse_pending = 0
+
+    def _ensure_sparse_state(self, max_new_rows: int):
+        w = self.weight
+        if self.sparse_grad is None or self.sparse_grad.device != w.device:
+            self.sparse_grad = K.zeros(w.shape, torch.float32, w.device)
+            self.sparse_flags = torch.zeros(w.shape[0], dtype=torch.int32, device=w.device)
+            self.sparse_count = torch.zeros(1, dtype=torch.int64, device=w.device)
+            self.sparse_rows = torch.empty(0, dtype=torch.int64, device=w.device)
+        need = min(self.sparse_pending + max_new_rows, w.shape[0])
+        if self.sparse_rows.numel() < need:
+            new = torch.empty(max(need, 2 * self.sparse_rows.numel()), dtype=torch.int64, device=w.device)
+            if self.sparse_rows.numel():
+                new[: self.sparse_rows.numel()].copy_(self.sparse_rows)
+            self.sparse_rows = new
+
+    def gather_weight(self):
+        if self._gather_dtype == torch.float32:
+            return self.weight
+        if self._shadow is None or self._shadow_version != self.weight._version or \
+                self._shadow.device != self.weight.device:
+            self._shadow = K.cast(self.weight.detach(), self._gather_dtype)
+            self._shadow_version = self.weight._version
+        return self._shadow
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.contiguous()
+        if self.sparse:
+            return _SparseKShiftFn.apply(ids, self.weight, self, self.gather_weight())
+        return K.kshift(ids, self.weight, self._num_embeddings, self._num_shifts, self._mode, F=self._F,
+                        out_dtype=self._out_dtype or self.weight.dtype)
+
+
+# ------------------------------------------------------------------ feature interaction
+class QuickGELU(nn.Module):
+    """commons/layers.py:9-11."""
+
+    def forward(self, x):
+        return K.ActivationFn.apply(x, K.ACT_QGELU)
+
+
+class MLP(nn.Module):
+    """commons/layers.py:65-81: (Linear + QuickGELU) per gate, final Linear — one fused chain op."""
+
+    def __init__(self, input_dim, out_dim, gate_sizes):
+        super().__init__()
+        previous_dim = input_dim
+        blocks = []
+        for gate_size in gate_sizes:
+            blocks.append(nn.Linear(previous_dim, gate_size))
+            blocks.append(QuickGELU())
+            previous_dim = gate_size
+        blocks.append(nn.Linear(previous_dim, out_dim))
+        self.model = nn.Sequential(*blocks)
+
+    def forward(self, x: torch.Tensor):
+        lins = [m for m in self.model if isinstance(m, nn.Linear)]
+        acts = [K.ACT_QGELU] * (len(lins) - 1) + [K.ACT_NONE]
+        return K.mlp_chain(x, lins, acts, out_f32=True)
+
+
+class PatternFromTimelocal(nn.Module):
+    """commons/layers.py:14-41 with the constructor fixed (SURVEY.md §3.5 #4):
+    index = (ts // div) mod mod -> nn.Embedding(mod, emb_dim)."""
+
+    def __init__(self, div, mod, emb_dim):
+        super().__init__()
+        self.div, self.mod, self.emb_dim = div, mod, emb_dim
+        self.emb = nn.Embedding(num_embeddings=mod, embedding_dim=emb_dim) if emb_dim > 0 else nn.Identity()
+
+    def index(self, x):
+        return torch.remainder(torch.floor_divide(x.long(), self.div), self.mod)
+
+    def forward(self, x):
+        return K.kshift(self.index(x), self.emb.weight, self.mod, 1, K.KSHIFT_NONE)
+
+
+class HistogramEmbedding(nn.Module):
+    """Build-defined (SURVEY.md §3.5 #1: imported by product_tower.py:6 but absent
+    from the reference): ``nbins`` uniform bins over [lo, hi] (clamped), one
+    ``emb_dim`` row per bin."""
+
+    def __init__(self, lo: float, hi: float, nbins: int, emb_dim: int):
+        super().__init__()
+        self.lo, self.hi, self.nbins = float(lo), float(hi), int(nbins)
+        self.emb = nn.Embedding(nbins, emb_dim)
+
+
+class QREmbedding(nn.Module):
+    """commons/layers.py:102-123 with the constructor fixed (SURVEY.md §3.5 #5):
+    Wq[(x mod d^2) // d mod d] + Wr[x mod d]."""
+
+    def __init__(self, num_embeddings: int, emb_dim: int, normalize_output: bool):
+        super().__init__()
+        self._div = int(math.sqrt(num_embeddings))
+        self.num_embeddings = self._div * self._div
+        self.emb_dim = emb_dim
+        self.emb_q = nn.Embedding(self._div, emb_dim)
+        self.emb_r = nn.Embedding(self._div, emb_dim)
+        self.normalize_output = normalize_output
+
+    def forward(self, x):
+        x = torch.remainder(x, self.num_embeddings)
+        q = torch.remainder(torch.div(x, self._div, rounding_mode="floor"), self._div)
+        r = torch.remainder(x, self._div)
+        y = K.kshift(q.contiguous(), self.emb_q.weight, self._div, 1, K.KSHIFT_NONE) + \
+            K.kshift(r.contiguous(), self.emb_r.weight, self._div, 1, K.KSHIFT_NONE)
+        if self.normalize_output:
+            y = K.kshift(torch.arange(y.shape[0], device=y.device), y, y.shape[0], 1, K.KSHIFT_NORMALIZE) \
+                if y.dim() == 2 else y / y.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        return y
+
+
+class StreamingLogQCorrectionModule(nn.Module):
+    """commons/layers.py:189-213 (train_step fixed: `self.a[hash] = batch_idx`, SURVEY.md §3.5 #7)."""
+
+    def __init__(self, num_buckets, hash_offset, alpha: float = 0.05, p_init: float = 0.01):
+        super().__init__()
+        self.num_buckets, self.hash_offset, self.alpha, self.p_init = num_buckets, hash_offset, alpha, p_init
+        self.register_buffer("b", (1.0 / p_init) * torch.ones((num_buckets,), dtype=torch.float32))
+        self.register_buffer("a", torch.zeros((num_buckets,), dtype=torch.float))
+
+    def hash_fn(self, products):
+        return (products + self.hash_offset) % self.num_buckets
+
+    def forward(self, products: torch.Tensor) -> torch.Tensor:
+        return -self.b[self.hash_fn(products)].log().reshape(*products.shape)
+
+    def train_step(self, products: torch.Tensor, batch_idx: int):
+        h = self.hash_fn(products)
+        self.b[h] = ((1 - self.alpha) * self.b[h]) + (self.alpha * (batch_idx - self.a[h])).float()
+        self.a[h] = float(batch_idx)
+
+
+class CascadedStreamingLogQCorrectionModule(nn.Module):
+    """commons/layers.py:217-237 (train_step loop fixed, SURVEY.md §3.5 #8)."""
+
+    def __init__(self, num_buckets, hash_offsets, alpha: float = 0.05, p_init: float = 0.01):
+        super().__init__()
+        self.models = nn.ModuleList([StreamingLogQCorrectionModule(num_buckets, o, alpha, p_init) for o in hash_offsets])
+
+    def forward(self, products):
+        result = None
+        for mod in self.models:
+            v = mod(products)
+            result = v if result is None else torch.minimum(result, v)
+        return result
+
+    def train_step(self, products, batch_idx):
+        for mod in self.models:
+            mod.train_step(products, batch_idx)

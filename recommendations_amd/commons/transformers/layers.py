@@ -247,3 +247,131 @@ class TransformerBlock(nn.Module):
     def forward_double_residual(self, x: torch.Tensor) -> torch.Tensor:
         """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137)."""
         return self._fused(x, True)
+
+
+# ------------------------------------------------------------------ vector-feature layers
+class CVEFn(torch.autograd.Function):
+    """Standalone CosineVectorEmbedding(s) (commons/transformers/layers.py:462-471):
+    normalise, project, bucketize, EmbeddingBag-sum — the product-tower kernel in
+    cve_only mode; backward = LDS-privatised bag scatter into the tables.  The
+    input (projected direction) receives no gradient, as in the reference
+    (bucketize is piecewise constant)."""
+
+    @staticmethod
+    def forward(ctx, x, mods, *tables):
+        import ctypes
+        from ..._lib import STRUCTS, call, dcode, ptr, stream
+        require_gpu(x)
+        shp = x.shape
+        x2 = x.detach().contiguous().view(-1, shp[-1])
+        n, Din = x2.shape
+        Dout = tables[0].shape[1]
+        dev = x.device
+        R = sum(t.shape[0] for t in tables)
+        tab = torch.cat([t.detach().float() for t in tables]) if len(tables) > 1 else tables[0].detach().float().contiguous()
+        proj = torch.cat([m.projection_mat.reshape(-1) for m in mods])
+        grids = torch.cat([m.grid.reshape(-1) for m in mods])
+        total = sum(m.n_proj for m in mods)
+        emb = torch.empty((n, Dout), dtype=torch.bfloat16, device=dev)
+        emb32 = torch.empty((n, Dout), dtype=torch.float32, device=dev)
+        rows = torch.empty((n, total), dtype=torch.int16, device=dev)
+        d = STRUCTS["lthm_ptower_desc"]()
+        d.ids, d.x, d.x_dtype, d.Din, d.n, d.Dout = None, ptr(x2), dcode(x2), Din, n, Dout
+        d.n_mod = len(mods)
+        d.proj, d.grids, d.tables, d.tab_dtype = ptr(proj), ptr(grids), ptr(tab), dcode(tab)
+        d.proj_total, d.grid_total, d.cve_rows, d.norm_bins, d.cve_only = proj.numel(), grids.numel(), R, 0, 1
+        ro = po = go = 0
+        for j, m in enumerate(mods):
+            d.mod_nproj[j], d.mod_nbins[j] = m.n_proj, m.num_bins
+            d.mod_row_off[j], d.mod_proj_off[j], d.mod_grid_off[j] = ro, po, go
+            ro += (m.num_bins + 1) * m.n_proj
+            po += m.projection_mat.numel()
+            go += m.grid.numel()
+        d.emb_out, d.rows_out, d.emb_dtype = ptr(emb32), ptr(rows), dcode(emb32)
+        call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
+        ctx.save_for_backward(rows)
+        ctx.meta = ([t.shape for t in tables], R, shp)
+        return emb32.view(*shp[:-1], Dout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (rows,) = ctx.saved_tensors
+        shapes, R, shp = ctx.meta
+        dtab = K.small_table_bwd(rows, dy.contiguous().view(rows.shape[0], -1).float(), R)
+        out, r = [], 0
+        for s in shapes:
+            out.append(dtab[r:r + s[0]])
+            r += s[0]
+        return (None, None, *out)
+
+
+class CosineVectorEmbedding(nn.Module):
+    """commons/transformers/layers.py:443-471 (buffers projection_mat, grid, pos_offset; emb.weight)."""
+
+    def __init__(self, inp_dim: int, emb_dim: int, n_proj: int = 16, num_bins: int = 20):
+        super().__init__()
+        proj = torch.randn((inp_dim, n_proj))
+        proj = torch.nn.functional.normalize(proj, p=2.0, dim=0)
+        self.register_buffer("projection_mat", proj, persistent=True)
+        resolution = 2.0 / float(num_bins)
+        grid = torch.linspace(-1.0, 1.0, steps=num_bins + 1)[:-1] + 0.5 * resolution
+        self.register_buffer("grid", grid, persistent=True)
+        self.register_buffer("pos_offset", ((num_bins + 1) * torch.arange(0, n_proj, dtype=torch.long)).reshape(n_proj),
+                             persistent=True)
+        self.emb = nn.EmbeddingBag((num_bins + 1) * n_proj, emb_dim, mode="sum")
+        self.emb_dim, self.n_proj, self.num_bins = emb_dim, n_proj, num_bins
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return CVEFn.apply(x, [self], self.emb.weight)
+
+
+class QuantileMapper(nn.Module):
+    """commons/transformers/layers.py:477-487: bucketize(x, q) / (len(q) + 1) - 0.5."""
+
+    def __init__(self, quantiles: List[float]):
+        super().__init__()
+        self.register_buffer("quantiles", torch.tensor(quantiles), persistent=True)
+        self.n_bins = len(quantiles) + 1
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return K.quantile_map(x.contiguous().float(), self.quantiles.view(1, -1).contiguous(), shared=True)
+
+
+class DenseMapper(nn.Module):
+    """commons/transformers/layers.py:490-511: per-feature quantile mapping, concat,
+    sum of CosineVectorEmbedding bags (one fused kernel for all modules)."""
+
+    def __init__(self, stats: Dict[str, Any], emb_dim: int, n_projs: List[int], num_bins: List[int]):
+        super().__init__()
+        self.mappers = nn.ModuleDict({f: QuantileMapper(stats[f]) for f in stats})
+        assert len(n_projs) == len(num_bins)
+        self.emb = nn.ModuleList([CosineVectorEmbedding(len(self.mappers), emb_dim, n_proj=p, num_bins=b)
+                                  for p, b in zip(n_projs, num_bins)])
+
+    def quantile_table(self) -> torch.Tensor:
+        return torch.stack([m.quantiles for m in self.mappers.values()])
+
+    def forward(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        x = torch.cat([batch[f].reshape(-1, 1) for f in self.mappers], dim=1).float().contiguous()
+        z = K.quantile_map(x, self.quantile_table().contiguous(), shared=False)
+        return CVEFn.apply(z.unsqueeze(1), list(self.emb), *[m.emb.weight for m in self.emb]).squeeze(1)
+
+
+class MLP(nn.Module):
+    """commons/transformers/layers.py:67-81 (Linear + GELU-tanh gates)."""
+
+    def __init__(self, in_features: int, out_features: int, gate_sizes: Optional[Tuple[int, ...]] = None, bias: bool = True):
+        super().__init__()
+        gate_sizes = gate_sizes if gate_sizes is not None else []
+        blocks: List[nn.Module] = []
+        prev = in_features
+        for gsz in gate_sizes:
+            blocks.append(nn.Linear(prev, gsz, bias=bias))
+            blocks.append(nn.GELU(approximate="tanh"))
+            prev = gsz
+        blocks.append(nn.Linear(prev, out_features, bias=bias))
+        self.model = nn.Sequential(*blocks)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        lins = [m for m in self.model if isinstance(m, nn.Linear)]
+        return K.mlp_chain(x, lins, [K.ACT_GELU] * (len(lins) - 1) + [K.ACT_NONE], out_f32=True)

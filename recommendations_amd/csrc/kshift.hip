@@ -113,7 +113,8 @@ template <typename TY, typename TO>
 __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
     const int64_t* __restrict__ ids, int64_t n_items, int F, const TY* __restrict__ dY,
     const TO* __restrict__ out, const float* __restrict__ norms, int64_t P, int D, int K, int mode,
-    float scale, int CH, int NP2, float* __restrict__ dW) {
+    float scale, int CH, int NP2, float* __restrict__ dW, int32_t* __restrict__ flags, int64_t* __restrict__ list,
+    unsigned long long* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* keys = reinterpret_cast<uint64_t*>(smem);                   // NP2
   float* g = reinterpret_cast<float*>(smem + (size_t)KB_NP * 8);        // CH * D
@@ -225,6 +226,9 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
         }
         atomicAdd(dW + row * D + d, acc);
       }
+      if (flags != nullptr && gl == 0) {
+        if (atomicExch(flags + row, 1) == 0) list[atomicAdd(count, 1ull)] = row;
+      }
     }
     __syncthreads();
   }
@@ -272,7 +276,8 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
 
 template <typename TY, typename TO>
 static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY, const void* out,
-                      const float* norms, int64_t P, int D, int K, int mode, float* dW, hipStream_t s) {
+                      const float* norms, int64_t P, int D, int K, int mode, float* dW, int32_t* flags,
+                      int64_t* list, unsigned long long* count, hipStream_t s) {
   int ch = KB_NP / K;
   if (ch * D > KB_G_FLOATS) ch = KB_G_FLOATS / D;
   LTHM_REQUIRE(ch >= 1);
@@ -282,7 +287,7 @@ static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY
   const size_t shmem = (size_t)KB_NP * 8 + (size_t)KB_G_FLOATS * 4 + (size_t)(KB_NP + 1) * 4;
   const int grid = grid_for(n_items, ch, 256 * 8);
   hipLaunchKernelGGL((kshift_bwd_dense_k<TY, TO>), dim3(grid), dim3(256), shmem, s, ids, n_items, F,
-                     (const TY*)dY, (const TO*)out, norms, P, D, K, mode, scale, ch, np2, dW);
+                     (const TY*)dY, (const TO*)out, norms, P, D, K, mode, scale, ch, np2, dW, flags, list, count);
   LTHM_CHECK_LAUNCH();
   return 0;
 }
@@ -346,6 +351,14 @@ int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* 
 int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
                           const void* out, int32_t out_dtype, const float* norms, int64_t P, int32_t D, int32_t K,
                           int32_t mode, float* dW, void* stream) {
+  return lthm_kshift_bwd_sparse(ids, n, F, dY, dy_dtype, out, out_dtype, norms, P, D, K, mode, dW, nullptr, nullptr,
+                                nullptr, stream);
+}
+
+int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                           const void* out, int32_t out_dtype, const float* norms, int64_t P, int32_t D, int32_t K,
+                           int32_t mode, float* dW, int32_t* flags, int64_t* list, int64_t* count, void* stream) {
+  LTHM_REQUIRE((flags == nullptr) == (list == nullptr) && (list == nullptr) == (count == nullptr));
   LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n >= 0 && F >= 1);
   LTHM_REQUIRE(mode >= 0 && mode <= 2);
   LTHM_REQUIRE(mode != LTHM_KSHIFT_NORMALIZE || (out != nullptr && norms != nullptr));
@@ -353,13 +366,13 @@ int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* 
   if (items == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (dy_dtype == LTHM_F32 && out_dtype == LTHM_F32)
-    return launch_bwd<float, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+    return launch_bwd<float, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
   if (dy_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
-    return launch_bwd<bf16_t, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+    return launch_bwd<bf16_t, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
   if (dy_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
-    return launch_bwd<float, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+    return launch_bwd<float, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
   if (dy_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
-    return launch_bwd<bf16_t, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, s);
+    return launch_bwd<bf16_t, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
   return (int)hipErrorInvalidValue;
 }
 

@@ -96,3 +96,88 @@ extern "C" int lthm_fill_f32(float* p, float v, int64_t n, void* stream) {
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- trim + activations
+namespace lthm {
+// first column t (of T) where some row is not padded -> *out (atomicMin); *out pre-set to T by the host wrapper
+__global__ void first_unmasked_k(const uint8_t* __restrict__ mask, int64_t B, int T, int* __restrict__ out) {
+  const int64_t n = B * T;
+  int best = T;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    if (mask[i] == 0 && t < best) best = t;
+  }
+  for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMin(out, best);
+}
+__global__ void set_int_k(int* p, int v) { *p = v; }
+
+__device__ __forceinline__ float act_f(int act, float x) {
+  if (act == LTHM_ACT_GELU) {
+    const float kb = 0.7978845608028654f, kk = 0.044715f;
+    return 0.5f * x * (1.f + tanhf(kb * (x + kk * x * x * x)));
+  }
+  return x / (1.f + expf(-1.702f * x));
+}
+__device__ __forceinline__ float act_g(int act, float x) {
+  if (act == LTHM_ACT_GELU) {
+    const float kb = 0.7978845608028654f, kk = 0.044715f;
+    const float x2 = x * x, t = tanhf(kb * (x + kk * x2 * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kb * (1.f + 3.f * kk * x2);
+  }
+  const float s = 1.f / (1.f + expf(-1.702f * x));
+  return s + 1.702f * x * s * (1.f - s);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void act_k(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ y, int64_t n, int act) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float xv = Elem<T>::ld(x + i);
+    Elem<T>::st(y + i, dy ? Elem<T>::ld(dy + i) * act_g(act, xv) : act_f(act, xv));
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_trim_first_valid(const uint8_t* mask, int64_t B, int32_t T, int32_t* out, void* stream) {
+  LTHM_REQUIRE(B >= 0 && T > 0);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(set_int_k, dim3(1), dim3(1), 0, s, (int*)out, (int)T);
+  if (B > 0) hipLaunchKernelGGL(first_unmasked_k, dim3(grid_for(B * T, 256, 1024)), dim3(256), 0, s, mask, B, T, (int*)out);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_activation(const void* x, const void* dy, void* y, int32_t dtype, int64_t n, int32_t act, void* stream) {
+  LTHM_REQUIRE(n >= 0 && (act == LTHM_ACT_GELU || act == LTHM_ACT_QGELU));
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(n, 256, 256 * 16);
+  if (dtype == LTHM_F32) hipLaunchKernelGGL((act_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, (const float*)dy, (float*)y, n, act);
+  else hipLaunchKernelGGL((act_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)y, n, act);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace lthm {
+__global__ void quantile_map_k(const float* __restrict__ x, int64_t B, int F, const float* __restrict__ q, int nq, int shared,
+                               float* __restrict__ out) {
+  const int64_t n = B * F;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i % F);
+    const float* qf = q + (shared ? 0 : (int64_t)f * nq);
+    const float v = x[i];
+    int b = 0;
+    for (int k = 0; k < nq; ++k) b += (qf[k] < v) ? 1 : 0;  // torch.bucketize(right=False)
+    out[i] = (float)b / (float)(nq + 1) - 0.5f;
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,
+                                 float* out, void* stream) {
+  LTHM_REQUIRE(B >= 0 && F > 0 && nq > 0);
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(quantile_map_k, dim3(grid_for(B * F, 256, 2048)), dim3(256), 0, (hipStream_t)stream, x, B, F,
+                     quantiles, nq, shared, out);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

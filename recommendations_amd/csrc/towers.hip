@@ -1,0 +1,383 @@
+// LTHM tower kernels for gfx950:
+//   * product tower forward (models/lthm/sequence/product_tower.py:43-62) fused
+//     into one wave-per-token kernel: norm + pad mask, L2 normalise, emb_mapper
+//     Linear(Din -> Dout), the 6 CosineVectorEmbedding modules
+//     (commons/transformers/layers.py:462-471: normalise, project, bucketize,
+//     EmbeddingBag-sum), the norm-histogram embedding and the masked fill;
+//   * LDS-privatised small-table gradient (EmbeddingBag / nn.Embedding backward
+//     for tables of <= a few thousand rows: CVE tables, time / action / position
+//     tables, outcome conditioning);
+//   * query-tower token assembly (models/lthm/sequence/query_tower.py:89-111)
+//     and outcome conditioning (:118-122);
+//   * history flip (models/lthm/sequence/encoder.py:52-54, 60-61).
+#include "common.hpp"
+
+namespace lthm {
+
+// ------------------------------------------------------------------ flip
+__global__ void flip_k(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t B, int T) {
+  const int64_t n = B * T;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / T;
+    const int t = (int)(i - b * T);
+    out[b * T + (T - 1 - t)] = in[i];
+  }
+}
+
+// ------------------------------------------------------------------ product tower
+struct PTArgs {
+  lthm_ptower_desc d;
+};
+
+template <typename TX, typename TT, int OPL>
+__global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int total_idx) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Din = d.Din, Dout = d.Dout;
+  float* wT = reinterpret_cast<float*>(smem);            // [Din][Dout]
+  float* proj = wT + Din * Dout;                          // concatenated [Din][nproj_j]
+  float* grids = proj + d.proj_total;                     // concatenated
+  float* xs = grids + d.grid_total;                       // [4][2][Din]
+  uint16_t* rbuf = reinterpret_cast<uint16_t*>(xs + 8 * Din);  // [4][total_idx]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!d.cve_only)
+    for (int i = tid; i < Din * Dout; i += 256) {
+      const int o = i / Din, k = i - o * Din;
+      wT[k * Dout + o] = d.w_map[i];
+    }
+  for (int i = tid; i < d.proj_total; i += 256) proj[i] = d.proj[i];
+  for (int i = tid; i < d.grid_total; i += 256) grids[i] = d.grids[i];
+  __syncthreads();
+  // OPL = Dout / 64 outputs per lane (Dout in {64, 128, 256, 512})
+  float* xw = xs + wave * 2 * Din;
+  float* xw2 = xw + Din;
+  uint16_t* rw = rbuf + wave * total_idx;
+  const TT* tab = reinterpret_cast<const TT*>(d.tables);
+  const TT* hist = reinterpret_cast<const TT*>(d.hist);
+  for (int64_t tok = (int64_t)blockIdx.x * 4 + wave; tok < d.n; tok += (int64_t)gridDim.x * 4) {
+    // norm, mask, normalise (product_tower.py:47-51)
+    float xv = 0.f;
+    if (lane < Din) xv = Elem<TX>::ld(reinterpret_cast<const TX*>(d.x) + tok * Din + lane);
+    const float nrm = sqrtf(wave_sum(xv * xv));
+    const bool masked = !d.cve_only && ((nrm < d.norm_threshold) || (d.ids[tok] == 0));
+    const float xn = xv / fmaxf(nrm, 1e-12f);
+    float xn2 = xn;
+    if (!d.cve_only) {  // CosineVectorEmbedding re-normalises its already normalised input (layers.py:464)
+      const float nrm2 = sqrtf(wave_sum(xn * xn));
+      xn2 = xn / fmaxf(nrm2, 1e-12f);
+    }
+    if (lane < Din) {
+      xw[lane] = xn;
+      xw2[lane] = xn2;
+      if (d.xn_out) reinterpret_cast<bf16_t*>(d.xn_out)[tok * Din + lane] = f2bf(xn);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // bucket rows for all modules: lane handles (module, projection) pairs
+    int base = 0;
+    for (int j = 0; j < d.n_mod; ++j) {
+      const int np = d.mod_nproj[j], nb = d.mod_nbins[j];
+      const float* pj = proj + d.mod_proj_off[j];
+      const float* gj = grids + d.mod_grid_off[j];
+      for (int p = lane; p < np; p += 64) {
+        float z = 0.f;
+        for (int i = 0; i < Din; ++i) z = fmaf(xw2[i], pj[i * np + p], z);
+        int bk = 0;
+        for (int q = 0; q < nb; ++q) bk += (gj[q] < z) ? 1 : 0;  // bucketize(right=False)
+        const int row = d.mod_row_off[j] + (nb + 1) * p + bk;
+        rw[base + p] = (uint16_t)row;
+      }
+      base += np;
+    }
+    int hbin = -1;
+    if (d.norm_bins > 0) {
+      float f = floorf(nrm * (float)d.norm_bins);  // HistogramEmbedding(0, 1, nbins): uniform bins, clamped
+      hbin = (int)fminf(fmaxf(f, 0.f), (float)(d.norm_bins - 1));
+      if (lane == 0) rw[base] = (uint16_t)(d.cve_rows + hbin);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // emb_mapper Linear
+    float acc[OPL];
+    for (int q = 0; q < OPL; ++q) {
+      const int o = lane * OPL + q;
+      float s = 0.f;
+      if (!d.cve_only) {
+        s = d.b_map ? d.b_map[o] : 0.f;
+        for (int i = 0; i < Din; ++i) s = fmaf(xw[i], wT[i * Dout + o], s);
+      }
+      acc[q] = s;
+    }
+    // EmbeddingBag sums, module by module, then add (product_tower.py:53-54)
+    int rb = 0;
+    for (int j = 0; j < d.n_mod; ++j) {
+      const int np = d.mod_nproj[j];
+      float bag[OPL];
+      for (int q = 0; q < OPL; ++q) bag[q] = 0.f;
+      int p = 0;
+      for (; p + 4 <= np; p += 4) {
+        float v0[OPL], v1[OPL], v2[OPL], v3[OPL];
+        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lane * OPL;
+        const TT* r1 = tab + (int64_t)rw[rb + p + 1] * Dout + lane * OPL;
+        const TT* r2 = tab + (int64_t)rw[rb + p + 2] * Dout + lane * OPL;
+        const TT* r3 = tab + (int64_t)rw[rb + p + 3] * Dout + lane * OPL;
+        for (int q = 0; q < OPL; ++q) { v0[q] = Elem<TT>::ld(r0 + q); v1[q] = Elem<TT>::ld(r1 + q);
+                                        v2[q] = Elem<TT>::ld(r2 + q); v3[q] = Elem<TT>::ld(r3 + q); }
+        for (int q = 0; q < OPL; ++q) bag[q] = (((bag[q] + v0[q]) + v1[q]) + v2[q]) + v3[q];
+      }
+      for (; p < np; ++p) {
+        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lane * OPL;
+        for (int q = 0; q < OPL; ++q) bag[q] += Elem<TT>::ld(r0 + q);
+      }
+      for (int q = 0; q < OPL; ++q) acc[q] += bag[q];
+      rb += np;
+    }
+    if (hbin >= 0) {
+      const TT* hr = hist + (int64_t)hbin * Dout + lane * OPL;
+      for (int q = 0; q < OPL; ++q) acc[q] += Elem<TT>::ld(hr + q);
+    }
+    if (d.emb_dtype == LTHM_F32) {
+      float* eo = reinterpret_cast<float*>(d.emb_out) + tok * Dout + lane * OPL;
+      for (int q = 0; q < OPL; ++q) eo[q] = masked ? 0.f : acc[q];
+    } else {
+      bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out) + tok * Dout + lane * OPL;
+      for (int q = 0; q < OPL; ++q) eo[q] = f2bf(masked ? 0.f : acc[q]);
+    }
+    if (lane == 0 && d.mask_out) d.mask_out[tok] = masked ? 1 : 0;
+    if (d.rows_out) {
+      for (int i = lane; i < total_idx; i += 64) d.rows_out[tok * total_idx + i] = masked ? (uint16_t)0xffff : rw[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ small-table gradient
+// dW[rows[t, i]] += dY[t] for every token t and index slot i (0xffff = skip).
+// grid.x: column groups of CG columns, grid.y: token chunks.  Per block the
+// whole table slice [R, CG] is privatised in LDS (ds_add_f32), then flushed
+// with one global f32 add per touched (row, column).
+template <typename TY, int CG>
+__global__ __launch_bounds__(256) void small_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx, const TY* __restrict__ dY,
+                                                      int64_t ldy, int64_t n, int R, int D, float* __restrict__ dW,
+                                                      int64_t tok_per_block) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* acc = reinterpret_cast<float*>(smem);  // [R][CG]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < R * CG; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const int c = tid % CG;
+  const int tl = tid / CG;
+  constexpr int TPAR = 256 / CG;
+  const int col = blockIdx.x * CG + c;
+  const int64_t t0 = (int64_t)blockIdx.y * tok_per_block;
+  const int64_t t1 = min(n, t0 + tok_per_block);
+  if (col < D) {
+    for (int64_t t = t0 + tl; t < t1; t += TPAR) {
+      const uint16_t* rr = rows + t * nidx;
+      const float v = Elem<TY>::ld(dY + t * ldy + col);
+      if (v == 0.f) continue;
+      for (int i = 0; i < nidx; ++i) {
+        const uint16_t r = rr[i];
+        if (r != 0xffff) atomicAdd(&acc[r * CG + c], v);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < R * CG; i += 256) {
+    const float v = acc[i];
+    const int r = i / CG, cc = i - r * CG;
+    const int cl = blockIdx.x * CG + cc;
+    if (v != 0.f && cl < D) atomicAdd(dW + (int64_t)r * D + cl, v);
+  }
+}
+
+// ------------------------------------------------------------------ token assembly
+// x0[b, 0]   = wpe[T] (+ ctx[b])
+// x0[b, t+1] = (mask ? pad : P[b,t] + act[lab] + hod[.] + how[.] + dow[.]) + wpe[T-1-t]
+template <typename TP>
+__global__ __launch_bounds__(256) void tokens_fwd_k(lthm_tokens_desc d) {
+  const int T = d.T_full - d.trim, Tp = T + 1, D = d.d;
+  const int64_t rows = d.B * Tp;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t b = r / Tp;
+    const int tp = (int)(r - b * Tp);
+    uint16_t ri[5] = {0xffff, 0xffff, 0xffff, 0xffff, 0xffff};
+    const int wrow = T - tp;  // pos = seq_len - arange(0, seq_len + 1)
+    ri[4] = (uint16_t)(d.off_wpe + wrow);
+    bool masked = false;
+    int64_t ia = 0, ih = 0, iw = 0, idw = 0;
+    int64_t src = -1;
+    if (tp > 0) {
+      const int64_t g = b * d.T_full + d.trim + (tp - 1);
+      masked = d.mask[g] != 0;
+      if (!masked) {
+        ia = pymod64(d.labels[g], 4);
+        const int64_t ts = d.ts[g];
+        ih = pymod64(floordiv64(ts, d.div_hod), d.mod_hod);
+        iw = pymod64(floordiv64(ts, d.div_how), d.mod_how);
+        idw = pymod64(floordiv64(ts, d.div_dow), d.mod_dow);
+        ri[0] = (uint16_t)(d.off_act + ia);
+        ri[1] = (uint16_t)(d.off_hod + ih);
+        ri[2] = (uint16_t)(d.off_how + iw);
+        ri[3] = (uint16_t)(d.off_dow + idw);
+        src = b * T + (tp - 1);
+      } else {
+        ri[0] = (uint16_t)d.off_pad;
+      }
+    }
+    for (int c = lane; c < D; c += 64) {
+      float v;
+      if (tp == 0) {
+        v = d.ctx ? d.ctx[b * D + c] : 0.f;
+      } else if (masked) {
+        v = d.pad[c];
+      } else {
+        v = Elem<TP>::ld(reinterpret_cast<const TP*>(d.P) + src * D + c);
+        v = v + d.act[ia * D + c] + d.hod[ih * D + c] + d.how[iw * D + c] + d.dow[idw * D + c];
+      }
+      v = v + d.wpe[(int64_t)wrow * D + c];
+      d.x0[r * D + c] = v;
+    }
+    if (d.rows_out && lane < 5) d.rows_out[r * 5 + lane] = ri[lane];
+  }
+}
+
+// dP[b, t] = mask ? 0 : dx0[b, t+1] (bf16), dctx[b] = dx0[b, 0]
+__global__ __launch_bounds__(256) void tokens_bwd_k(lthm_tokens_desc d, const float* __restrict__ dx0, bf16_t* __restrict__ dP,
+                                                    float* __restrict__ dctx) {
+  const int T = d.T_full - d.trim, Tp = T + 1, D = d.d;
+  const int64_t rows = d.B * Tp;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t b = r / Tp;
+    const int tp = (int)(r - b * Tp);
+    if (tp == 0) {
+      if (dctx)
+        for (int c = lane; c < D; c += 64) dctx[b * D + c] = dx0[r * D + c];
+      continue;
+    }
+    const bool masked = d.mask[b * d.T_full + d.trim + tp - 1] != 0;
+    for (int c = lane; c < D; c += 64) dP[(b * T + tp - 1) * D + c] = f2bf(masked ? 0.f : dx0[r * D + c]);
+  }
+}
+
+// out[b, t'] = bf16(x[b, t'] + oc[outcome(b, t')]);  outcome = label of token t' (t' < T), future (t' = T)
+__global__ __launch_bounds__(256) void outcome_fwd_k(const float* __restrict__ x, const int64_t* __restrict__ labels, int64_t B,
+                                                     int T_full, int trim, int64_t future, const float* __restrict__ oc,
+                                                     int noc, int D, bf16_t* __restrict__ out, uint16_t* __restrict__ rows) {
+  const int T = T_full - trim, Tp = T + 1;
+  const int64_t nrow = B * Tp;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nrow; r += (int64_t)gridDim.x * 4) {
+    const int64_t b = r / Tp;
+    const int tp = (int)(r - b * Tp);
+    const int64_t lab = (tp < T) ? labels[b * T_full + trim + tp] : future;
+    const int64_t o = pymod64(lab, noc);
+    for (int c = lane; c < D; c += 64) out[r * D + c] = f2bf(x[r * D + c] + oc[o * D + c]);
+    if (lane == 0 && rows) rows[r] = (uint16_t)o;
+  }
+}
+
+}  // namespace lthm
+
+using namespace lthm;
+
+extern "C" int lthm_flip_tokens(const int64_t* in, int64_t* out, int64_t B, int32_t T, void* stream) {
+  LTHM_REQUIRE(B >= 0 && T >= 0 && in != out);
+  if (B * T == 0) return 0;
+  hipLaunchKernelGGL(flip_k, dim3(grid_for(B * T, 256)), dim3(256), 0, (hipStream_t)stream, in, out, B, T);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
+  LTHM_REQUIRE(d && d->n >= 0 && d->Din > 0 && d->Din <= 64 && d->n_mod >= 0 && d->n_mod <= LTHM_MAX_CVE);
+  LTHM_REQUIRE(d->Dout % 64 == 0 && d->Dout <= 512);
+  if (d->n == 0) return 0;
+  int total = 0;
+  for (int j = 0; j < d->n_mod; ++j) total += d->mod_nproj[j];
+  total += d->norm_bins > 0 ? 1 : 0;
+  LTHM_REQUIRE(total <= 1024);
+  const size_t sh = (size_t)(d->Din * d->Dout + d->proj_total + d->grid_total + 8 * d->Din) * 4 + (size_t)4 * total * 2 + 16;
+  LTHM_REQUIRE(sh <= 160 * 1024);
+  const int grid = grid_for(d->n, 4, 256 * 8);
+  hipStream_t s = (hipStream_t)stream;
+  const int opl = d->Dout / 64;
+#define LTHM_PT(TX, TT)                                                                                   \
+  if (opl == 1) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 1>), dim3(grid), dim3(256), sh, s, *d, total);    \
+  else if (opl == 2) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 2>), dim3(grid), dim3(256), sh, s, *d, total); \
+  else if (opl == 4) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 4>), dim3(grid), dim3(256), sh, s, *d, total); \
+  else hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 8>), dim3(grid), dim3(256), sh, s, *d, total);
+  LTHM_REQUIRE(opl == 1 || opl == 2 || opl == 4 || opl == 8);
+  if (d->x_dtype == LTHM_BF16 && d->tab_dtype == LTHM_BF16) { LTHM_PT(bf16_t, bf16_t) }
+  else if (d->x_dtype == LTHM_F32 && d->tab_dtype == LTHM_F32) { LTHM_PT(float, float) }
+  else if (d->x_dtype == LTHM_BF16 && d->tab_dtype == LTHM_F32) { LTHM_PT(bf16_t, float) }
+  else { LTHM_PT(float, bf16_t) }
+#undef LTHM_PT
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,
+                                    int64_t n, int32_t R, int32_t D, float* dW, void* stream) {
+  LTHM_REQUIRE(n >= 0 && nidx > 0 && R > 0 && D > 0 && R < 0xffff);
+  if (n == 0) return 0;
+  int CG = 16;
+  while (CG > 1 && (size_t)R * CG * 4 > 96 * 1024) CG >>= 1;
+  LTHM_REQUIRE((size_t)R * CG * 4 <= 96 * 1024);
+  const int gx = (D + CG - 1) / CG;
+  int64_t gy = 2048 / gx;
+  if (gy < 1) gy = 1;
+  int64_t tpb = (n + gy - 1) / gy;
+  if (tpb < 64) tpb = 64;
+  gy = (n + tpb - 1) / tpb;
+  const size_t sh = (size_t)R * CG * 4;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(gx, (unsigned)gy);
+#define LTHM_STB(CGV)                                                                                          \
+  if (CG == CGV) {                                                                                             \
+    if (dy_dtype == LTHM_F32)                                                                                  \
+      hipLaunchKernelGGL((small_tab_bwd_k<float, CGV>), grid, dim3(256), sh, s, rows, nidx, (const float*)dY,  \
+                         ldy, n, R, D, dW, tpb);                                                               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((small_tab_bwd_k<bf16_t, CGV>), grid, dim3(256), sh, s, rows, nidx, (const bf16_t*)dY, \
+                         ldy, n, R, D, dW, tpb);                                                               \
+  }
+  LTHM_STB(16) else LTHM_STB(8) else LTHM_STB(4) else LTHM_STB(2) else LTHM_STB(1)
+#undef LTHM_STB
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_tokens_fwd(const lthm_tokens_desc* d, void* stream) {
+  LTHM_REQUIRE(d && d->B >= 0 && d->T_full > 0 && d->trim >= 0 && d->trim < d->T_full && d->d > 0);
+  if (d->B == 0) return 0;
+  const int64_t rows = d->B * (d->T_full - d->trim + 1);
+  hipStream_t s = (hipStream_t)stream;
+  if (d->p_dtype == LTHM_BF16)
+    hipLaunchKernelGGL((tokens_fwd_k<bf16_t>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, *d);
+  else
+    hipLaunchKernelGGL((tokens_fwd_k<float>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, *d);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_tokens_bwd(const lthm_tokens_desc* d, const float* dx0, void* dP, float* dctx, void* stream) {
+  LTHM_REQUIRE(d && d->B >= 0);
+  if (d->B == 0) return 0;
+  const int64_t rows = d->B * (d->T_full - d->trim + 1);
+  hipLaunchKernelGGL(tokens_bwd_k, dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, (hipStream_t)stream, *d, dx0,
+                     (bf16_t*)dP, dctx);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_outcome_fwd(const float* x, const int64_t* labels, int64_t B, int32_t T_full, int32_t trim,
+                                int64_t future, const float* table, int32_t n_outcomes, int32_t D, void* out,
+                                uint16_t* rows, void* stream) {
+  LTHM_REQUIRE(B >= 0 && T_full > 0 && trim >= 0 && trim < T_full && n_outcomes > 0);
+  if (B == 0) return 0;
+  const int64_t nrow = B * (T_full - trim + 1);
+  hipLaunchKernelGGL(outcome_fwd_k, dim3(grid_for(nrow, 4, 256 * 8)), dim3(256), 0, (hipStream_t)stream, x, labels, B,
+                     T_full, trim, future, table, n_outcomes, D, (bf16_t*)out, rows);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -241,3 +241,203 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
     if part is not None:
         dtab = colsum(part.view(B, (2 * T + 1) * H)).view(2 * T + 1, H)
     return dqkv, dtab
+
+
+# ----------------------------------------------------------------- sparse KShift backward
+def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count):
+    """Accumulate into dense dW and append the touched rows (see include/lthm.h)."""
+    n = ids.numel() // F
+    D = dW.shape[1]
+    call("lthm_kshift_bwd_sparse", ptr(ids), n, F, ptr(gy), dcode(gy),
+         ptr(out) if out is not None else None, dcode(out) if out is not None else F32, ptr(norms),
+         P, D, K, mode, ptr(dW), ptr(flags), ptr(rows_list), ptr(count), stream())
+
+
+# ----------------------------------------------------------------- optimizers / norms
+def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, zero_grad=False):
+    call("lthm_adamw", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, betas[0], betas[1], eps, wd, step,
+         grad_scale, ptr(shadow), int(zero_grad), stream())
+
+
+def adagrad_(p, g, s, lr, lr_decay, eps, wd, step, zero_grad=False):
+    call("lthm_adagrad", ptr(p), ptr(g), ptr(s), p.numel(), lr, lr_decay, eps, wd, step, int(zero_grad), stream())
+
+
+def sparse_adamw_(rows, count, max_rows, p, g, m, v, flags, lr, betas, eps, wd, step, shadow=None):
+    call("lthm_sparse_adamw", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(m), ptr(v),
+         ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), stream())
+
+
+def sparse_adagrad_(rows, count, max_rows, p, g, s, flags, lr, lr_decay, eps, step, shadow=None):
+    call("lthm_sparse_adagrad", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(s), ptr(flags),
+         lr, lr_decay, eps, step, ptr(shadow), stream())
+
+
+def sumsq(x, acc):
+    call("lthm_sumsq", ptr(x), dcode(x), x.numel(), ptr(acc), stream())
+
+
+def scale_by_norm(x, y, ss, add_eps=1e-6, max_norm=0.0):
+    call("lthm_scale_by_norm", ptr(x), ptr(y), dcode(x), x.numel(), ptr(ss), add_eps, max_norm, stream())
+
+
+class CapGradientsFn(torch.autograd.Function):
+    """commons/functional.py:4-25: identity forward, g / (||g||_2 + 1e-6) backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        require_gpu(x)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        ss = torch.zeros(1, dtype=torch.float32, device=g.device)
+        sumsq(g, ss)
+        out = torch.empty_like(g)
+        scale_by_norm(g, out, ss, add_eps=1e-6)
+        return out
+
+
+# ----------------------------------------------------------------- towers
+def flip_tokens(x):
+    require_gpu(x)
+    out = torch.empty_like(x)
+    B, T = x.shape
+    call("lthm_flip_tokens", ptr(x), ptr(out), B, T, stream())
+    return out
+
+
+def small_table_bwd(rows, dY, R, out=None):
+    """rows uint16 stored as int16 [n, nidx]; dY [n, D] -> f32 [R, D] (accumulated into out)."""
+    n, nidx = rows.shape
+    D = dY.shape[-1]
+    if out is None:
+        out = torch.zeros((R, D), dtype=torch.float32, device=dY.device)
+    call("lthm_small_table_bwd", ptr(rows), nidx, ptr(dY), dcode(dY), D, n, R, D, ptr(out), stream())
+    return out
+
+
+def rownorm(x2d):
+    rows, D = x2d.shape
+    out = torch.empty((rows, D), dtype=torch.bfloat16, device=x2d.device)
+    norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    call("lthm_rownorm", ptr(x2d), dcode(x2d), rows, D, ptr(out), ptr(norms), stream())
+    return out, norms
+
+
+def rownorm_bwd(x2d, norms, g, want_f32=False):
+    rows, D = x2d.shape
+    dxb = torch.empty((rows, D), dtype=torch.bfloat16, device=x2d.device)
+    dxf = torch.empty((rows, D), dtype=torch.float32, device=x2d.device) if want_f32 else None
+    call("lthm_rownorm_bwd", ptr(x2d), dcode(x2d), ptr(norms), ptr(g), rows, D, ptr(dxb), ptr(dxf), stream())
+    return dxb, dxf
+
+
+# ----------------------------------------------------------------- MLP chains
+class MLPChainFn(torch.autograd.Function):
+    """x -> Linear -> act -> Linear -> act ... -> Linear (acts[i] after layer i; last is ACT_NONE).
+
+    Every Linear is one MFMA GEMM with the bias and activation fused in its
+    epilogue; the backward fuses act' into the preceding dgrad GEMM.  Serves
+    commons/layers.py:65-81 (QuickGELU gates) and commons/transformers/layers.py:67-81.
+    """
+
+    @staticmethod
+    def forward(ctx, x, acts, out_f32, *wb):
+        require_gpu(x)
+        shp = x.shape
+        h = x.contiguous().view(-1, shp[-1])
+        h = h if h.dtype == torch.bfloat16 else cast(h, torch.bfloat16)
+        n = len(wb) // 2
+        ws = [cast(wb[2 * i].detach().contiguous(), torch.bfloat16) for i in range(n)]
+        hs, pres = [h], []
+        for i in range(n):
+            last = i == n - 1
+            b = wb[2 * i + 1]
+            pre = None
+            if acts[i] != ACT_NONE:
+                pre = torch.empty((h.shape[0], ws[i].shape[0]), dtype=torch.bfloat16, device=x.device)
+            h = linear_fwd(h, ws[i], bias=None if b is None else b.detach().contiguous(), act=acts[i], aux_out=pre,
+                           out_dtype=torch.float32 if (last and out_f32) else torch.bfloat16)
+            pres.append(pre)
+            if not last:
+                hs.append(h)
+        ctx.save_for_backward(*hs, *[p for p in pres if p is not None], *ws)
+        ctx.meta = (n, acts, [p is not None for p in pres], [wb[2 * i + 1] is not None for i in range(n)], shp,
+                    x.dtype)
+        return h.view(*shp[:-1], h.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, acts, has_pre, has_b, shp, xdt = ctx.meta
+        saved = ctx.saved_tensors
+        hs = saved[:n]
+        npre = sum(has_pre)
+        pre_list = list(saved[n:n + npre])
+        ws = saved[n + npre:]
+        pres = []
+        it = iter(pre_list)
+        for hp in has_pre:
+            pres.append(next(it) if hp else None)
+        g = dy.contiguous().view(-1, dy.shape[-1])
+        gb = g if g.dtype == torch.bfloat16 else cast(g, torch.bfloat16)
+        grads = [None] * (2 * n)
+        dx = None
+        for i in range(n - 1, -1, -1):
+            grads[2 * i] = linear_wgrad(gb, hs[i])
+            if has_b[i]:
+                grads[2 * i + 1] = colsum(gb)
+            if i > 0:
+                ag = {ACT_GELU: ACT_GELU_GRAD, ACT_QGELU: ACT_QGELU_GRAD}.get(acts[i - 1], ACT_NONE)
+                gb = linear_dgrad(gb, ws[i], act_grad=ag, aux=pres[i - 1])
+            else:
+                dx = linear_dgrad(gb, ws[0], out_dtype=torch.float32 if xdt == torch.float32 else torch.bfloat16)
+        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, *grads)
+
+
+def mlp_chain(x, linears, acts, out_f32=True):
+    wb = []
+    for lin in linears:
+        wb += [lin.weight, lin.bias]
+    return MLPChainFn.apply(x, tuple(acts), out_f32, *wb)
+
+
+class ActivationFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        require_gpu(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("lthm_activation", ptr(x), None, ptr(y), dcode(x), x.numel(), act, stream())
+        ctx.save_for_backward(x)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        dx = torch.empty_like(x)
+        call("lthm_activation", ptr(x), ptr(dy), ptr(dx), dcode(x), x.numel(), ctx.act, stream())
+        return dx, None
+
+
+def zeros(shape, dtype, device):
+    """Zero-filled tensor (f32 through the HIP fill kernel; other dtypes via memset)."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if dtype == torch.float32:
+        call("lthm_fill_f32", ptr(t), 0.0, t.numel(), stream())
+    else:
+        t.zero_()
+    return t
+
+
+def quantile_map(x, quantiles, shared):
+    """QuantileMapper (commons/transformers/layers.py:484-487) on x [B, F]:
+    bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [1 or F, nq]."""
+    require_gpu(x, quantiles)
+    B, Fd = x.shape if x.dim() == 2 else (x.numel(), 1)
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    call("lthm_quantile_map", ptr(x), B, Fd, ptr(quantiles), quantiles.shape[-1], int(shared), ptr(out), stream())
+    return out

@@ -1,0 +1,68 @@
+"""Encoder — drop-in for models/lthm/sequence/encoder.py:18-61.
+
+``product_emb_module`` is the item KShiftEmbedding (encoder.py:32-37; bf16
+table, normalised output, forward-only because product_tower.py:47 detaches
+it).  The history is flipped to left padding first (encoder.py:52-54) —
+equivalent to the reference's flip after the per-token product tower.
+``user_context`` (build-defined, BASELINE C2-C4 categorical features):
+table-batched KShift lookups -> cap_gradients -> MLP(QuickGELU) -> CLS token.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+import torch.nn as nn
+
+from .... import kernels as K
+from ....commons.functional import cap_gradients
+from ....commons.layers import KShiftEmbedding, MLP, TableBatchedKShiftEmbedding
+from .product_tower import ProductTower
+from .query_tower import QueryTower
+
+
+class UserContext(nn.Module):
+    def __init__(self, cfg, d_model: int):
+        super().__init__()
+        self.tables = TableBatchedKShiftEmbedding(cfg.n_features, cfg.vocab_size, cfg.emb_dim, cfg.num_shifts,
+                                                  normalize_output=False, sparse=True,
+                                                  gather_dtype=torch.bfloat16 if cfg.gather_bf16 else torch.float32,
+                                                  out_dtype=torch.bfloat16)
+        with torch.no_grad():
+            self.tables.weight.normal_(0.0, 1.0)
+        self.mlp = MLP(cfg.n_features * cfg.emb_dim, d_model, cfg.gate_sizes)
+
+    def forward(self, cat_ids: torch.Tensor) -> torch.Tensor:
+        B = cat_ids.shape[0]
+        e = self.tables(cat_ids)                       # [B, F, Dc] bf16
+        e = cap_gradients(e.view(B, -1))               # commons/functional.py:28
+        return self.mlp(e)                             # [B, d] f32
+
+
+class Encoder(nn.Module):
+    def __init__(self, model_config):
+        super().__init__()
+        pt = model_config.product_tower
+        if pt.model_init_metadata is not None:
+            raise NotImplementedError("TorchScript item-embedding artifacts are loaded via load_item_artifact()")
+        lm = pt.latent_model_config
+        self.product_emb_module = KShiftEmbedding(lm.vocab_size_latent, pt.inp_emb_dim, num_shifts=lm.num_shifts_latent,
+                                                  normalize_output=lm.normalize_embedding,
+                                                  out_dtype=torch.bfloat16 if model_config.item_table_bf16 else None)
+        if model_config.item_table_bf16:
+            self.product_emb_module.emb.weight.data = self.product_emb_module.emb.weight.data.to(torch.bfloat16)
+        self.product_emb_module.emb.weight.requires_grad_(False)  # detached by product_tower.py:47
+        self.product_tower = ProductTower(model_config)
+        self.query_tower = QueryTower(model_config)
+        self.user_context = UserContext(model_config.categorical, model_config.emb_dim) \
+            if model_config.categorical.n_features > 0 else None
+
+    def forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        ids = K.flip_tokens(batch["product_ids"].contiguous())
+        labels = K.flip_tokens(batch["labels"].contiguous())
+        ts = K.flip_tokens(batch["timestamp"].contiguous())
+        with torch.no_grad():
+            embs = self.product_emb_module(ids)
+        inp, target, mask = self.product_tower(ids, embs)
+        ctx = self.user_context(batch["categorical_ids"]) if self.user_context is not None else None
+        return self.query_tower(inp, target, mask, labels, ts, ids, ctx)

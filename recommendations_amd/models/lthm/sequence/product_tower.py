@@ -1,0 +1,116 @@
+"""ProductTower — drop-in for models/lthm/sequence/product_tower.py:10-62.
+
+Module tree and parameter names follow the reference (``emb_mapper``,
+``direction_emb.{j}.emb.weight`` + buffers, ``norm_emb.emb.weight``,
+``product_mapper.weight``).  The forward is one fused gfx950 kernel per token
+(``lthm_product_tower_fwd``) plus the product_mapper MFMA GEMM; the backward
+is an LDS-privatised scatter into the 6 CVE tables + histogram table and two
+weight-gradient GEMMs.  Bug resolutions: #1 HistogramEmbedding
+is build-defined (commons/layers.py here), #2 ``num_proj`` maps to ``n_proj``,
+#3 the config fields are declared (models/lthm/config.py).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from .... import kernels as K
+from ...._lib import STRUCTS, call, dcode, ptr, require_gpu, stream
+from ....commons.layers import HistogramEmbedding
+from ....commons.transformers.layers import CosineVectorEmbedding
+
+
+class ProductTowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, x, w_map, b_map, w_pm, hist_w, tower, *tables):
+        require_gpu(ids, x)
+        n = ids.numel()
+        Din, Dout = x.shape[-1], w_map.shape[0]
+        dev = x.device
+        cve = tower.direction_emb
+        R_cve = sum(t.shape[0] for t in tables)
+        nb = tower.norm_bins if tower.norm_bins > 1 else 0
+        # bf16 gather images of the small tables (cast kernel into one buffer)
+        tab = torch.empty((R_cve + max(nb, 1), Dout), dtype=torch.bfloat16, device=dev)
+        r = 0
+        for t in tables:
+            call("lthm_cast", ptr(t), dcode(t), ptr(tab[r]), dcode(tab), t.numel(), stream())
+            r += t.shape[0]
+        if nb:
+            call("lthm_cast", ptr(hist_w), dcode(hist_w), ptr(tab[R_cve]), dcode(tab), hist_w.numel(), stream())
+        proj = torch.cat([m.projection_mat.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
+        grids = torch.cat([m.grid.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
+        total = sum(m.n_proj for m in cve) + (1 if nb else 0)
+        emb = torch.empty((n, Dout), dtype=torch.bfloat16, device=dev)
+        rows = torch.empty((n, total), dtype=torch.int16, device=dev)
+        xn = torch.empty((n, Din), dtype=torch.bfloat16, device=dev)
+        mask = torch.empty(n, dtype=torch.uint8, device=dev)
+        d = STRUCTS["lthm_ptower_desc"]()
+        d.ids, d.x, d.x_dtype, d.Din, d.n, d.Dout = ptr(ids), ptr(x), dcode(x), Din, n, Dout
+        d.n_mod = len(cve)
+        d.w_map, d.b_map = ptr(w_map.detach()), ptr(b_map.detach()) if b_map is not None else None
+        d.proj, d.grids = ptr(proj), ptr(grids)
+        d.tables, d.hist, d.tab_dtype = ptr(tab), ptr(tab[R_cve]) if nb else None, dcode(tab)
+        d.proj_total, d.grid_total, d.cve_rows, d.norm_bins = proj.numel(), grids.numel(), R_cve, nb
+        d.norm_threshold, d.cve_only, d.emb_dtype = float(tower.norm_threshold), 0, dcode(emb)
+        ro = po = go = 0
+        for j, m in enumerate(cve):
+            d.mod_nproj[j], d.mod_nbins[j] = m.n_proj, m.num_bins
+            d.mod_row_off[j], d.mod_proj_off[j], d.mod_grid_off[j] = ro, po, go
+            ro += (m.num_bins + 1) * m.n_proj
+            po += m.projection_mat.numel()
+            go += m.grid.numel()
+        d.emb_out, d.rows_out, d.xn_out, d.mask_out = ptr(emb), ptr(rows), ptr(xn), ptr(mask)
+        call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
+        w_pm_b = K.cast(w_pm.detach().contiguous(), torch.bfloat16)
+        prod = K.linear_fwd(emb, w_pm_b)
+        ctx.save_for_backward(rows, xn, emb, w_pm_b)
+        ctx.meta = (R_cve, nb, [t.shape for t in tables], b_map is not None)
+        ctx.mark_non_differentiable(mask)
+        return emb.view(*ids.shape, Dout), prod.view(*ids.shape, -1), mask.view(ids.shape)
+
+    @staticmethod
+    def backward(ctx, d_emb, d_prod, _dmask):
+        rows, xn, emb, w_pm_b = ctx.saved_tensors
+        R_cve, nb, shapes, has_b = ctx.meta
+        Dout = emb.shape[1]
+        dpb = d_prod.contiguous().view(-1, d_prod.shape[-1])
+        dpb = dpb if dpb.dtype == torch.bfloat16 else K.cast(dpb, torch.bfloat16)
+        dw_pm = K.linear_wgrad(dpb, emb)
+        res = None if d_emb is None else d_emb.contiguous().view(-1, Dout)
+        de = K.linear_dgrad(dpb, w_pm_b, res1=res)  # bf16 total gradient of `emb`
+        dw_map = K.linear_wgrad(de, xn)
+        db_map = K.colsum(de) if has_b else None
+        dtab = K.small_table_bwd(rows, de, R_cve + max(nb, 1))
+        grads, r = [], 0
+        for s in shapes:
+            grads.append(dtab[r:r + s[0]])
+            r += s[0]
+        dhist = dtab[R_cve:R_cve + nb] if nb else None
+        return (None, None, dw_map, db_map, dw_pm, dhist, None, *grads)
+
+
+class ProductTower(nn.Module):
+    def __init__(self, model_config):
+        super().__init__()
+        tc = model_config.product_tower
+        self.inp_emb_dim, self.out_emb_dim = tc.inp_emb_dim, tc.out_emb_dim
+        self.norm_threshold, self.norm_bins = tc.norm_threshold, tc.norm_bins
+        self.emb_mapper = nn.Linear(tc.inp_emb_dim, tc.out_emb_dim)
+        self.direction_emb = nn.ModuleList([
+            CosineVectorEmbedding(tc.inp_emb_dim, tc.out_emb_dim, n_proj=c.num_proj, num_bins=c.num_bins)
+            for c in tc.cosine_lsh_config])
+        if self.norm_bins > 1:
+            self.norm_emb = HistogramEmbedding(0, 1, tc.norm_bins, emb_dim=tc.out_emb_dim)
+        self.product_mapper = nn.Linear(tc.out_emb_dim, tc.product_emb_dim, bias=False)
+
+    def forward(self, ids: torch.Tensor, x: torch.Tensor):
+        """ids [B, T] int64, x [B, T, inp_emb_dim] (item embedding; detached as in
+        product_tower.py:47) -> (emb [B, T, out] bf16, prod_emb [B, T, P_e] bf16, mask [B, T] uint8)."""
+        x = x.detach().contiguous()
+        hist = self.norm_emb.emb.weight if self.norm_bins > 1 else None
+        return ProductTowerFn.apply(ids.contiguous(), x, self.emb_mapper.weight, self.emb_mapper.bias,
+                                    self.product_mapper.weight, hist, self,
+                                    *[m.emb.weight for m in self.direction_emb])

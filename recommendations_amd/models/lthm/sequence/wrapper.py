@@ -1,0 +1,237 @@
+"""LTHMModelWrapper — drop-in for models/lthm/sequence/wrapper.py:16-275.
+
+Same BaseModelWrapper surface: ``forward(batch) -> dict``, ``train_step``,
+``val_step``, ``optim_group``, ``optimizers_for_param_groups``.  The loss of
+``_mini_batch_mapper`` + ``_train_or_val_step_helper`` (wrapper.py:78-245) is
+one fused op over all mini-batches (``ContrastiveLossFn``, csrc/loss.hip):
+identical math per 32-sequence mini-batch and lookahead head, with the
+lookahead offsets drawn per mini-batch exactly as wrapper.py:147-153 does
+(from a seeded ``random.Random`` instead of the global ``random``).
+
+Bug resolutions: #11 ``self._model_config`` -> ``self.model_config``;
+#12 ``current_token_id`` -> ``current_token_ids``; #13 ``sparse`` /
+``log_q_config`` / ``loss_type`` declared in the config.  The logQ correction is
+applied only when ``log_q_config.beta != 0`` (the shipped YAML has beta = 0, so
+its lookups cannot change the loss).
+"""
+from __future__ import annotations
+
+import ctypes
+import random
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .... import kernels as K
+from ...._lib import STRUCTS, call, ptr, stream
+from ....commons.base_model_wrapper import BaseModelWrapper
+from ....optim import FusedAdamW, SparseRowAdamW
+from .encoder import Encoder
+
+NSTAT_BASE = 7
+
+
+class ContrastiveLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, target, mask, offsets_dev, cfg):
+        """y [B, T+1, NH, De] (next_token_emb), target [B, T, De] (current_token_emb),
+        mask [B, T] uint8 (row stride = mask.stride(0)), offsets_dev int32 [n_mb, NH]."""
+        B, Tp, NH, De = y.shape
+        T = Tp - 1
+        mbs, tau, ks = cfg["mb"], cfg["tau"], cfg["ks"]
+        n_mb = (B + mbs - 1) // mbs
+        n_max = ((mbs * T + 63) // 64) * 64
+        dev = y.device
+        yc = y.contiguous()
+        tc = target.contiguous()
+        yn, ynorm = K.rownorm(yc.view(-1, De))
+        tn, tnorm = K.rownorm(tc.view(-1, De))
+        f32 = dict(dtype=torch.float32, device=dev)
+        lse = torch.empty((NH, n_mb, n_max), **f32)
+        pos = torch.empty((NH, n_mb, n_max), **f32)
+        diag = torch.empty((NH, n_mb, n_max), **f32)
+        w = torch.empty((NH, n_mb, n_max), **f32)
+        cnt = torch.empty((NH, n_mb, n_max), dtype=torch.int32, device=dev)
+        rank = torch.empty((NH, n_mb, n_max), dtype=torch.int32, device=dev)
+        nstat = NSTAT_BASE + len(ks)
+        stats = torch.empty((NH, n_mb, nstat), **f32)
+        ks_dev = torch.tensor(ks, dtype=torch.int32).to(dev, non_blocking=True)
+        descs = []
+        for h in range(NH):
+            d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
+                                        lse[h], pos[h], cnt[h], rank[h], diag[h], w[h])
+            call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats[h]), nstat, ptr(ks_dev), len(ks),
+                 1.0 / n_mb, stream())
+            descs.append(d)
+        # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
+        loss = torch.empty(1, **f32)
+        call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
+        loss = loss / n_mb
+        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, mask, offsets_dev)
+        ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
+        ctx.stats = stats
+        return loss
+
+    @staticmethod
+    def _desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev, lse, pos, cnt, rank, diag, w):
+        d = STRUCTS["lthm_contrastive_desc"]()
+        d.out_n, d.in_n, d.mask, d.mask_stride = ptr(yn), ptr(tn), ptr(mask), mask.stride(0)
+        d.B, d.T, d.n_heads, d.head, d.De = B, T, NH, h, De
+        d.mb_size, d.n_mb, d.n_max, d.tau = mbs, n_mb, n_max, tau
+        d.offsets = ptr(offsets_dev)
+        d.lse, d.pos, d.cnt, d.rank, d.diag, d.w = ptr(lse), ptr(pos), ptr(cnt), ptr(rank), ptr(diag), ptr(w)
+        return d
+
+    @staticmethod
+    def backward(ctx, dloss):
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, mask, offsets_dev = ctx.saved_tensors
+        B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
+        dev = yc.device
+        g = dloss.contiguous().float()
+        d_out = K.zeros((B, T + 1, NH, De), torch.float32, dev)
+        d_in = K.zeros((B, T, De), torch.float32, dev)
+        for h in range(NH):
+            d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
+                                        lse[h], None, None, None, None, w[h])
+            d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
+            call("lthm_contrastive_bwd", ctypes.addressof(d), stream())
+        dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
+        dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
+        return dy.view(yc.shape), dt.view(tc.shape), None, None, None
+
+
+class LTHMModelWrapper(BaseModelWrapper):
+    def __init__(self, model_config, stats=None):
+        super().__init__(dummy_params=model_config.sparse, sparse=model_config.sparse)
+        self.model_config = model_config
+        self._sparse = model_config.sparse
+        self._softmax_temperature = model_config.softmax_temperature
+        self._export_span = model_config.export_span
+        self._export_tokens = model_config.export_tokens
+        self._loss_type = model_config.loss_type
+        self._metrics_k_all = list(model_config.metrics_k_all)
+        self._lookahead = list(model_config.lookahead)
+        self._log_q_beta = model_config.log_q_config.beta
+        if self._log_q_beta != 0.0:
+            raise NotImplementedError("log_q_config.beta != 0: logQ-corrected logits are not fused yet")
+        self._model = Encoder(model_config)
+        self.batch_idx = 0
+        self._rng = random.Random(model_config.seed)
+        self.last_stats = None
+
+    # wrapper.py:48-64
+    def format_inputs(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        for k in ("product_ids", "labels", "timestamp"):
+            assert batch[k].dtype == torch.int64, f"{k} was expected to be of type long but was {batch[k].dtype}"
+        return batch
+
+    def forward(self, batch: Dict[str, torch.Tensor]):
+        return self._model(self.format_inputs(batch))
+
+    def draw_offsets(self, n_mb: int) -> np.ndarray:
+        """wrapper.py:147-153, once per mini-batch: head 0 uses lookahead[0], head i
+        draws randint(previous + 1, lookahead[i])."""
+        out = np.zeros((n_mb, len(self._lookahead)), dtype=np.int32)
+        for mb in range(n_mb):
+            prev = 0
+            for i, mx in enumerate(self._lookahead):
+                if i == 0:
+                    off = mx
+                else:
+                    off = self._rng.randint(prev + 1, mx)
+                prev = off
+                out[mb, i] = off
+        return out
+
+    def train_step(self, batch, output):
+        return self._loss_and_metrics(output, "train")
+
+    def val_step(self, batch, output):
+        return self._loss_and_metrics(output, "val")
+
+    def _loss_and_metrics(self, output, step_type: str):
+        y = output["next_token_emb"]
+        tgt = output["current_token_emb"]
+        mask = output["current_token_mask"]
+        B, Tp = y.shape[0], y.shape[1]
+        mbs = self.model_config.train_mini_batch_size if step_type == "train" else B
+        if mbs < 0:
+            mbs = B
+        mbs = min(mbs, B)
+        n_mb = (B + mbs - 1) // mbs
+        offs = self.draw_offsets(n_mb)
+        if (Tp - 1 - offs).min() <= 0:
+            raise ValueError("a lookahead offset reaches past the (trimmed) history")
+        offsets_dev = torch.from_numpy(offs).pin_memory().to(y.device, non_blocking=True)
+        cfg = dict(mb=mbs, tau=self._softmax_temperature, ks=self._metrics_k_all)
+        loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg)
+        self.batch_idx += 1
+        self.last_stats = (loss.grad_fn, offs, step_type, B)
+        return loss, {}
+
+    def metrics(self) -> Dict[str, float]:
+        """Metric dict of the last step, keyed like wrapper.py:222-242 (one device->host copy)."""
+        if self.last_stats is None:
+            return {}
+        fn, offs, step_type, B = self.last_stats
+        stats = fn.stats.cpu().numpy()  # [NH, n_mb, nstat]
+        return lthm_metrics(stats, offs, step_type, self._metrics_k_all, B)
+
+    def is_sparse(self, param_name: str):
+        return super().is_sparse(param_name) or "user_context.tables" in param_name
+
+    def optim_group(self, parent_module: nn.Module, full_param_name: str, numel: int) -> Optional[str]:
+        return "SPARSE_ROWS" if "user_context.tables" in full_param_name else "USE_OPTIM"
+
+    def optimizers_for_param_groups(self, param_groups: Dict[str, List[torch.nn.Parameter]]):
+        result = []
+        dense = [p for p in param_groups.get("USE_OPTIM", []) if p.requires_grad]
+        if dense:
+            result.append(FusedAdamW(dense, lr=self.model_config.lr, weight_decay=self.model_config.weight_decay,
+                                     betas=self.model_config.betas))
+        if param_groups.get("SPARSE_ROWS") and self._model.user_context is not None:
+            result.append(SparseRowAdamW([self._model.user_context.tables], lr=self.model_config.lr,
+                                         betas=self.model_config.betas, weight_decay=self.model_config.weight_decay))
+        return result
+
+    def param_groups(self) -> Dict[str, List[torch.nn.Parameter]]:
+        groups: Dict[str, List[torch.nn.Parameter]] = {}
+        for name, p in self.named_parameters():
+            groups.setdefault(self.optim_group(self, name, p.numel()), []).append(p)
+        return groups
+
+
+def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[int], B: int) -> Dict[str, float]:
+    """Per-mini-batch metrics averaged over the mini-batches that produced each key (wrapper.py:95-111)."""
+    acc: Dict[str, float] = {}
+    cnt: Dict[str, int] = {}
+    NH, n_mb, _ = stats.shape
+    T_loss = 0.0
+    for mb in range(n_mb):
+        m = {f"{step_type}_batch_size": None}
+        loss_mb = 0.0
+        for h in range(NH):
+            st = stats[h, mb]
+            off = int(offs[mb, h])
+            used = int(st[1])
+            if used == 0:
+                continue
+            loss_mb += float(st[0])
+            m[f"{step_type}_effective_batch_size_offset_{off}"] = used
+            m[f"{step_type}_average_negatives_per_token_offset_{off}"] = float(st[2])
+            m[f"{step_type}_used_tokens_offset_{off}"] = used
+            m[f"{step_type}_loss_all_tokens_offset_{off}"] = float(st[0])
+            m[f"{step_type}_average_hit_position_offset_{off}"] = float(st[4])
+            m[f"{step_type}_median_hit_position_offset_{off}"] = float(st[5])
+            for q, k in enumerate(ks):
+                m[f"{step_type}_hit_rate_at_{k}_offset_{off}"] = float(st[NSTAT_BASE + q])
+        m[f"{step_type}_loss"] = loss_mb
+        m.pop(f"{step_type}_batch_size")
+        for k, v in m.items():
+            acc[k] = acc.get(k, 0.0) + v
+            cnt[k] = cnt.get(k, 0) + 1
+    out = {k: acc[k] / cnt[k] for k in acc}
+    out[f"{step_type}_overall_batch_size"] = B
+    return out

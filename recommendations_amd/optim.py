@@ -1,0 +1,115 @@
+"""Optimizers whose steps are single fused HIP kernels (include/lthm.h).
+
+``FusedAdamW`` / ``FusedAdagrad`` reproduce torch.optim.AdamW / Adagrad update
+rules (wrapper.py:263-275, embedding_module_gen.py:97,137) on fp32 parameters.
+``SparseRowAdamW`` / ``SparseRowAdagrad`` update only the rows of a
+``TableBatchedKShiftEmbedding`` that the step touched (lazy Adam: untouched
+rows do not decay) — the documented deviation that makes 100M-row tables
+trainable; bias corrections use the optimizer's global step.
+"""
+from __future__ import annotations
+
+from typing import Iterable
+
+import torch
+
+from . import kernels as K
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0):
+        loss = closure() if closure is not None else None
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                    raise TypeError("FusedAdamW keeps fp32 masters")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = K.zeros(p.shape, torch.float32, p.device)
+                    st["exp_avg_sq"] = K.zeros(p.shape, torch.float32, p.device)
+                st["step"] += 1
+                grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                K.adamw_(p.data, grad, st["exp_avg"], st["exp_avg_sq"], g["lr"], g["betas"], g["eps"],
+                         g["weight_decay"], st["step"], grad_scale=grad_scale)
+        return loss
+
+
+class FusedAdagrad(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-2, lr_decay=0.0, weight_decay=0.0, eps=1e-10, initial_accumulator_value=0.0):
+        super().__init__(params, dict(lr=lr, lr_decay=lr_decay, weight_decay=weight_decay, eps=eps,
+                                      initial_accumulator_value=initial_accumulator_value))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["sum"] = torch.full_like(p, g["initial_accumulator_value"])
+                st["step"] += 1
+                K.adagrad_(p.data, p.grad.contiguous(), st["sum"], g["lr"], g["lr_decay"], g["eps"],
+                           g["weight_decay"], st["step"])
+        return loss
+
+
+class SparseRowAdamW:
+    """Row-wise AdamW over TableBatchedKShiftEmbedding modules (sparse=True)."""
+
+    def __init__(self, modules: Iterable, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.modules = list(modules)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.step_count = 0
+        self.state = {}
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        for m in self.modules:
+            if m.sparse_count is None or m.sparse_pending == 0:
+                continue
+            st = self.state.get(id(m))
+            if st is None:
+                st = self.state[id(m)] = (K.zeros(m.weight.shape, torch.float32, m.weight.device),
+                                          K.zeros(m.weight.shape, torch.float32, m.weight.device))
+            shadow = m._shadow if (m._shadow is not None and m._shadow_version == m.weight._version) else None
+            K.sparse_adamw_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
+                            m.sparse_grad, st[0], st[1], m.sparse_flags, self.lr, self.betas, self.eps,
+                            self.weight_decay, self.step_count, shadow=shadow)
+            m.sparse_count.zero_()
+            m.sparse_pending = 0
+
+    def zero_grad(self, set_to_none: bool = True):
+        pass  # the row-wise step consumes and re-zeroes exactly the rows it updates
+
+
+class SparseRowAdagrad(SparseRowAdamW):
+    def __init__(self, modules: Iterable, lr=1e-2, lr_decay=0.0, eps=1e-10):
+        super().__init__(modules, lr=lr)
+        self.lr_decay, self.eps = lr_decay, eps
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        for m in self.modules:
+            if m.sparse_count is None or m.sparse_pending == 0:
+                continue
+            st = self.state.get(id(m))
+            if st is None:
+                st = self.state[id(m)] = K.zeros(m.weight.shape, torch.float32, m.weight.device)
+            shadow = m._shadow if (m._shadow is not None and m._shadow_version == m.weight._version) else None
+            K.sparse_adagrad_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
+                              m.sparse_grad, st, m.sparse_flags, self.lr, self.lr_decay, self.eps, self.step_count,
+                              shadow=shadow)
+            m.sparse_count.zero_()
+            m.sparse_pending = 0
