@@ -102,9 +102,17 @@ __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t 
       gk = k + (idx >> 4);
       gr = r0 + (idx & 15) * 8;
     }
+    // the chunk's 8 elements are contiguous in memory (along k, or along rows)
+    const int64_t lim = KCONTIG ? (k1 - gk) : (rows - gr);
     if (gr < rows && gk < k1) {
       const bf16_t* src = KCONTIG ? (P + gr * ld + gk) : (P + gk * ld + gr);
-      reg[i] = *reinterpret_cast<const u32x4*>(src);
+      if (lim >= 8 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+        reg[i] = *reinterpret_cast<const u32x4*>(src);
+      } else {  // ragged tail / unaligned row stride: element loads, zero fill
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int e = 0; e < 8 && e < lim; ++e) w[e >> 1] |= (uint32_t)src[e] << ((e & 1) * 16);
+        reg[i] = u32x4{w[0], w[1], w[2], w[3]};
+      }
     } else {
       reg[i] = u32x4{0u, 0u, 0u, 0u};
     }
@@ -257,12 +265,9 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   LTHM_REQUIRE(d->out_dtype == LTHM_F32 || d->out_dtype == LTHM_BF16);
   if (d->M == 0 || d->N == 0) return 0;
   const bool ka = d->a_kcontig != 0, kb = d->b_kcontig != 0;
-  // 16-byte chunk alignment of every staged row
-  LTHM_REQUIRE(((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0);
-  LTHM_REQUIRE(d->lda % 8 == 0 && d->ldb % 8 == 0);
-  LTHM_REQUIRE(ka ? (d->K % 8 == 0) : (d->M % 8 == 0));
-  LTHM_REQUIRE(kb ? (d->K % 8 == 0) : (d->N % 8 == 0));
-  LTHM_REQUIRE(d->batch == 1 || (d->sA % 8 == 0 && d->sB % 8 == 0));
+  // any shape / stride: aligned full chunks take 16-B loads, ragged tails element loads
+  LTHM_REQUIRE(((uintptr_t)d->A % 2) == 0 && ((uintptr_t)d->B % 2) == 0);
+  LTHM_REQUIRE(d->lda >= (ka ? d->K : d->M) && d->ldb >= (kb ? d->K : d->N));
   LTHM_REQUIRE(d->act >= 0 && d->act <= LTHM_ACT_QGELU_GRAD);
   LTHM_REQUIRE(!(d->act == LTHM_ACT_GELU_GRAD || d->act == LTHM_ACT_QGELU_GRAD) || d->aux != nullptr);
   int splits = d->splits < 1 ? 1 : d->splits;

@@ -47,7 +47,9 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
   for (int i = tid; i < d.proj_total; i += 256) proj[i] = d.proj[i];
   for (int i = tid; i < d.grid_total; i += 256) grids[i] = d.grids[i];
   __syncthreads();
-  // OPL = Dout / 64 outputs per lane (Dout in {64, 128, 256, 512})
+  // OPL outputs per lane; lanes with lane*OPL >= Dout idle (Dout < 64 or not a multiple of 64)
+  const bool lane_on = lane * OPL < Dout;
+  const int lcol = lane_on ? lane * OPL : 0;
   float* xw = xs + wave * 2 * Din;
   float* xw2 = xw + Din;
   uint16_t* rw = rbuf + wave * total_idx;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
     // emb_mapper Linear
     float acc[OPL];
     for (int q = 0; q < OPL; ++q) {
-      const int o = lane * OPL + q;
+      const int o = lcol + q;
       float s = 0.f;
       if (!d.cve_only) {
         s = d.b_map ? d.b_map[o] : 0.f;
@@ -114,30 +116,31 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
       int p = 0;
       for (; p + 4 <= np; p += 4) {
         float v0[OPL], v1[OPL], v2[OPL], v3[OPL];
-        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lane * OPL;
-        const TT* r1 = tab + (int64_t)rw[rb + p + 1] * Dout + lane * OPL;
-        const TT* r2 = tab + (int64_t)rw[rb + p + 2] * Dout + lane * OPL;
-        const TT* r3 = tab + (int64_t)rw[rb + p + 3] * Dout + lane * OPL;
+        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lcol;
+        const TT* r1 = tab + (int64_t)rw[rb + p + 1] * Dout + lcol;
+        const TT* r2 = tab + (int64_t)rw[rb + p + 2] * Dout + lcol;
+        const TT* r3 = tab + (int64_t)rw[rb + p + 3] * Dout + lcol;
         for (int q = 0; q < OPL; ++q) { v0[q] = Elem<TT>::ld(r0 + q); v1[q] = Elem<TT>::ld(r1 + q);
                                         v2[q] = Elem<TT>::ld(r2 + q); v3[q] = Elem<TT>::ld(r3 + q); }
         for (int q = 0; q < OPL; ++q) bag[q] = (((bag[q] + v0[q]) + v1[q]) + v2[q]) + v3[q];
       }
       for (; p < np; ++p) {
-        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lane * OPL;
+        const TT* r0 = tab + (int64_t)rw[rb + p] * Dout + lcol;
         for (int q = 0; q < OPL; ++q) bag[q] += Elem<TT>::ld(r0 + q);
       }
       for (int q = 0; q < OPL; ++q) acc[q] += bag[q];
       rb += np;
     }
     if (hbin >= 0) {
-      const TT* hr = hist + (int64_t)hbin * Dout + lane * OPL;
+      const TT* hr = hist + (int64_t)hbin * Dout + lcol;
       for (int q = 0; q < OPL; ++q) acc[q] += Elem<TT>::ld(hr + q);
     }
-    if (d.emb_dtype == LTHM_F32) {
-      float* eo = reinterpret_cast<float*>(d.emb_out) + tok * Dout + lane * OPL;
+    if (!lane_on) {
+    } else if (d.emb_dtype == LTHM_F32) {
+      float* eo = reinterpret_cast<float*>(d.emb_out) + tok * Dout + lcol;
       for (int q = 0; q < OPL; ++q) eo[q] = masked ? 0.f : acc[q];
     } else {
-      bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out) + tok * Dout + lane * OPL;
+      bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out) + tok * Dout + lcol;
       for (int q = 0; q < OPL; ++q) eo[q] = f2bf(masked ? 0.f : acc[q]);
     }
     if (lane == 0 && d.mask_out) d.mask_out[tok] = masked ? 1 : 0;
@@ -290,7 +293,7 @@ extern "C" int lthm_flip_tokens(const int64_t* in, int64_t* out, int64_t B, int3
 
 extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   LTHM_REQUIRE(d && d->n >= 0 && d->Din > 0 && d->Din <= 64 && d->n_mod >= 0 && d->n_mod <= LTHM_MAX_CVE);
-  LTHM_REQUIRE(d->Dout % 64 == 0 && d->Dout <= 512);
+  LTHM_REQUIRE(d->Dout > 0 && d->Dout <= 512);
   if (d->n == 0) return 0;
   int total = 0;
   for (int j = 0; j < d->n_mod; ++j) total += d->mod_nproj[j];
@@ -300,7 +303,8 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   LTHM_REQUIRE(sh <= 160 * 1024);
   const int grid = grid_for(d->n, 4, 256 * 8);
   hipStream_t s = (hipStream_t)stream;
-  const int opl = d->Dout / 64;
+  const int opl = d->Dout <= 64 ? 1 : d->Dout <= 128 ? 2 : d->Dout <= 256 ? 4 : 8;
+  LTHM_REQUIRE(d->Dout % opl == 0);
 #define LTHM_PT(TX, TT)                                                                                   \
   if (opl == 1) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 1>), dim3(grid), dim3(256), sh, s, *d, total);    \
   else if (opl == 2) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 2>), dim3(grid), dim3(256), sh, s, *d, total); \

@@ -46,9 +46,10 @@ class Encoder(nn.Module):
         if pt.model_init_metadata is not None:
             raise NotImplementedError("TorchScript item-embedding artifacts are loaded via load_item_artifact()")
         lm = pt.latent_model_config
+        # fp32 output: the CVE bucketize downstream is discontinuous, a bf16-rounded
+        # input would flip ~1% of the bucket decisions relative to the reference
         self.product_emb_module = KShiftEmbedding(lm.vocab_size_latent, pt.inp_emb_dim, num_shifts=lm.num_shifts_latent,
-                                                  normalize_output=lm.normalize_embedding,
-                                                  out_dtype=torch.bfloat16 if model_config.item_table_bf16 else None)
+                                                  normalize_output=lm.normalize_embedding, out_dtype=torch.float32)
         if model_config.item_table_bf16:
             self.product_emb_module.emb.weight.data = self.product_emb_module.emb.weight.data.to(torch.bfloat16)
         self.product_emb_module.emb.weight.requires_grad_(False)  # detached by product_tower.py:47
