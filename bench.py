@@ -1,0 +1,222 @@
+"""LTHM training-step benchmark (BASELINE.json metric: training samples/sec, LTHM
+fwd+bwd, plus embedding HBM GB/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c4x]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = the reference's inner training step (accelerate_training_strategy.py:
+351-368): model(batch) -> train_step (fused contrastive loss) -> backward ->
+DP gradient exchange (N > 1) -> optimizer steps (fused AdamW on dense params,
+row-wise AdamW on the categorical KShift tables).  Inputs are synthetic batches
+of the C2 shape already resident in HBM.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec, bf16 dense MFMA 2.5 PF
+HBM_PEAK_GBS = 8000.0
+BF16_PEAK_TFLOPS = 2500.0
+
+CONFIGS = {
+    # BASELINE.json configs[1]: LTHM on 1x MI355X, 32 cat x 1M vocab, seq 128, d 256, 4 layers, bf16, batch 4096
+    "c2": dict(B=4096, T=128, d=256, L=4, H=4, n_cat=32, cat_vocab=1_000_000, item_vocab=1_000_000),
+    # BASELINE.json configs[0] shape (tiny; plumbing)
+    "c1": dict(B=128, T=32, d=64, L=2, H=1, n_cat=2, cat_vocab=10_000, item_vocab=10_000),
+}
+
+
+def build(cfgd, dev):
+    from recommendations_amd.models.lthm.builder import LTHMModelBuilder
+    from recommendations_amd.models.lthm.config import lthm_config
+    torch.manual_seed(1234)  # identical replicas on every rank
+    cfg = lthm_config(T=cfgd["T"], d=cfgd["d"], n_layers=cfgd["L"], n_head=cfgd["H"], cat_features=cfgd["n_cat"],
+                      cat_vocab=cfgd["cat_vocab"], item_vocab=cfgd["item_vocab"])
+    model = LTHMModelBuilder(None, cfg).build().to(dev)
+    return cfg, model
+
+
+def cpu_baseline(cfg, model, cfgd, B_cpu):
+    """The oracle's CPU restatement of the same step (fwd + bwd + torch.optim.AdamW over
+    all params, as wrapper.py:263-275 / accelerate_training_strategy.py:351-368), on a
+    bounded sample of B_cpu sequences of the same workload."""
+    from oracle import lthm_ref
+    from recommendations_amd.data import synthetic_lthm_batch
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    sd = {k: (v.detach().float().cpu().clone().requires_grad_(True) if v.is_floating_point() else v.cpu())
+          for k, v in model.state_dict().items()}
+    params = [v for v in sd.values() if v.is_floating_point() and "product_emb_module" not in k_of(sd, v)]
+    opt = torch.optim.AdamW(params, lr=cfg.lr, weight_decay=cfg.weight_decay, betas=cfg.betas)
+    batch = synthetic_lthm_batch(B_cpu, cfgd["T"], n_cat=cfgd["n_cat"], seed=99)
+    n_mb = (B_cpu + cfg.train_mini_batch_size - 1) // cfg.train_mini_batch_size
+    offs = np.array([[0, 3, 6, 9, 17, 25]] * n_mb, dtype=np.int32)
+
+    def step():
+        loss = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()  # warm-up (allocates the optimizer state, as the reference's first step would)
+    t0 = time.perf_counter()
+    n = 1
+    step()
+    dt = time.perf_counter() - t0
+    return dict(value=round(B_cpu * n / dt, 3), unit="samples/s", cores=cores, kind="port",
+                sample=f"{B_cpu} sequences of the {cfgd} workload, 1 timed step after 1 warm-up "
+                       f"(fp32 torch-CPU oracle: oracle/lthm_ref.py + torch.optim.AdamW over every parameter)")
+
+
+def k_of(sd, v):
+    for k, t in sd.items():
+        if t is v:
+            return k
+    return ""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    from recommendations_amd import _lib
+    from recommendations_amd.data import synthetic_lthm_batch
+    from recommendations_amd.distributed import GradBucketAllReduce, init_from_env, step_flags
+
+    rank, local, world = init_from_env()
+    if world != args.gpus and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    cfgd = dict(CONFIGS[args.config])
+    if args.batch:
+        cfgd["B"] = args.batch
+    cfg, model = build(cfgd, dev)
+    B = cfgd["B"]
+    if world > 1 and model._model.user_context is not None:
+        model._model.user_context.tables.replicated_dp = True
+    opts = model.optimizers_for_param_groups(model.param_groups())
+    dense_params = [p for n, p in model.named_parameters() if p.requires_grad and "user_context.tables" not in n]
+    allreduce = GradBucketAllReduce(dense_params)
+    batch = synthetic_lthm_batch(B, cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=rank, device=dev)
+
+    def step():
+        out = model(batch)
+        loss, _ = model.train_step(batch, out)
+        loss.backward()
+        allreduce()
+        flags = step_flags(False, loss)
+        for o in opts:
+            o.step()
+            o.zero_grad(set_to_none=True)
+        return loss, flags
+
+    for _ in range(args.warmup):
+        loss, flags = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    if not args.no_kernel_timing:
+        _lib.TIMER = _lib.KernelTimer()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, flags = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timer, _lib.TIMER = _lib.TIMER, None
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    assert float(flags[1]) == 0.0, "non-finite loss"
+    samples = B * world * args.steps
+    res = {
+        "metric": "training samples/sec (LTHM fwd+bwd) at 1/2/4/8 MI355X; embedding HBM GB/s",
+        "value": round(samples / dt, 2),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded full-range int64 item ids with 0-padding, labels 0..3, 2023 timestamps, "
+                "uniform int64 categorical ids); random-init weights",
+        "config": {"workload": f"LTHM {args.config.upper()}: item KShift P={cfgd['item_vocab']} D=32 K=16, "
+                               f"{cfgd['n_cat']} cat x {cfgd['cat_vocab']} KShift D=32 K=8, T={cfgd['T']}, "
+                               f"d={cfgd['d']}, {cfgd['L']} layers, H={cfgd['H']}, 6 lookahead heads",
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd["T"],
+                   "parallelism": f"dp{world}" + (" (replicated KShift tables, gathered row updates)" if world > 1 else "")},
+        "final_loss": round(float(loss), 5),
+    }
+    if timer is not None:
+        summ = timer.summary()
+        kern = {}
+        for k, s in summ.items():
+            avg_ms = s["ms"] / s["calls"]
+            e = {"calls_per_step": s["calls"] / args.steps, "avg_ms": round(avg_ms, 4),
+                 "share": round(s["ms"] / (1000 * dt) , 4)}
+            if s["work"]:
+                rate = s["work"] / (s["ms"] / 1000.0)
+                if s["unit"] == "byte":
+                    e["GB/s"] = round(rate / 1e9, 1)
+                    e["frac_hbm_peak"] = round(rate / 1e9 / HBM_PEAK_GBS, 4)
+                else:
+                    e["TFLOP/s"] = round(rate / 1e12, 1)
+                    e["frac_bf16_peak"] = round(rate / 1e12 / BF16_PEAK_TFLOPS, 4)
+            kern[k] = e
+        dom = max(summ, key=lambda k: summ[k]["ms"])
+        s = summ[dom]
+        avg_s = s["ms"] / s["calls"] / 1000.0
+        per_launch = (s["work"] or 0.0) / s["calls"]
+        if s["unit"] == "byte":
+            ach, peak, unit, bound = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+        else:
+            ach, peak, unit, bound = per_launch / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s", "mfma"
+        res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                           "frac": round(ach / peak, 4), "traffic": None,
+                           "avg_launch_ms": round(s["ms"] / s["calls"], 4)}
+        if "kshift_fwd_k" in summ:
+            g = summ["kshift_fwd_k"]
+            res["embedding_gather"] = {"kernel": "kshift_fwd_k", "bound": "hbm",
+                                       "achieved": round(g["work"] / (g["ms"] / 1000) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                       "unit": "GB/s",
+                                       "frac": round(g["work"] / (g["ms"] / 1000) / 1e9 / HBM_PEAK_GBS, 4)}
+        res["kernels"] = kern
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(cfg, model, cfgd, args.cpu_batch)
+    if rank == 0:
+        print(json.dumps(res))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

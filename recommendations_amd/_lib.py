@@ -122,9 +122,40 @@ def load() -> ctypes.CDLL:
     return lib
 
 
-def call(name: str, *args) -> None:
+class KernelTimer:
+    """Live per-entry-point timing with HIP events on torch's current stream (the
+    stream every launch goes to).  bench.py enables it over the timed region;
+    ``work`` is the algorithmic bytes / flops the wrapper declares per call."""
+
+    def __init__(self):
+        self.records = []  # (key, ev0, ev1, work, unit)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for key, e0, e1, work, unit in self.records:
+            s = out.setdefault(key, {"calls": 0, "ms": 0.0, "work": 0.0, "unit": unit})
+            s["calls"] += 1
+            s["ms"] += e0.elapsed_time(e1)
+            s["work"] += work or 0.0
+        return out
+
+
+TIMER = None  # type: KernelTimer
+
+
+def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = None) -> None:
     lib = load()
-    rc = getattr(lib, name)(*args)
+    t = TIMER
+    if t is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        t.records.append((_key or name, e0, e1, _work, _unit))
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with hip error {rc}")
 

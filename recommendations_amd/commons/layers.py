@@ -100,7 +100,8 @@ class _SparseKShiftFn(torch.autograd.Function):
         out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
         norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if mode == K.KSHIFT_NORMALIZE else None
         call("lthm_kshift_fwd_multi", ptr(ids), ids.numel() // F_, F_, ptr(gather_w), dcode(gather_w), P, D, Kk, mode,
-             ptr(out), dcode(out), ptr(norms), stream())
+             ptr(out), dcode(out), ptr(norms), stream(), _key="kshift_fwd_k",
+             _work=ids.numel() * (8 + Kk * D * gather_w.element_size() + D * out.element_size()), _unit="byte")
         ctx.mod = mod
         ctx.save_for_backward(ids, out if mode == K.KSHIFT_NORMALIZE else None, norms)
         return out
@@ -109,8 +110,15 @@ class _SparseKShiftFn(torch.autograd.Function):
     def backward(ctx, gy):
         ids, out, norms = ctx.saved_tensors
         mod = ctx.mod
+        gy = gy.contiguous()
+        if mod.replicated_dp:
+            # data parallel over replicated tables: every rank applies every rank's updates
+            from ..distributed import all_gather_rows
+            ids, gy = all_gather_rows(ids), all_gather_rows(gy)
+            if out is not None:
+                out, norms = all_gather_rows(out), all_gather_rows(norms)
         mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
-        K.kshift_bwd_sparse(ids, gy.contiguous(), out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
+        K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
                             mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count)
         mod.sparse_pending += ids.numel() * mod._num_shifts
         return None, None, None, None
@@ -138,6 +146,7 @@ class TableBatchedKShiftEmbedding(nn.Module):
         self._shadow_version = -1
         self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
         self.sparse_pending = 0
+        self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
 
     def _ensure_sparse_state(self, max_new_rows: int):
         w = self.weight

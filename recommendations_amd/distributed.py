@@ -1,0 +1,91 @@
+"""One process per GPU over RCCL (torch.distributed backend "nccl" = RCCL on ROCm).
+
+The reference never synchronises gradients (its model is not passed to
+``accelerator.prepare``: commons/training_strategy/accelerate_training_strategy.py:
+165, 211-229 — each Ray worker trains an independent replica).  This build adds
+real data parallelism:
+
+* dense parameters: one bucketed fp32 all-reduce (average) of the flattened
+  gradients per step;
+* table-batched KShift tables (replicated, sparse row-wise optimizer): the
+  backward all-gathers every rank's (ids, pooled-gradient) pairs and applies
+  all of them locally, so replicas receive identical row updates without ever
+  exchanging a [P, D] gradient;
+* the reference's per-step stop-flag all_gather (accelerate_training_strategy.py:
+  464-480) and NaN guard (:378-398) become ONE 8-byte all_reduce(MAX).
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend: Optional[str] = None):
+    """Initialise the process group from torchrun's env (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, local, world
+
+
+def world_size() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+class GradBucketAllReduce:
+    """Average dense gradients across ranks with a few large flat all-reduces."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 64 << 20):
+        self.params = [p for p in params if p.requires_grad]
+        self.bucket_bytes = bucket_bytes
+
+    def __call__(self):
+        ws = world_size()
+        if ws == 1:
+            return
+        grads = [p.grad for p in self.params if p.grad is not None]
+        bucket: List[torch.Tensor] = []
+        size = 0
+        for g in grads:
+            bucket.append(g)
+            size += g.numel() * g.element_size()
+            if size >= self.bucket_bytes:
+                self._flush(bucket, ws)
+                bucket, size = [], 0
+        if bucket:
+            self._flush(bucket, ws)
+
+    @staticmethod
+    def _flush(bucket: List[torch.Tensor], ws: int):
+        flat = torch._utils._flatten_dense_tensors(bucket)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.div_(ws)
+        for g, f in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
+            g.copy_(f)
+
+
+def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
+    """Concatenate t from every rank along dim 0 (rank order)."""
+    ws = world_size()
+    if ws == 1:
+        return t
+    out = torch.empty((ws * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous())
+    return out
+
+
+def step_flags(stop: bool, loss: torch.Tensor) -> torch.Tensor:
+    """[stop, non-finite loss] MAX-reduced over ranks in one collective (no host sync here)."""
+    f = torch.stack([torch.tensor(float(stop), device=loss.device), (~torch.isfinite(loss.detach())).float().reshape(())])
+    if world_size() > 1:
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+    return f

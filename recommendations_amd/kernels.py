@@ -41,7 +41,8 @@ class KShiftFn(torch.autograd.Function):
         need_norms = mode == KSHIFT_NORMALIZE and weight.requires_grad
         norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if need_norms else None
         call("lthm_kshift_fwd_multi", ptr(ids), n, F, ptr(weight), dcode(weight), P, D, K, mode,
-             ptr(out), dcode(out), ptr(norms), stream())
+             ptr(out), dcode(out), ptr(norms), stream(), _key="kshift_fwd_k",
+             _work=ids.numel() * (8 + K * D * weight.element_size() + D * out.element_size()), _unit="byte")
         ctx.save_for_backward(ids, out if mode == KSHIFT_NORMALIZE else None, norms)
         ctx.cfg = (P, K, mode, F, D, weight.shape, weight.dtype)
         return out
@@ -133,7 +134,8 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
         d.workspace, d.workspace_bytes = ptr(ws), ws.numel() * 4
     d.splits = splits
     import ctypes
-    call("lthm_gemm", ctypes.addressof(d), stream())
+    call("lthm_gemm", ctypes.addressof(d), stream(), _key=f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>",
+         _work=2.0 * M * N * K * batch, _unit="flop")
     return out
 
 
@@ -223,7 +225,8 @@ def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True):
     k = qkv[:, C:]
     v = qkv[:, 2 * C:]
     d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
-    call("lthm_attn_fwd", ctypes.addressof(d), stream())
+    call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
+         _unit="flop")
     return out, lse
 
 
@@ -236,7 +239,8 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
     d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
     d.dout, d.dq, d.dk, d.dv = ptr(dout), ptr(dqkv), ptr(dqkv[:, C:]), ptr(dqkv[:, 2 * C:])
     d.dtable_part = ptr(part)
-    call("lthm_attn_bwd", ctypes.addressof(d), stream())
+    call("lthm_attn_bwd", ctypes.addressof(d), stream(), _key="attn_bwd_k", _work=10.0 * B * H * T * T * E,
+         _unit="flop")
     dtab = None
     if part is not None:
         dtab = colsum(part.view(B, (2 * T + 1) * H)).view(2 * T + 1, H)

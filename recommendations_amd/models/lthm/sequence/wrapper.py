@@ -63,7 +63,7 @@ class ContrastiveLossFn(torch.autograd.Function):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
                                         lse[h], pos[h], cnt[h], rank[h], diag[h], w[h])
             call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats[h]), nstat, ptr(ks_dev), len(ks),
-                 1.0 / n_mb, stream())
+                 1.0 / n_mb, stream(), _key="cl_fwd_k", _work=cfg["flops"][h], _unit="flop")
             descs.append(d)
         # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
         loss = torch.empty(1, **f32)
@@ -72,6 +72,7 @@ class ContrastiveLossFn(torch.autograd.Function):
         ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, mask, offsets_dev)
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
+        ctx.flops = cfg["flops"]
         return loss
 
     @staticmethod
@@ -96,7 +97,8 @@ class ContrastiveLossFn(torch.autograd.Function):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
                                         lse[h], None, None, None, None, w[h])
             d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
-            call("lthm_contrastive_bwd", ctypes.addressof(d), stream())
+            call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
+                 _work=4.0 * ctx.flops[h], _unit="flop")
         dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
         dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
         return dy.view(yc.shape), dt.view(tc.shape), None, None, None
@@ -165,7 +167,15 @@ class LTHMModelWrapper(BaseModelWrapper):
         if (Tp - 1 - offs).min() <= 0:
             raise ValueError("a lookahead offset reaches past the (trimmed) history")
         offsets_dev = torch.from_numpy(offs).pin_memory().to(y.device, non_blocking=True)
-        cfg = dict(mb=mbs, tau=self._softmax_temperature, ks=self._metrics_k_all)
+        T = Tp - 1
+        flops = []  # algorithmic logits flops per head: sum over mini-batches of 2 n^2 De
+        for h in range(offs.shape[1]):
+            tot = 0.0
+            for mb in range(n_mb):
+                n = min(mbs, B - mb * mbs) * (T - int(offs[mb, h]))
+                tot += 2.0 * n * n * y.shape[-1]
+            flops.append(tot)
+        cfg = dict(mb=mbs, tau=self._softmax_temperature, ks=self._metrics_k_all, flops=flops)
         loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg)
         self.batch_idx += 1
         self.last_stats = (loss.grad_fn, offs, step_type, B)
