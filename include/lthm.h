@@ -23,6 +23,8 @@
 extern "C" {
 #endif
 
+#define LTHM_ABI_VERSION 2 /* bumped on any signature / struct layout change */
+
 #define LTHM_F32 0
 #define LTHM_BF16 1
 
@@ -34,6 +36,7 @@ extern "C" {
 /* ------------------------------------------------------------------------- */
 /* version / capability                                                      */
 /* ------------------------------------------------------------------------- */
+/* returns LTHM_ABI_VERSION of the built library */
 int lthm_abi_version(void);
 /* number of gfx950 devices visible (0 on a host without a GPU); never fails */
 int lthm_device_count(void);
@@ -235,10 +238,23 @@ typedef struct lthm_ptower_desc {
 
 int lthm_product_tower_fwd(const lthm_ptower_desc* desc, void* stream);
 
-/* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i (0xffff = skip).
- * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows. */
+/* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i < nidx <= 64 (0xffff = skip).
+ * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows.
+ * `workspace` (device, may be NULL) holds per-token-chunk partial sums; with
+ * >= 2 * R * D * 4 bytes the tokens are split into chunks that are folded into
+ * dW in a fixed order (no global atomics).  dW is accumulated into. */
 int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,
-                         int64_t n, int32_t R, int32_t D, float* dW, void* stream);
+                         int64_t n, int32_t R, int32_t D, float* dW, void* workspace, int64_t workspace_bytes,
+                         void* stream);
+/* Same, with the slots grouped into nseg (<= 64) segments: segment s covers slots
+ * [seg_slot0[s], +seg_nslot[s]) (nslot <= 64) whose rows all lie in
+ * [seg_row0[s], +seg_nrow[s]); segment row ranges are disjoint.  A segment's
+ * [nrow, 64] f32 slice is held in LDS, so nrow <= 640 (<= 256 keeps two blocks
+ * per CU).  The seg_* arrays are HOST arrays. */
+int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nseg, const int32_t* seg_slot0,
+                             const int32_t* seg_nslot, const int32_t* seg_row0, const int32_t* seg_nrow,
+                             const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
+                             void* workspace, int64_t workspace_bytes, void* stream);
 /* QuantileMapper (commons/transformers/layers.py:477-487) on x [B, F]:
  * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
 int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,

@@ -96,6 +96,7 @@ class _SparseKShiftFn(torch.autograd.Function):
         require_gpu(ids, weight)
         F_, P, Kk, mode = mod._F, mod._num_embeddings, mod._num_shifts, mod._mode
         D = weight.shape[1]
+        K._check_kshift(ids, P, Kk, F_, D, table_rows=gather_w.shape[0])
         out_dtype = mod._out_dtype or torch.float32
         out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
         norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if mode == K.KSHIFT_NORMALIZE else None
@@ -119,7 +120,8 @@ class _SparseKShiftFn(torch.autograd.Function):
                 out, norms = all_gather_rows(out), all_gather_rows(norms)
         mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
         K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
-                            mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count)
+                            mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,
+                            pending=mod.sparse_pending)
         mod.sparse_pending += ids.numel() * mod._num_shifts
         return None, None, None, None
 

@@ -290,14 +290,18 @@ class CVEFn(torch.autograd.Function):
         d.emb_out, d.rows_out, d.emb_dtype = ptr(emb32), ptr(rows), dcode(emb32)
         call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
         ctx.save_for_backward(rows)
-        ctx.meta = ([t.shape for t in tables], R, shp)
+        segs, so = [], 0
+        for j, m in enumerate(mods):
+            segs += K.cve_segments(m.n_proj, m.num_bins + 1, so, d.mod_row_off[j])
+            so += m.n_proj
+        ctx.meta = ([t.shape for t in tables], R, shp, segs)
         return emb32.view(*shp[:-1], Dout)
 
     @staticmethod
     def backward(ctx, dy):
         (rows,) = ctx.saved_tensors
-        shapes, R, shp = ctx.meta
-        dtab = K.small_table_bwd(rows, dy.contiguous().view(rows.shape[0], -1).float(), R)
+        shapes, R, shp, segs = ctx.meta
+        dtab = K.segmented_table_bwd(rows, dy.contiguous().view(rows.shape[0], -1).float(), R, segs)
         out, r = [], 0
         for s in shapes:
             out.append(dtab[r:r + s[0]])

@@ -63,7 +63,7 @@ __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   return dt == LTHM_F32 ? reinterpret_cast<const float*>(p)[i] : bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
 }
 
-__device__ __forceinline__ float epilogue(const GemmArgs& g, float v, int64_t row, int64_t col, int64_t b) {
+__device__ __forceinline__ float epilogue(const GemmArgs g, float v, int64_t row, int64_t col, int64_t b) {
   if (g.bias) v += g.bias[col];
   if (g.act == LTHM_ACT_GELU || g.act == LTHM_ACT_QGELU) {
     if (g.aux_out) g.aux_out[b * g.M * g.ldaux + row * g.ldaux + col] = f2bf(v);
@@ -76,6 +76,95 @@ __device__ __forceinline__ float epilogue(const GemmArgs& g, float v, int64_t ro
   if (g.res1) v += ld_any(g.res1, g.res1_dt, b * g.M * g.ldr1 + row * g.ldr1 + col);
   if (g.res2) v += ld_any(g.res2, g.res2_dt, b * g.M * g.ldr2 + row * g.ldr2 + col);
   return v;
+}
+
+// ---- 8-wide epilogue helpers (vector path when the 8 columns are in range and 16-B aligned)
+__device__ __forceinline__ void ld8(const void* p, int dt, int64_t idx, int nv, float (&out)[8]) {
+  if (dt == LTHM_F32) {
+    const float* q = reinterpret_cast<const float*>(p) + idx;
+    if (nv == 8 && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(q), c = *reinterpret_cast<const f32x4*>(q + 4);
+      out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w; out[4] = c.x; out[5] = c.y; out[6] = c.z; out[7] = c.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = (e < nv) ? q[e] : 0.f;
+    }
+  } else {
+    const bf16_t* q = reinterpret_cast<const bf16_t*>(p) + idx;
+    if (nv == 8 && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
+      load_vec<bf16_t, 16>(q, out);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = (e < nv) ? bf2f(q[e]) : 0.f;
+    }
+  }
+}
+__device__ __forceinline__ void st8(void* p, int dt, int64_t idx, int nv, const float (&v)[8]) {
+  if (dt == LTHM_F32) {
+    float* q = reinterpret_cast<float*>(p) + idx;
+    if (nv == 8 && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
+      *reinterpret_cast<f32x4*>(q) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(q + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < nv) q[e] = v[e];
+    }
+  } else {
+    bf16_t* q = reinterpret_cast<bf16_t*>(p) + idx;
+    if (nv == 8 && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
+      store_vec<bf16_t, 8>(q, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < nv) q[e] = f2bf(v[e]);
+    }
+  }
+}
+
+__device__ __forceinline__ void epilogue8(const GemmArgs& g, float (&v)[8], int64_t row, int64_t col0, int64_t b, int split) {
+  const int nv = (int)min((int64_t)8, g.N - col0);
+  if (g.ws) {  // split-K slab (raw alpha * acc); the combine kernel applies the epilogue
+    st8(g.ws, LTHM_F32, ((int64_t)split * gridDim.y + b) * g.M * g.N + row * g.N + col0, nv, v);
+    return;
+  }
+  float t[8];
+  if (g.bias) {
+    ld8(g.bias, LTHM_F32, col0, nv, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  const int64_t ai = b * g.M * g.ldaux + row * g.ldaux + col0;
+  if (g.act == LTHM_ACT_GELU || g.act == LTHM_ACT_QGELU) {
+    if (g.aux_out) st8(g.aux_out, LTHM_BF16, ai, nv, v);
+    if (g.act == LTHM_ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = qgelu(v[e]);
+    }
+  } else if (g.act == LTHM_ACT_GELU_GRAD || g.act == LTHM_ACT_QGELU_GRAD) {
+    ld8(g.aux, LTHM_BF16, ai, nv, t);
+    if (g.act == LTHM_ACT_GELU_GRAD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(t[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(t[e]);
+    }
+  }
+  if (g.res1) {
+    ld8(g.res1, g.res1_dt, b * g.M * g.ldr1 + row * g.ldr1 + col0, nv, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (g.res2) {
+    ld8(g.res2, g.res2_dt, b * g.M * g.ldr2 + row * g.ldr2 + col0, nv, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  st8(g.C, g.out_dt, b * g.sC + row * g.ldc + col0, nv, v);
 }
 
 constexpr int BM = 128, BN = 128, BK = 64;
@@ -108,9 +197,13 @@ __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t 
       const bf16_t* src = KCONTIG ? (P + gr * ld + gk) : (P + gk * ld + gr);
       if (lim >= 8 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
         reg[i] = *reinterpret_cast<const u32x4*>(src);
-      } else {  // ragged tail / unaligned row stride: element loads, zero fill
+      } else {  // ragged tail / unaligned row stride: element loads, zero fill (static indices only)
         uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (int e = 0; e < 8 && e < lim; ++e) w[e >> 1] |= (uint32_t)src[e] << ((e & 1) * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t v = (e < lim) ? (uint32_t)src[e] : 0u;
+          w[e >> 1] |= v << ((e & 1) * 16);
+        }
         reg[i] = u32x4{w[0], w[1], w[2], w[3]};
       }
     } else {
@@ -212,29 +305,35 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs g, int tiles_n) {
     cur ^= 1;
   }
 
-  // epilogue
-  const bool split_mode = g.ws != nullptr;
+  // epilogue: restage the 128x128 f32 tile through LDS in two 64-row halves
+  // (static accumulator indices only), then every thread finishes 8 contiguous
+  // columns of a row with 16-B loads/stores.
+  float* ct = reinterpret_cast<float*>(smem);  // [64][CT_LD]
+  constexpr int CT_LD = 132;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (row < g.M && col < g.N) {
-          float v = g.alpha * acc[i][j][r];
-          if (split_mode) {
-            g.ws[((int64_t)split * gridDim.y + b) * g.M * g.N + row * g.N + col] = v;
-          } else {
-            v = epilogue(g, v, row, col, b);
-            const int64_t o = b * g.sC + row * g.ldc + col;
-            if (g.out_dt == LTHM_F32) reinterpret_cast<float*>(g.C)[o] = v;
-            else reinterpret_cast<bf16_t*>(g.C)[o] = f2bf(v);
-          }
-        }
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(i * 16 + (lane >> 4) * 4 + r) * CT_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int q = tid; q < 64 * 16; q += 256) {
+      const int lr = q >> 4, c8 = (q & 15) * 8;
+      const int64_t row = m0 + half * 64 + lr;
+      const int64_t col0 = n0 + c8;
+      if (row < g.M && col0 < g.N) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = g.alpha * ct[lr * CT_LD + c8 + e];
+        epilogue8(g, v, row, col0, b, split);
       }
     }
+    __syncthreads();
   }
 }
 

@@ -180,13 +180,13 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
     }
     // 4) segment heads -> compact segment starts (block exclusive scan)
     const int PER = NP2 / 256;  // NP2 >= 256 guaranteed by host
-    int flags[KB_NP / 256];
+    int hflag[KB_NP / 256];
     int cnt = 0;
     for (int q = 0; q < PER; ++q) {
       const int p = tid * PER + q;
       int h = 0;
       if (p < np) h = (p == 0) || ((keys[p] >> 12) != (keys[p - 1] >> 12));
-      flags[q] = h;
+      hflag[q] = h;
       cnt += h;
     }
     // wave inclusive scan of cnt
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
     if (tid == 255) s_nseg = woff + incl;
     int pos = woff + incl - cnt;
     for (int q = 0; q < PER; ++q) {
-      if (flags[q]) segs[pos++] = tid * PER + q;
+      if (hflag[q]) segs[pos++] = tid * PER + q;
     }
     __syncthreads();
     const int nseg = s_nseg;
@@ -298,7 +298,7 @@ using namespace lthm;
 
 extern "C" {
 
-int lthm_abi_version(void) { return 1; }
+int lthm_abi_version(void) { return LTHM_ABI_VERSION; }
 
 int lthm_device_count(void) {
   int n = 0;

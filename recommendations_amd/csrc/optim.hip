@@ -49,11 +49,11 @@ __global__ __launch_bounds__(256) void adagrad_k(float* __restrict__ p, float* _
 // rows[0 .. *count) touched rows of a [R, D] table; the gradient row is consumed and re-zeroed,
 // the row's touched flag reset.  One wave per row.
 __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
-                                                      int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                      int64_t max_rows, int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                       float* __restrict__ v, int32_t* __restrict__ flags, float lr, float b1,
                                                       float b2, float eps, float wd, float bc1, float bc2_sqrt,
                                                       bf16_t* __restrict__ shadow) {
-  const int64_t cnt = *count;
+  const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
   const int lane = threadIdx.x & 63;
   for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < cnt; k += (int64_t)gridDim.x * 4) {
     const int64_t r = rows[k];
@@ -75,10 +75,10 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
 }
 
 __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
-                                                        int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ s,
+                                                        int64_t max_rows, int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ s,
                                                         int32_t* __restrict__ flags, float clr, float eps,
                                                         bf16_t* __restrict__ shadow) {
-  const int64_t cnt = *count;
+  const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
   const int lane = threadIdx.x & 63;
   for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < cnt; k += (int64_t)gridDim.x * 4) {
     const int64_t r = rows[k];
@@ -159,7 +159,7 @@ extern "C" int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int6
   if (max_rows == 0) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
-  hipLaunchKernelGGL(sparse_adamw_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count, D,
+  hipLaunchKernelGGL(sparse_adamw_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
                      p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
   LTHM_CHECK_LAUNCH();
   return 0;
@@ -172,7 +172,7 @@ extern "C" int lthm_sparse_adagrad(const int64_t* rows, const int64_t* count, in
   if (max_rows == 0) return 0;
   const float clr = lr / (1.f + (float)(step - 1) * lr_decay);
   hipLaunchKernelGGL(sparse_adagrad_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count,
-                     D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow);
+                     max_rows, D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

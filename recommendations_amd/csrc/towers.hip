@@ -10,6 +10,8 @@
 //   * query-tower token assembly (models/lthm/sequence/query_tower.py:89-111)
 //     and outcome conditioning (:118-122);
 //   * history flip (models/lthm/sequence/encoder.py:52-54, 60-61).
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace lthm {
@@ -153,41 +155,81 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
 
 // ------------------------------------------------------------------ small-table gradient
 // dW[rows[t, i]] += dY[t] for every token t and index slot i (0xffff = skip).
-// grid.x: column groups of CG columns, grid.y: token chunks.  Per block the
-// whole table slice [R, CG] is privatised in LDS (ds_add_f32), then flushed
-// with one global f32 add per touched (row, column).
-template <typename TY, int CG>
-__global__ __launch_bounds__(256) void small_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx, const TY* __restrict__ dY,
-                                                      int64_t ldy, int64_t n, int R, int D, float* __restrict__ dW,
-                                                      int64_t tok_per_block) {
+// The slots are grouped into segments (e.g. a run of CosineVectorEmbedding
+// projections whose rows form one contiguous range).  Grid: (64-column groups,
+// segments, token chunks).  A block privatises its segment's [rows, 64] slice in
+// LDS.  One wave walks one token at a time: its 64 lanes hold the token's 64
+// dY columns, the slot row indices are loaded one per lane and broadcast with
+// v_readlane into SGPRs, so every slot costs one return-less ds_add_f32 over 64
+// consecutive banks (no LDS round trip on the critical path).  Chunk z writes
+// its slice with plain stores into part[z] (or adds it to dW when there is one
+// chunk); seg_tab_reduce_k then folds the chunks into dW in a fixed order, so
+// no global atomics are used and the cross-chunk sum is deterministic.
+constexpr int ST_CG = 64;
+constexpr int ST_MAXSEG = 64;
+struct SegTab {
+  int nseg;
+  int slot0[ST_MAXSEG], nslot[ST_MAXSEG], row0[ST_MAXSEG], nrow[ST_MAXSEG];
+};
+
+template <typename TY>
+__global__ __launch_bounds__(256) void seg_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx, const TY* __restrict__ dY,
+                                                    int64_t ldy, int64_t n, int D, float* __restrict__ dst,
+                                                    int64_t zstride, int direct, int64_t tok_per_block, SegTab st) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* acc = reinterpret_cast<float*>(smem);  // [R][CG]
-  const int tid = threadIdx.x;
-  for (int i = tid; i < R * CG; i += 256) acc[i] = 0.f;
+  float* acc = reinterpret_cast<float*>(smem);  // [R][64]
+  const int seg = blockIdx.y;
+  const int s0 = st.slot0[seg], ns = st.nslot[seg], r0 = st.row0[seg], R = st.nrow[seg];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < R * ST_CG; i += 256) acc[i] = 0.f;
   __syncthreads();
-  const int c = tid % CG;
-  const int tl = tid / CG;
-  constexpr int TPAR = 256 / CG;
-  const int col = blockIdx.x * CG + c;
-  const int64_t t0 = (int64_t)blockIdx.y * tok_per_block;
+  const int col = blockIdx.x * ST_CG + lane;
+  const bool cv = col < D;
+  const int64_t t0 = (int64_t)blockIdx.z * tok_per_block;
   const int64_t t1 = min(n, t0 + tok_per_block);
-  if (col < D) {
-    for (int64_t t = t0 + tl; t < t1; t += TPAR) {
-      const uint16_t* rr = rows + t * nidx;
-      const float v = Elem<TY>::ld(dY + t * ldy + col);
-      if (v == 0.f) continue;
-      for (int i = 0; i < nidx; ++i) {
-        const uint16_t r = rr[i];
-        if (r != 0xffff) atomicAdd(&acc[r * CG + c], v);
+  float* accl = acc + lane;
+  for (int64_t t = t0 + wave; t < t1; t += 8) {
+    // two tokens per iteration (t, t+4): both loads are in flight before the adds
+    const int64_t u = t + 4;
+    const bool uv = u < t1;
+    const float va = cv ? Elem<TY>::ld(dY + t * ldy + col) : 0.f;
+    const float vb = (cv && uv) ? Elem<TY>::ld(dY + u * ldy + col) : 0.f;
+    const int ra = lane < ns ? (int)rows[t * nidx + s0 + lane] : 0xffff;
+    const int rb = (lane < ns && uv) ? (int)rows[u * nidx + s0 + lane] : 0xffff;
+    for (int i = 0; i < ns; ++i) {
+      const int r = __builtin_amdgcn_readlane(ra, i) - r0;
+      if ((unsigned)r < (unsigned)R) atomicAdd(accl + r * ST_CG, va);
+    }
+    if (uv) {
+      for (int i = 0; i < ns; ++i) {
+        const int r = __builtin_amdgcn_readlane(rb, i) - r0;
+        if ((unsigned)r < (unsigned)R) atomicAdd(accl + r * ST_CG, vb);
       }
     }
   }
   __syncthreads();
-  for (int i = tid; i < R * CG; i += 256) {
-    const float v = acc[i];
-    const int r = i / CG, cc = i - r * CG;
-    const int cl = blockIdx.x * CG + cc;
-    if (v != 0.f && cl < D) atomicAdd(dW + (int64_t)r * D + cl, v);
+  float* out = dst + (direct ? 0 : (int64_t)blockIdx.z * zstride);
+  for (int i = tid; i < R * ST_CG; i += 256) {
+    const int rr = i / ST_CG, cc = i - rr * ST_CG;
+    const int cl = blockIdx.x * ST_CG + cc;
+    if (cl < D) {
+      float* p = out + (int64_t)(r0 + rr) * D + cl;
+      if (direct) *p += acc[i];
+      else *p = acc[i];
+    }
+  }
+}
+
+// dW[r, :] += sum_z part[z, r, :] over the rows of every segment (z ascending).
+__global__ __launch_bounds__(256) void seg_tab_reduce_k(const float* __restrict__ part, int64_t zstride, int nz, int D,
+                                                       float* __restrict__ dW, SegTab st) {
+  const int seg = blockIdx.y;
+  const int64_t base = (int64_t)st.row0[seg] * D;
+  const int64_t cnt = (int64_t)st.nrow[seg] * D;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < nz; ++z) s += part[z * zstride + base + i];
+    dW[base + i] += s;
   }
 }
 
@@ -320,35 +362,66 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   return 0;
 }
 
-extern "C" int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,
-                                    int64_t n, int32_t R, int32_t D, float* dW, void* stream) {
-  LTHM_REQUIRE(n >= 0 && nidx > 0 && R > 0 && D > 0 && R < 0xffff);
+extern "C" int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nseg, const int32_t* seg_slot0,
+                                        const int32_t* seg_nslot, const int32_t* seg_row0, const int32_t* seg_nrow,
+                                        const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
+                                        void* workspace, int64_t workspace_bytes, void* stream) {
+  LTHM_REQUIRE(n >= 0 && nidx > 0 && D > 0 && nseg > 0 && nseg <= ST_MAXSEG);
   if (n == 0) return 0;
-  int CG = 16;
-  while (CG > 1 && (size_t)R * CG * 4 > 96 * 1024) CG >>= 1;
-  LTHM_REQUIRE((size_t)R * CG * 4 <= 96 * 1024);
-  const int gx = (D + CG - 1) / CG;
-  int64_t gy = 2048 / gx;
-  if (gy < 1) gy = 1;
-  int64_t tpb = (n + gy - 1) / gy;
-  if (tpb < 64) tpb = 64;
-  gy = (n + tpb - 1) / tpb;
-  const size_t sh = (size_t)R * CG * 4;
-  hipStream_t s = (hipStream_t)stream;
-  dim3 grid(gx, (unsigned)gy);
-#define LTHM_STB(CGV)                                                                                          \
-  if (CG == CGV) {                                                                                             \
-    if (dy_dtype == LTHM_F32)                                                                                  \
-      hipLaunchKernelGGL((small_tab_bwd_k<float, CGV>), grid, dim3(256), sh, s, rows, nidx, (const float*)dY,  \
-                         ldy, n, R, D, dW, tpb);                                                               \
-    else                                                                                                       \
-      hipLaunchKernelGGL((small_tab_bwd_k<bf16_t, CGV>), grid, dim3(256), sh, s, rows, nidx, (const bf16_t*)dY, \
-                         ldy, n, R, D, dW, tpb);                                                               \
+  SegTab st;
+  st.nseg = nseg;
+  int maxr = 1, rtot = 0;
+  for (int i = 0; i < nseg; ++i) {
+    st.slot0[i] = seg_slot0[i]; st.nslot[i] = seg_nslot[i]; st.row0[i] = seg_row0[i]; st.nrow[i] = seg_nrow[i];
+    LTHM_REQUIRE(st.slot0[i] >= 0 && st.nslot[i] > 0 && st.nslot[i] <= 64 && st.slot0[i] + st.nslot[i] <= nidx &&
+                 st.nrow[i] > 0 && st.row0[i] >= 0);
+    if (st.nrow[i] > maxr) maxr = st.nrow[i];
+    if (st.row0[i] + st.nrow[i] > rtot) rtot = st.row0[i] + st.nrow[i];
   }
-  LTHM_STB(16) else LTHM_STB(8) else LTHM_STB(4) else LTHM_STB(2) else LTHM_STB(1)
-#undef LTHM_STB
+  // row ranges must be disjoint: every (row, column) has exactly one owner block per chunk
+  for (int i = 0; i < nseg; ++i)
+    for (int j = i + 1; j < nseg; ++j)
+      LTHM_REQUIRE(st.row0[i] + st.nrow[i] <= st.row0[j] || st.row0[j] + st.nrow[j] <= st.row0[i]);
+  const size_t sh = (size_t)maxr * ST_CG * 4;
+  LTHM_REQUIRE(sh <= 160 * 1024);
+  const int gx = (D + ST_CG - 1) / ST_CG;
+  // enough token chunks for ~4 blocks per CU, each chunk >= 512 tokens,
+  // bounded by the partial-buffer workspace
+  const int64_t zbytes = (int64_t)rtot * D * 4;
+  int64_t gz = (1024 + (int64_t)gx * nseg - 1) / ((int64_t)gx * nseg);
+  gz = std::min<int64_t>(gz, (n + 511) / 512);
+  gz = std::min<int64_t>(gz, workspace ? workspace_bytes / zbytes : (int64_t)1);
+  if (gz < 2) gz = 1;
+  int64_t tpb = (n + gz - 1) / gz;
+  gz = (n + tpb - 1) / tpb;
+  const int direct = gz == 1;
+  float* dst = direct ? dW : (float*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(gx, nseg, (unsigned)gz);
+  const int64_t zs = (int64_t)rtot * D;
+  if (dy_dtype == LTHM_F32)
+    hipLaunchKernelGGL((seg_tab_bwd_k<float>), grid, dim3(256), sh, s, rows, nidx, (const float*)dY, ldy, n, D, dst, zs,
+                       direct, tpb, st);
+  else
+    hipLaunchKernelGGL((seg_tab_bwd_k<bf16_t>), grid, dim3(256), sh, s, rows, nidx, (const bf16_t*)dY, ldy, n, D, dst,
+                       zs, direct, tpb, st);
   LTHM_CHECK_LAUNCH();
+  if (!direct) {
+    const int bx = (int)std::min<int64_t>(((int64_t)maxr * D + 255) / 256, 256);
+    hipLaunchKernelGGL(seg_tab_reduce_k, dim3(bx, nseg), dim3(256), 0, s, (const float*)workspace, zs, (int)gz, D, dW,
+                       st);
+    LTHM_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+extern "C" int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,
+                                    int64_t n, int32_t R, int32_t D, float* dW, void* workspace,
+                                    int64_t workspace_bytes, void* stream) {
+  LTHM_REQUIRE(R > 0 && R < 0xffff && nidx <= 64);
+  const int32_t s0 = 0, ns = nidx, r0 = 0, nr = R;
+  return lthm_segmented_table_bwd(rows, nidx, 1, &s0, &ns, &r0, &nr, dY, dy_dtype, ldy, n, D, dW, workspace,
+                                  workspace_bytes, stream);
 }
 
 extern "C" int lthm_tokens_fwd(const lthm_tokens_desc* d, void* stream) {

@@ -20,9 +20,38 @@ KSHIFT_SCALE, KSHIFT_NORMALIZE, KSHIFT_NONE = 0, 1, 2
 def kshift_rows(ids: torch.Tensor, P: int, K: int) -> torch.Tensor:
     """All K row indices of every id: [.., K] int64 (commons/layers.py:174-185)."""
     require_gpu(ids)
+    _check_kshift(ids, P, K, 1, 1)
     rows = torch.empty(ids.shape + (K,), dtype=torch.int64, device=ids.device)
     call("lthm_kshift_rows", ptr(ids), ids.numel(), P, K, ptr(rows), stream())
     return rows
+
+
+def _check(cond, msg):
+    """Host-side operand check before a launch: the kernels trust their sizes."""
+    if not cond:
+        raise ValueError(msg)
+
+
+def _need(t, n: int, name: str):
+    """t must back at least n elements from its data pointer (views included)."""
+    if t is None:
+        return
+    avail = t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+    _check(avail >= n, f"{name}: needs {n} elements from its data pointer, has {avail}")
+
+
+def _check_kshift(ids, P, K, F, D, table_rows=None, gy=None, out=None, norms=None):
+    _check(ids.dtype == torch.int64, f"ids must be int64, got {ids.dtype}")
+    _check(P > 0 and 0 < K <= 64 and F >= 1, f"bad KShift config P={P} K={K} F={F}")
+    _check(ids.numel() % F == 0, f"ids.numel()={ids.numel()} is not a multiple of F={F}")
+    if table_rows is not None:
+        _check(table_rows == F * P, f"table has {table_rows} rows, expected F*P = {F * P}")
+    if gy is not None:
+        _check(gy.numel() == ids.numel() * D, f"grad has {gy.numel()} elements, expected {ids.numel() * D}")
+    if out is not None:
+        _check(out.numel() == ids.numel() * D, f"out has {out.numel()} elements, expected {ids.numel() * D}")
+    if norms is not None:
+        _check(norms.numel() == ids.numel(), "norms must hold one value per id")
 
 
 class KShiftFn(torch.autograd.Function):
@@ -36,6 +65,7 @@ class KShiftFn(torch.autograd.Function):
     def forward(ctx, ids, weight, P: int, K: int, mode: int, F: int, out_dtype):
         require_gpu(ids, weight)
         D = weight.shape[1]
+        _check_kshift(ids, P, K, F, D, table_rows=weight.shape[0])
         n = ids.numel() // F
         out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
         need_norms = mode == KSHIFT_NORMALIZE and weight.requires_grad
@@ -52,6 +82,7 @@ class KShiftFn(torch.autograd.Function):
         ids, out, norms = ctx.saved_tensors
         P, K, mode, F, D, wshape, wdtype = ctx.cfg
         gy = gy.contiguous()
+        _check_kshift(ids, P, K, F, D, table_rows=wshape[0], gy=gy, out=out, norms=norms)
         dW = torch.zeros(wshape, dtype=torch.float32, device=gy.device)
         n = ids.numel() // F
         call("lthm_kshift_bwd_dense", ptr(ids), n, F, ptr(gy), dcode(gy),
@@ -112,6 +143,18 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
     if out is None:
         shape = (batch, M, N) if batch > 1 else (M, N)
         out = torch.empty(shape, dtype=out_dtype, device=dev)
+    lda_ = lda if lda is not None else (K if a_kcontig else M)
+    ldb_ = ldb if ldb is not None else (K if b_kcontig else N)
+    ldc_ = ldc if ldc is not None else N
+    sC_ = sC if sC else M * ldc_
+    _check(min(M, N, K, batch) >= 1, f"bad GEMM dims M={M} N={N} K={K} batch={batch}")
+    _check(lda_ >= (K if a_kcontig else M) and ldb_ >= (K if b_kcontig else N) and ldc_ >= N, "bad leading dims")
+    _need(A, (batch - 1) * sA + ((M - 1) * lda_ + K if a_kcontig else (K - 1) * lda_ + M), "A")
+    _need(B, (batch - 1) * sB + ((N - 1) * ldb_ + K if b_kcontig else (K - 1) * ldb_ + N), "B")
+    _need(out, (batch - 1) * sC_ + (M - 1) * ldc_ + N, "C")
+    for t, nm in ((aux, "aux"), (aux_out, "aux_out"), (res1, "res1"), (res2, "res2")):
+        _need(t, M * N * batch, nm)
+    _need(bias, N, "bias")
     d = STRUCTS["lthm_gemm_desc"]()
     d.A, d.B, d.C = ptr(A), ptr(B), ptr(out)
     d.M, d.N, d.K = M, N, K
@@ -178,6 +221,8 @@ def linear_wgrad(dy2d, x2d, out=None, accumulate=False):
 def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
     require_gpu(x2d, w)
     M, D = x2d.shape
+    _need(w, D, "ln weight")
+    _need(b, D, "ln bias")
     y = torch.empty((M, D), dtype=y_dtype, device=x2d.device)
     mean = torch.empty(M, dtype=torch.float32, device=x2d.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x2d.device)
@@ -188,6 +233,11 @@ def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
 def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True):
     from ._lib import load
     M, D = x2d.shape
+    for t, nm in ((dy2d, "dy"), (res1, "res1"), (res2, "res2")):
+        _need(t, M * D, nm)
+    _need(w, D, "ln weight")
+    _need(mean, M, "mean")
+    _need(rstd, M, "rstd")
     nblk = load().lthm_layernorm_bwd_blocks(M)
     part = torch.empty((2, nblk, D), dtype=torch.float32, device=x2d.device)
     dx = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
@@ -202,6 +252,12 @@ def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True
 # ----------------------------------------------------------------- attention
 def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs):
     from ._lib import STRUCTS
+    _check(min(B, T, H, E) >= 1 and T <= 256, f"attention takes 1 <= T <= 256 (got B={B} T={T} H={H} E={E})")
+    _need(q, (B - 1) * T * q_ts + (T - 1) * q_ts + (H - 1) * E + E, "q")
+    _need(k, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "k")
+    _need(v, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "v")
+    _need(out, B * T * H * E, "out")
+    _need(lse, B * H * T, "lse")
     d = STRUCTS["lthm_attn_desc"]()
     d.q, d.k, d.v = ptr(q), ptr(k), ptr(v)
     d.q_tok_stride, d.k_tok_stride, d.v_tok_stride = q_ts, kv_ts, kv_ts
@@ -248,10 +304,19 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
 
 
 # ----------------------------------------------------------------- sparse KShift backward
-def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count):
-    """Accumulate into dense dW and append the touched rows (see include/lthm.h)."""
-    n = ids.numel() // F
+def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0):
+    """Accumulate into dense dW and append the touched rows (see include/lthm.h).
+    Table-batched layout: dW and flags cover all F*P rows; rows_list must hold
+    every row that can still be appended (<= F*P, <= pending + ids*K)."""
+    require_gpu(ids, gy, out, norms, dW, flags, rows_list, count)
     D = dW.shape[1]
+    _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0], gy=gy, out=out, norms=norms)
+    _check(dW.dtype == torch.float32, "dW must be float32")
+    _check(flags.dtype == torch.int32 and flags.numel() >= F * P, "flags must be int32 with >= F*P entries")
+    cap = min(F * P, pending + ids.numel() * K)
+    _check(rows_list.dtype == torch.int64 and rows_list.numel() >= cap, f"rows_list must be int64 with >= {cap} entries")
+    _check(count.dtype == torch.int64 and count.numel() >= 1, "count must be an int64 scalar buffer")
+    n = ids.numel() // F
     call("lthm_kshift_bwd_sparse", ptr(ids), n, F, ptr(gy), dcode(gy),
          ptr(out) if out is not None else None, dcode(out) if out is not None else F32, ptr(norms),
          P, D, K, mode, ptr(dW), ptr(flags), ptr(rows_list), ptr(count), stream())
@@ -259,20 +324,34 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
 
 # ----------------------------------------------------------------- optimizers / norms
 def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, zero_grad=False):
+    for t, nm in ((g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq"), (shadow, "shadow")):
+        _need(t, p.numel(), nm)
     call("lthm_adamw", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, betas[0], betas[1], eps, wd, step,
          grad_scale, ptr(shadow), int(zero_grad), stream())
 
 
 def adagrad_(p, g, s, lr, lr_decay, eps, wd, step, zero_grad=False):
+    _need(g, p.numel(), "grad")
+    _need(s, p.numel(), "state_sum")
     call("lthm_adagrad", ptr(p), ptr(g), ptr(s), p.numel(), lr, lr_decay, eps, wd, step, int(zero_grad), stream())
 
 
+def _check_sparse_rows(rows, max_rows, p, flags, *states):
+    _check(p.dim() == 2 and max_rows <= p.shape[0], "sparse update: p must be [R, D] and max_rows <= R")
+    _need(rows, max_rows, "rows")
+    _need(flags, p.shape[0], "flags")
+    for t in states:
+        _need(t, p.numel(), "state")
+
+
 def sparse_adamw_(rows, count, max_rows, p, g, m, v, flags, lr, betas, eps, wd, step, shadow=None):
+    _check_sparse_rows(rows, max_rows, p, flags, g, m, v, shadow)
     call("lthm_sparse_adamw", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(m), ptr(v),
          ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), stream())
 
 
 def sparse_adagrad_(rows, count, max_rows, p, g, s, flags, lr, lr_decay, eps, step, shadow=None):
+    _check_sparse_rows(rows, max_rows, p, flags, g, s, shadow)
     call("lthm_sparse_adagrad", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(s), ptr(flags),
          lr, lr_decay, eps, step, ptr(shadow), stream())
 
@@ -312,13 +391,30 @@ def flip_tokens(x):
     return out
 
 
+def _table_ws(dev, n, R, D):
+    """Partial-sum workspace for lthm_*_table_bwd: up to 32 token chunks of [R, D] f32."""
+    nz = max(1, min(32, (n + 511) // 512))
+    if nz < 2:
+        return None, 0
+    ws = _workspace(dev, nz * R * D * 4)
+    return ws, ws.numel() * 4
+
+
 def small_table_bwd(rows, dY, R, out=None):
     """rows uint16 stored as int16 [n, nidx]; dY [n, D] -> f32 [R, D] (accumulated into out)."""
+    require_gpu(rows, dY, out)
     n, nidx = rows.shape
     D = dY.shape[-1]
+    _check(rows.dtype == torch.int16 and dY.numel() == n * D, "rows must be int16 [n, nidx] and dY [n, D]")
+    _check(0 < nidx <= 64 and 0 < R < 0xFFFF, f"small_table_bwd takes nidx <= 64 slots and R < 65535 rows")
+    _check(R * 64 * 4 <= 160 * 1024, f"R={R} rows exceed the LDS slice; use segmented_table_bwd")
     if out is None:
         out = torch.zeros((R, D), dtype=torch.float32, device=dY.device)
-    call("lthm_small_table_bwd", ptr(rows), nidx, ptr(dY), dcode(dY), D, n, R, D, ptr(out), stream())
+    _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
+    ws, wsb = _table_ws(dY.device, n, R, D)
+    call("lthm_small_table_bwd", ptr(rows), nidx, ptr(dY), dcode(dY), D, n, R, D, ptr(out),
+         ptr(ws) if ws is not None else None, wsb, stream(), _key="small_tab_bwd_k",
+         _work=float(n) * D * dY.element_size(), _unit="byte")
     return out
 
 
@@ -444,4 +540,36 @@ def quantile_map(x, quantiles, shared):
     B, Fd = x.shape if x.dim() == 2 else (x.numel(), 1)
     out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
     call("lthm_quantile_map", ptr(x), B, Fd, ptr(quantiles), quantiles.shape[-1], int(shared), ptr(out), stream())
+    return out
+
+
+def cve_segments(n_proj: int, rows_per_slot: int, slot0: int = 0, row0: int = 0, max_rows: int = 256):
+    """Backward segments of one CosineVectorEmbedding module: projection p owns rows
+    [row0 + p*rows_per_slot, +rows_per_slot); runs of projections of <= max_rows
+    rows keep each block's LDS slice <= 64 KiB (two blocks per CU)."""
+    per = max(1, min(64, max_rows // rows_per_slot))
+    return [(slot0 + p0, min(per, n_proj - p0), row0 + p0 * rows_per_slot, min(per, n_proj - p0) * rows_per_slot)
+            for p0 in range(0, n_proj, per)]
+
+
+def segmented_table_bwd(rows, dY, R, segments, out=None):
+    """Like small_table_bwd, with slots grouped into (slot0, nslot, row0, nrow) segments."""
+    import numpy as _np
+    require_gpu(rows, dY, out)
+    n, nidx = rows.shape
+    D = dY.shape[-1]
+    _check(rows.dtype == torch.int16 and dY.numel() == n * D, "rows must be int16 [n, nidx] and dY [n, D]")
+    for s0, ns, r0, nr in segments:
+        _check(0 <= s0 and 0 < ns <= 64 and s0 + ns <= nidx, f"segment slots ({s0}, {ns}) outside [0, {nidx})")
+        _check(0 <= r0 and 0 < nr <= 640 and r0 + nr <= R, f"segment rows ({r0}, {nr}) outside [0, {R}) or > 640")
+    if out is None:
+        out = zeros((R, D), torch.float32, dY.device)
+    _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
+    ws, wsb = _table_ws(dY.device, n, R, D)
+    for g in range(0, len(segments), 64):  # the kernel takes <= 64 segments per launch
+        seg = _np.ascontiguousarray(_np.array(segments[g:g + 64], dtype=_np.int32).T)
+        call("lthm_segmented_table_bwd", ptr(rows), nidx, seg.shape[1], seg[0].ctypes.data, seg[1].ctypes.data,
+             seg[2].ctypes.data, seg[3].ctypes.data, ptr(dY), dcode(dY), D, n, D, ptr(out),
+             ptr(ws) if ws is not None else None, wsb, stream(),
+             _key="seg_tab_bwd_k", _work=float(n) * D * dY.element_size(), _unit="byte")
     return out

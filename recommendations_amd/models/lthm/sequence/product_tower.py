@@ -68,6 +68,13 @@ class ProductTowerFn(torch.autograd.Function):
         prod = K.linear_fwd(emb, w_pm_b)
         ctx.save_for_backward(rows, xn, emb, w_pm_b)
         ctx.meta = (R_cve, nb, [t.shape for t in tables], b_map is not None)
+        segs, so = [], 0  # backward segments per CVE module (+ the histogram slot)
+        for j, m in enumerate(cve):
+            segs += K.cve_segments(m.n_proj, m.num_bins + 1, so, d.mod_row_off[j])
+            so += m.n_proj
+        if nb:
+            segs.append((so, 1, R_cve, nb))
+        ctx.segments = segs
         ctx.mark_non_differentiable(mask)
         return emb.view(*ids.shape, Dout), prod.view(*ids.shape, -1), mask.view(ids.shape)
 
@@ -83,7 +90,7 @@ class ProductTowerFn(torch.autograd.Function):
         de = K.linear_dgrad(dpb, w_pm_b, res1=res)  # bf16 total gradient of `emb`
         dw_map = K.linear_wgrad(de, xn)
         db_map = K.colsum(de) if has_b else None
-        dtab = K.small_table_bwd(rows, de, R_cve + max(nb, 1))
+        dtab = K.segmented_table_bwd(rows, de, R_cve + max(nb, 1), ctx.segments)
         grads, r = [], 0
         for s in shapes:
             grads.append(dtab[r:r + s[0]])

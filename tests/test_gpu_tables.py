@@ -1,0 +1,118 @@
+"""GPU parity: small-table (EmbeddingBag / CVE / token-table) backward and the
+sparse touched-row list of the KShift backward.
+
+Table backward is an fp32 scatter-add whose summation order differs from the
+float64 reference below (index_add in double), so the bound is
+|err| <= 1e-5 * sum|contributions| per element.  The touched-row list is
+integer work: compared exactly, as a set, against the unique row ids.
+"""
+import numpy as np
+import pytest
+import torch
+
+from recommendations_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def table_ref(rows, dy, R, segments=None):
+    rows = rows.long() & 0xFFFF
+    n, nidx = rows.shape
+    out = torch.zeros((R, dy.shape[1]), dtype=torch.float64)
+    mag = torch.zeros_like(out)
+    slots = range(nidx) if segments is None else [s0 + i for s0, ns, _, _ in segments for i in range(ns)]
+    dyd = dy.double().cpu()
+    for i in slots:
+        r = rows[:, i].cpu()
+        keep = r != 0xFFFF
+        out.index_add_(0, r[keep], dyd[keep])
+        mag.index_add_(0, r[keep], dyd[keep].abs())
+    return out, mag
+
+
+def check(got, ref, mag):
+    err = (got.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-7).all()), float((err - 1e-5 * mag).max())
+
+
+@pytest.mark.parametrize("n,nidx,R,D,dt", [(1, 3, 7, 16, torch.float32), (5000, 5, 333, 256, torch.bfloat16),
+                                           (70000, 32, 96, 100, torch.float32), (2048, 64, 600, 64, torch.bfloat16)])
+def test_small_table_bwd(dev, n, nidx, R, D, dt):
+    g = torch.Generator().manual_seed(n + R)
+    rows = torch.randint(0, R, (n, nidx), generator=g, dtype=torch.int32)
+    rows[torch.rand((n, nidx), generator=g) < 0.1] = 0xFFFF  # skipped slots
+    rows = rows.to(torch.int16)  # uint16 bit pattern
+    dy = torch.randn((n, D), generator=g).to(dt)
+    got = K.small_table_bwd(rows.to(dev), dy.to(dev), R)
+    torch.cuda.synchronize()
+    ref, mag = table_ref(rows, dy, R)
+    check(got, ref, mag)
+
+
+@pytest.mark.parametrize("n,D", [(3, 256), (40000, 256), (9000, 48)])
+def test_segmented_table_bwd_cve_layout(dev, n, D):
+    """Product-tower layout: per CVE module, slot p owns rows [off + p*(nb+1), +nb+1),
+    split into <= 256-row runs, plus a one-slot histogram segment."""
+    g = torch.Generator().manual_seed(n)
+    bins = (2, 4, 8, 12, 16, 20)
+    nproj, segs, cols, so, ro = 32, [], [], 0, 0
+    for nb in bins:
+        rps = nb + 1
+        segs += K.cve_segments(nproj, rps, so, ro)
+        for p in range(nproj):
+            cols.append(ro + p * rps + torch.randint(0, rps, (n,), generator=g))
+        so += nproj
+        ro += rps * nproj
+    segs.append((so, 1, ro, 20))
+    cols.append(ro + torch.randint(0, 20, (n,), generator=g))
+    R = ro + 20
+    rows = torch.stack(cols, 1).to(torch.int32)
+    rows[:, 5][torch.rand(n, generator=g) < 0.3] = 0xFFFF
+    rows = rows.to(torch.int16)
+    dy = torch.randn((n, D), generator=g).to(torch.bfloat16)
+    got = K.segmented_table_bwd(rows.to(dev), dy.to(dev), R, segs)
+    torch.cuda.synchronize()
+    ref, mag = table_ref(rows, dy, R, segs)
+    check(got, ref, mag)
+
+
+def test_kshift_sparse_rejects_short_buffers(dev):
+    ids = torch.zeros((8, 4), dtype=torch.int64, device=dev)
+    dy = torch.zeros((8, 4, 32), dtype=torch.bfloat16, device=dev)
+    P = 100
+    dW = torch.zeros((P, 32), device=dev)  # needs F*P rows
+    flags = torch.zeros(4 * P, dtype=torch.int32, device=dev)
+    lst = torch.zeros(4 * P, dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError, match="F\\*P"):
+        K.kshift_bwd_sparse(ids, dy, None, None, P, 8, 0, 4, dW, flags, lst, torch.zeros(1, dtype=torch.int64, device=dev))
+
+
+def test_segmented_table_bwd_rejects_overlap(dev):
+    rows = torch.zeros((4, 2), dtype=torch.int16, device=dev)
+    dy = torch.ones((4, 8), device=dev)
+    with pytest.raises(RuntimeError):
+        K.segmented_table_bwd(rows, dy, 10, [(0, 1, 0, 6), (1, 1, 4, 6)])
+
+
+@pytest.mark.parametrize("P,D,Kk,F,n", [(1000, 32, 16, 1, 3000), (50000, 32, 8, 4, 20000)])
+def test_kshift_sparse_touched_rows(dev, P, D, Kk, F, n):
+    """lthm_kshift_bwd_sparse appends every touched row exactly once and flags it."""
+    from oracle.ref import kshift_rows
+    g = np.random.default_rng(P + n)
+    ids = g.integers(-2**63, 2**63 - 1, size=(n, F), dtype=np.int64)
+    ids[: n // 4] = ids[0]  # heavy duplication
+    dy = torch.randn((n, F, D), dtype=torch.float32).to(torch.bfloat16).to(dev)
+    # table-batched layout: feature f owns rows [f*P, (f+1)*P)
+    dW = torch.zeros((F * P, D), dtype=torch.float32, device=dev)
+    flags = torch.zeros(F * P, dtype=torch.int32, device=dev)
+    lst = torch.zeros(F * P, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    K.kshift_bwd_sparse(torch.from_numpy(ids).to(dev), dy, None, None, P, Kk, 0, F, dW, flags, lst, cnt)
+    torch.cuda.synchronize()
+    rows = kshift_rows(ids.reshape(-1), P, Kk).reshape(n, F, Kk) + (np.arange(F) * P)[None, :, None]
+    want = np.unique(rows.reshape(-1))
+    c = int(cnt.item())
+    got = np.sort(lst[:c].cpu().numpy())
+    np.testing.assert_array_equal(got, want)
+    fl = flags.cpu().numpy()
+    assert fl[want].all() and fl.sum() == len(want)

@@ -1,0 +1,48 @@
+"""Microbenchmark of the MFMA GEMM (csrc/gemm.hip) on the LTHM C2 encoder shapes,
+with torch.matmul (hipBLASLt) timed beside it as a yardstick only."""
+import sys
+import os
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from recommendations_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    dev = torch.device("cuda")
+    M = 4096 * 129
+    shapes = [("qkv", M, 768, 256), ("proj", M, 256, 256), ("fc", M, 1024, 256), ("fc2", M, 256, 1024),
+              ("sq4096", 4096, 4096, 4096)]
+    for name, m, n, k in shapes:
+        a = torch.randn(m, k, device=dev).to(torch.bfloat16)
+        w = torch.randn(n, k, device=dev).to(torch.bfloat16)
+        fl = 2.0 * m * n * k
+        t0 = timeit(lambda: K.linear_fwd(a, w))
+        t1 = timeit(lambda: K.linear_fwd(a, w, act=K.ACT_GELU, aux_out=None))
+        t2 = timeit(lambda: torch.matmul(a, w.T))
+        dy = torch.randn(m, n, device=dev).to(torch.bfloat16)
+        t3 = timeit(lambda: K.linear_dgrad(dy, w))
+        t4 = timeit(lambda: K.linear_wgrad(dy, a), iters=5)
+        t5 = timeit(lambda: torch.matmul(dy.T, a), iters=5)
+        print(f"{name:7s} M={m} N={n} K={k}: fwd {t0:.3f} ms ({fl / t0 / 1e9:.0f} TF)  +gelu {t1:.3f}  "
+              f"hipblaslt {t2:.3f} ({fl / t2 / 1e9:.0f} TF) | dgrad {t3:.3f} ({fl / t3 / 1e9:.0f} TF) | "
+              f"wgrad {t4:.3f} ({fl / t4 / 1e9:.0f} TF) hipblaslt {t5:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
