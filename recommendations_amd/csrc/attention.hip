@@ -233,6 +233,386 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnArgs a) {
   }
 }
 
+// ===========================================================================
+// MFMA path (E in {32, 64, 128}): v_mfma_f32_16x16x32_bf16 tiles.
+//
+// Fragment layouts (wave64, 16x16x32):  A[l&15][8(l>>4)+i],  B[8(l>>4)+i][l&15],
+// C[4(l>>4)+j][l&15].  Whole-head operands live in LDS "images": row-major
+// [Tk, E] bf16 with 16-byte chunks XOR-swizzled so that 16 consecutive rows
+// read at one chunk hit distinct banks (row-fragment reads), while
+// ds_read_tr16_b64 gives the k-strided B fragments (keys / queries as k).
+// Probabilities P and dS leave the C layout through a padded per-wave f32
+// scratch and enter the next MFMA as bf16 hi + lo halves, so the second
+// product (P.V, dS.K, P^T.dO, dS^T.Q) carries ~16 mantissa bits of P / dS.
+// ===========================================================================
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int SCR_LD = 36;  // scratch row stride (floats): conflict-free C-layout writes, 16 B aligned reads
+
+template <int E>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  constexpr int NC = E / 8;
+  constexpr int RPL = (256 / (2 * E)) > 0 ? 256 / (2 * E) : 1;  // rows per 256-byte bank line
+  return row * (2 * E) + ((ch ^ ((row / RPL) & (NC - 1))) << 4);
+}
+
+// stage rows [0, Tk) of a head (row r at src + r*ts) into an image; rows >= T are zero
+template <int E>
+__device__ __forceinline__ void stage_img(unsigned char* img, const bf16_t* __restrict__ src, int64_t ts, int T, int Tk,
+                                          int tid) {
+  constexpr int NC = E / 8;
+  for (int idx = tid; idx < Tk * NC; idx += 256) {
+    const int r = idx / NC, c = idx - r * NC;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r < T) v = *reinterpret_cast<const u32x4*>(src + (int64_t)r * ts + c * 8);
+    *reinterpret_cast<u32x4*>(img + img_off<E>(r, c)) = v;
+  }
+}
+
+// row fragment: B[k = 32s + 8(l>>4) + i][n = row0 + (l&15)] = img[row0 + (l&15)][32s + ...]
+template <int E>
+__device__ __forceinline__ bf16x8v img_row_frag(const unsigned char* img, int row0, int s, int lane) {
+  return __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + img_off<E>(row0 + (lane & 15), s * 4 + (lane >> 4))));
+}
+
+// transposed fragment: B[k = kb + 8(l>>4) + i][n = nb + (l&15)] = img[kb + ...][nb + (l&15)]
+template <int E>
+__device__ __forceinline__ bf16x8v img_tr_frag(const unsigned char* img, int kb, int nb, int lane) {
+  const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int kr = kb + 8 * gq + q;
+  const int ch = (nb >> 3) + (p >> 1);
+  const unsigned char* a0 = img + img_off<E>(kr, ch) + 8 * (p & 1);
+  const unsigned char* a1 = img + img_off<E>(kr + 4, ch) + 8 * (p & 1);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// A fragments of 16 global rows r0 + (l&15) (zero for rows >= T)
+template <int E>
+__device__ __forceinline__ void glob_row_frags(bf16x8v (&f)[E / 32], const bf16_t* __restrict__ base, int64_t ts, int r0,
+                                               int T, int lane) {
+  const int r = r0 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < E / 32; ++s) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r < T) v = *reinterpret_cast<const u32x4*>(base + (int64_t)r * ts + (s * 4 + (lane >> 4)) * 8);
+    f[s] = __builtin_bit_cast(bf16x8v, v);
+  }
+}
+
+// C-layout pair (cols 0..15, 16..31) -> A fragment (k = 32 cols) as bf16 hi + lo
+__device__ __forceinline__ void c_to_a_split(float* scr, const f32x4& c0, const f32x4& c1, int lane, bf16x8v& hi,
+                                             bf16x8v& lo) {
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    scr[(rg + j) * SCR_LD + col] = c0[j];
+    scr[(rg + j) * SCR_LD + 16 + col] = c1[j];
+  }
+  __builtin_amdgcn_wave_barrier();
+  const float* rp = scr + (lane & 15) * SCR_LD + 8 * (lane >> 4);
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp);
+  const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + 4);
+  __builtin_amdgcn_wave_barrier();
+  s16x8 h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float v = i < 4 ? x0[i] : x1[i - 4];
+    const uint32_t u = __float_as_uint(v) & 0xffff0000u;  // truncated high half (exact remainder below)
+    h[i] = (short)(u >> 16);
+    l[i] = (short)f2bf(v - __uint_as_float(u));
+  }
+  hi = __builtin_bit_cast(bf16x8v, h);
+  lo = __builtin_bit_cast(bf16x8v, l);
+}
+
+__device__ __forceinline__ float row16_max(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+template <int E>
+__global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NS = E / 32, NE = E / 16;
+  const int T = a.T, Tk = (T + 31) & ~31, Tq = (T + 15) & ~15;
+  unsigned char* Ki = smem;
+  unsigned char* Vi = Ki + Tk * E * 2;
+  float* bias = reinterpret_cast<float*>(Vi + Tk * E * 2);  // [2T+1], region padded to 16 B
+  float* scr_all = bias + ((2 * T + 4) & ~3);                 // [4][16][SCR_LD], 16 B aligned
+  const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  stage_img<E>(Ki, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, T, Tk, tid);
+  stage_img<E>(Vi, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, T, Tk, tid);
+  for (int i = tid; i <= 2 * T; i += 256) bias[i] = a.table ? a.table[(int64_t)i * a.H + h] : 0.f;
+  __syncthreads();
+  float* scr = scr_all + wave * 16 * SCR_LD;
+  const float rs = rsqrtf((float)E);
+  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  for (int q0 = wave * 16; q0 < Tq; q0 += 64) {
+    bf16x8v qf[NS];
+    glob_row_frags<E>(qf, qg, a.q_ts, q0, T, lane);
+    f32x4 o[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) o[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
+    const int kend = a.causal ? min(Tk, (q0 + 16 + 31) & ~31) : Tk;
+    for (int k0 = 0; k0 < kend; k0 += 32) {
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s0 = MFMA(qf[s], img_row_frag<E>(Ki, k0, s, lane), s0);
+        s1 = MFMA(qf[s], img_row_frag<E>(Ki, k0 + 16, s, lane), s1);
+      }
+      float bm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + rg + j;
+        const int ka = k0 + col, kb = k0 + 16 + col;
+        const bool va = q < T && ka < T && (!a.causal || ka <= q);
+        const bool vb = q < T && kb < T && (!a.causal || kb <= q);
+        s0[j] = va ? s0[j] * rs + bias[q - ka + T] : -INFINITY;
+        s1[j] = vb ? s1[j] * rs + bias[q - kb + T] : -INFINITY;
+        bm[j] = row16_max(fmaxf(s0[j], s1[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float mn = fmaxf(m[j], bm[j]);
+        const float alpha = (mn == -INFINITY) ? 1.f : __expf(m[j] - mn);
+        m[j] = mn;
+        const float pa = (s0[j] == -INFINITY) ? 0.f : __expf(s0[j] - mn);
+        const float pb = (s1[j] == -INFINITY) ? 0.f : __expf(s1[j] - mn);
+        s0[j] = pa;
+        s1[j] = pb;
+        l[j] = l[j] * alpha + pa + pb;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) o[e][j] *= alpha;
+      }
+      bf16x8v ph, pl;
+      c_to_a_split(scr, s0, s1, lane, ph, pl);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const bf16x8v vf = img_tr_frag<E>(Vi, k0, e * 16, lane);
+        o[e] = MFMA(ph, vf, o[e]);
+        o[e] = MFMA(pl, vf, o[e]);
+      }
+    }
+    bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = q0 + rg + j;
+      const float lt = row16_sum(l[j]);
+      if (q < T) {
+        const float inv = 1.f / lt;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) og[(int64_t)q * a.o_ts + e * 16 + col] = f2bf(o[e][j] * inv);
+        if (col == 0) a.lse[((int64_t)b * a.H + h) * T + q] = m[j] + __logf(lt);
+      }
+    }
+  }
+}
+
+// Backward, blockIdx.y == 0: query tiles -> dQ and the bias gradient.
+//           blockIdx.y == 1: key tiles   -> dK and dV.
+// P = exp(S - lse) is recomputed from the forward's LSE; delta = rowsum(dO * O).
+template <int E>
+__global__ __launch_bounds__(256) void attn_bwd_mfma_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NS = E / 32, NE = E / 16;
+  const int T = a.T, Tk = (T + 31) & ~31, Tq = (T + 15) & ~15;
+  unsigned char* I0 = smem;                 // pass 0: K image, pass 1: Q image
+  unsigned char* I1 = I0 + Tk * E * 2;      // pass 0: V image, pass 1: dO image
+  float* bias = reinterpret_cast<float*>(I1 + Tk * E * 2);  // [2T+2]
+  float* dbias = bias + 2 * T + 2;                            // [2T+2]
+  float* lse = dbias + 2 * T + 2;                             // [Tk]
+  float* delta = lse + Tk;                                    // [Tk]
+  float* scr_all = delta + Tk;                                // [4][16][SCR_LD]
+  const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
+  const bool rows_pass = blockIdx.y == 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+  const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+  const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+  const bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+  const bf16_t* dog = a.dout + b * a.o_bs + h * a.o_hs;
+  if (rows_pass) {
+    stage_img<E>(I0, kg, a.k_ts, T, Tk, tid);
+    stage_img<E>(I1, vg, a.v_ts, T, Tk, tid);
+  } else {
+    stage_img<E>(I0, qg, a.q_ts, T, Tk, tid);
+    stage_img<E>(I1, dog, a.o_ts, T, Tk, tid);
+  }
+  for (int i = tid; i < 2 * T + 2; i += 256) {
+    bias[i] = (a.table && i <= 2 * T) ? a.table[(int64_t)i * a.H + h] : 0.f;
+    dbias[i] = 0.f;
+  }
+  const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  for (int i = tid; i < Tk; i += 256) lse[i] = i < T ? lse_g[i] : 0.f;
+  // delta[q] = dO[q] . O[q]  (a wave per row, bf16 products in f32)
+  for (int q = wave; q < Tk; q += 4) {
+    float d = 0.f;
+    if (q < T)
+      for (int e = lane; e < E; e += 64) d += bf2f(dog[(int64_t)q * a.o_ts + e]) * bf2f(og[(int64_t)q * a.o_ts + e]);
+    d = wave_sum(d);
+    if (lane == 0) delta[q] = d;
+  }
+  __syncthreads();
+  float* scr = scr_all + wave * 16 * SCR_LD;
+  const float rs = rsqrtf((float)E);
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  if (rows_pass) {
+    for (int q0 = wave * 16; q0 < Tq; q0 += 64) {
+      bf16x8v qf[NS], df[NS];
+      glob_row_frags<E>(qf, qg, a.q_ts, q0, T, lane);
+      glob_row_frags<E>(df, dog, a.o_ts, q0, T, lane);
+      f32x4 dq[NE];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) dq[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float lq[4], dl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lq[j] = lse[min(q0 + rg + j, Tk - 1)]; dl[j] = delta[min(q0 + rg + j, Tk - 1)]; }
+      const int kend = a.causal ? min(Tk, (q0 + 16 + 31) & ~31) : Tk;
+      for (int k0 = 0; k0 < kend; k0 += 32) {
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, p0 = s0, p1 = s0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          s0 = MFMA(qf[s], img_row_frag<E>(I0, k0, s, lane), s0);
+          s1 = MFMA(qf[s], img_row_frag<E>(I0, k0 + 16, s, lane), s1);
+          p0 = MFMA(df[s], img_row_frag<E>(I1, k0, s, lane), p0);
+          p1 = MFMA(df[s], img_row_frag<E>(I1, k0 + 16, s, lane), p1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = q0 + rg + j;
+          const int ka = k0 + col, kb = k0 + 16 + col;
+          const bool va = q < T && ka < T && (!a.causal || ka <= q);
+          const bool vb = q < T && kb < T && (!a.causal || kb <= q);
+          const float da = va ? __expf(s0[j] * rs + bias[q - ka + T] - lq[j]) * (p0[j] - dl[j]) : 0.f;
+          const float db = vb ? __expf(s1[j] * rs + bias[q - kb + T] - lq[j]) * (p1[j] - dl[j]) : 0.f;
+          if (va) atomicAdd(&dbias[q - ka + T], da);
+          if (vb) atomicAdd(&dbias[q - kb + T], db);
+          s0[j] = da;
+          s1[j] = db;
+        }
+        bf16x8v gh, gl;
+        c_to_a_split(scr, s0, s1, lane, gh, gl);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const bf16x8v kf = img_tr_frag<E>(I0, k0, e * 16, lane);
+          dq[e] = MFMA(gh, kf, dq[e]);
+          dq[e] = MFMA(gl, kf, dq[e]);
+        }
+      }
+      bf16_t* dqg = a.dq + b * a.q_bs + h * a.q_hs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + rg + j;
+        if (q < T)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) dqg[(int64_t)q * a.q_ts + e * 16 + col] = f2bf(dq[e][j] * rs);
+      }
+    }
+    __syncthreads();
+    if (a.dtable_part)
+      for (int i = tid; i <= 2 * T; i += 256) a.dtable_part[((int64_t)b * (2 * T + 1) + i) * a.H + h] = dbias[i];
+  } else {
+    for (int k0 = wave * 16; k0 < Tq; k0 += 64) {
+      bf16x8v kf[NS], vf[NS];
+      glob_row_frags<E>(kf, kg, a.k_ts, k0, T, lane);
+      glob_row_frags<E>(vf, vg, a.v_ts, k0, T, lane);
+      f32x4 dk[NE], dv[NE];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) { dk[e] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[e] = dk[e]; }
+      const int qbeg = a.causal ? (k0 & ~31) : 0;
+      for (int q0 = qbeg; q0 < Tk; q0 += 32) {
+        // transposed scores: rows = keys k0 + rg + j, cols = queries q0 + col (+16)
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, p0 = s0, p1 = s0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          s0 = MFMA(kf[s], img_row_frag<E>(I0, q0, s, lane), s0);
+          s1 = MFMA(kf[s], img_row_frag<E>(I0, q0 + 16, s, lane), s1);
+          p0 = MFMA(vf[s], img_row_frag<E>(I1, q0, s, lane), p0);
+          p1 = MFMA(vf[s], img_row_frag<E>(I1, q0 + 16, s, lane), p1);
+        }
+        const int qa = q0 + col, qb = q0 + 16 + col;
+        const float la = lse[qa], lb = lse[qb], da_ = delta[qa], db_ = delta[qb];
+        f32x4 g0, g1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + rg + j;
+          const bool va = k < T && qa < T && (!a.causal || k <= qa);
+          const bool vb = k < T && qb < T && (!a.causal || k <= qb);
+          const float pa = va ? __expf(s0[j] * rs + bias[qa - k + T] - la) : 0.f;
+          const float pb = vb ? __expf(s1[j] * rs + bias[qb - k + T] - lb) : 0.f;
+          g0[j] = pa * (p0[j] - da_);
+          g1[j] = pb * (p1[j] - db_);
+          s0[j] = pa;
+          s1[j] = pb;
+        }
+        bf16x8v ph, pl, gh, gl;
+        c_to_a_split(scr, s0, s1, lane, ph, pl);
+        c_to_a_split(scr, g0, g1, lane, gh, gl);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const bf16x8v dof = img_tr_frag<E>(I1, q0, e * 16, lane);
+          dv[e] = MFMA(ph, dof, dv[e]);
+          dv[e] = MFMA(pl, dof, dv[e]);
+          const bf16x8v qf = img_tr_frag<E>(I0, q0, e * 16, lane);
+          dk[e] = MFMA(gh, qf, dk[e]);
+          dk[e] = MFMA(gl, qf, dk[e]);
+        }
+      }
+      bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
+      bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + rg + j;
+        if (k < T)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            dkg[(int64_t)k * a.k_ts + e * 16 + col] = f2bf(dk[e][j] * rs);
+            dvg[(int64_t)k * a.v_ts + e * 16 + col] = f2bf(dv[e][j]);
+          }
+      }
+    }
+  }
+}
+#undef MFMA
+
+static size_t fwd_mfma_lds(int T, int E) {
+  const int Tk = (T + 31) & ~31;
+  return (size_t)2 * Tk * E * 2 + (size_t)((2 * T + 4) & ~3) * 4 + (size_t)4 * 16 * SCR_LD * 4;
+}
+static size_t bwd_mfma_lds(int T, int E) {
+  const int Tk = (T + 31) & ~31;
+  return (size_t)2 * Tk * E * 2 + (size_t)(2 * T + 2) * 8 + (size_t)2 * Tk * 4 + (size_t)4 * 16 * SCR_LD * 4;
+}
+
+template <int E>
+static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
+  const size_t sh = bwd ? bwd_mfma_lds(a.T, E) : fwd_mfma_lds(a.T, E);
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (bwd) hipLaunchKernelGGL((attn_bwd_mfma_k<E>), dim3(B * a.H, 2), dim3(256), sh, s, a);
+  else hipLaunchKernelGGL((attn_fwd_mfma_k<E>), dim3(B * a.H), dim3(256), sh, s, a);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
 static size_t fwd_lds(int T, int E) { return (size_t)2 * T * (E + ROWPAD) * 2 + (size_t)(2 * T + 2) * 4 + (size_t)4 * T * 4; }
 static size_t bwd_lds(int T, int E) {
   return (size_t)4 * T * (E + ROWPAD) * 2 + (size_t)(2 * T + 2) * 8 + (size_t)2 * T * 4 + (size_t)8 * T * 4;
@@ -262,9 +642,9 @@ static int attn_launch(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
   switch (E) {
     case 16: return attn_launch<16>(a, B, bwd, s);
-    case 32: return attn_launch<32>(a, B, bwd, s);
-    case 64: return attn_launch<64>(a, B, bwd, s);
-    case 128: return attn_launch<128>(a, B, bwd, s);
+    case 32: return attn_launch_mfma<32>(a, B, bwd, s);
+    case 64: return attn_launch_mfma<64>(a, B, bwd, s);
+    case 128: return attn_launch_mfma<128>(a, B, bwd, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
