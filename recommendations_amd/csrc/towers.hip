@@ -233,6 +233,152 @@ __global__ __launch_bounds__(256) void seg_tab_reduce_k(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ CVE table gradient on MFMA
+// For tables laid out like the CosineVectorEmbedding modules (module j: slots
+// [slot0_j, +nslot_j), slot s owning rows [row0_j + (s - slot0_j)*rps_j, +rps_j)):
+//     dW[m, :] += sum_t [rows[t, s(m)] == m] * dY[t, :]
+// is a one-hot GEMM  dW[M, D] = A[M, tokens] . dY[tokens, D]  with A built on
+// the fly (one compare per element; A is exactly 0/1 in bf16 and dY is bf16, so
+// every product is exact and only the f32 summation order differs from a
+// scatter-add).  Block = 8 waves = 128 table rows (one 16-row MFMA tile per
+// wave) x all D columns; tokens stream through LDS 32 at a time, double-buffered
+// (dY as a swizzled [32, D] image read with ds_read_tr16_b64, bucket ids
+// transposed to [slot][token]).  Token chunks (blockIdx.z) write f32 partials
+// that seg_tab_reduce_k folds in a fixed order.  Replaces the LDS-atomic scatter
+// for this layout: LDS float atomics sustain ~1 slot-update per ~190 CU cycles.
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int CT_MAXTILE = 64;
+constexpr int CT_ROWS = 128;   // rows per tile (8 waves x 16)
+constexpr int CT_KT = 32;      // tokens per k-step
+constexpr int CT_MAXSL = 128;  // slots covering one tile
+struct CveTiles {
+  int ntile;
+  int row0[CT_MAXTILE], nrow[CT_MAXTILE], sfirst[CT_MAXTILE], nsl[CT_MAXTILE];
+  int mrow0[CT_MAXTILE], mslot0[CT_MAXTILE], rps[CT_MAXTILE];
+};
+
+template <int D>
+__device__ __forceinline__ int ct_off(int row, int ch) {
+  constexpr int NC = D / 8;
+  constexpr int RPL = (256 / (2 * D)) > 0 ? 256 / (2 * D) : 1;
+  return row * (2 * D) + ((ch ^ ((row / RPL) & (NC - 1))) << 4);
+}
+
+template <int D>
+__device__ __forceinline__ bf16x8v ct_tr_frag(const unsigned char* img, int nb, int lane) {
+  const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int kr = 8 * gq + q;
+  const int ch = (nb >> 3) + (p >> 1);
+  const unsigned char* a0 = img + ct_off<D>(kr, ch) + 8 * (p & 1);
+  const unsigned char* a1 = img + ct_off<D>(kr + 4, ch) + 8 * (p & 1);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx,
+                                                    const bf16_t* __restrict__ dY, int64_t ldy, int64_t n,
+                                                    float* __restrict__ dst, int64_t zstride, int direct,
+                                                    int64_t tok_per_block, CveTiles ct) {
+  constexpr int NF = D / 16;
+  constexpr int NCH = D / 8;                    // 16-byte chunks per dY row
+  constexpr int IMG = CT_KT * D * 2;            // dY image bytes
+  constexpr int RTB = CT_MAXSL * CT_KT * 2;     // bucket-id tile bytes
+  constexpr int BUF = IMG + RTB;
+  constexpr int PD = (CT_KT * NCH + 511) / 512;
+  constexpr int PR = (CT_KT * CT_MAXSL + 511) / 512;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tile = blockIdx.x;
+  const int row0 = ct.row0[tile], nrow = ct.nrow[tile], sfirst = ct.sfirst[tile], nsl = ct.nsl[tile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t t0 = (int64_t)blockIdx.z * tok_per_block;
+  const int64_t t1 = min(n, t0 + tok_per_block);
+  const int ml = wave * 16 + (lane & 15);
+  const bool mvalid = ml < nrow;
+  const int m = row0 + ml;
+  const int ls = mvalid ? ct.mslot0[tile] + (m - ct.mrow0[tile]) / ct.rps[tile] - sfirst : 0;
+  f32x4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 pd[PD];
+  uint16_t pr[PR];
+  auto fetch = [&](int64_t tb) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int idx = tid + 512 * k;
+      const int r = idx / NCH, c = idx - r * NCH;
+      pd[k] = u32x4{0u, 0u, 0u, 0u};
+      if (idx < CT_KT * NCH && tb + r < t1) pd[k] = *reinterpret_cast<const u32x4*>(dY + (tb + r) * ldy + c * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int idx = tid + 512 * k;
+      const int r = idx / nsl, s = idx - r * nsl;
+      pr[k] = 0xffff;
+      if (idx < CT_KT * nsl && tb + r < t1) pr[k] = rows[(tb + r) * nidx + sfirst + s];
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned char* img = smem + buf * BUF;
+    uint16_t* rt = reinterpret_cast<uint16_t*>(img + IMG);
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int idx = tid + 512 * k;
+      const int r = idx / NCH, c = idx - r * NCH;
+      if (idx < CT_KT * NCH) *reinterpret_cast<u32x4*>(img + ct_off<D>(r, c)) = pd[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int idx = tid + 512 * k;
+      const int r = idx / nsl, s = idx - r * nsl;
+      if (idx < CT_KT * nsl) rt[s * CT_KT + r] = pr[k];
+    }
+  };
+  const int64_t nsteps = (t1 - t0 + CT_KT - 1) / CT_KT;
+  if (nsteps > 0) {
+    fetch(t0);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t st = 0; st < nsteps; ++st) {
+    const int cur = (int)(st & 1);
+    if (st + 1 < nsteps) fetch(t0 + (st + 1) * CT_KT);  // global loads in flight during the MFMAs
+    const unsigned char* img = smem + cur * BUF;
+    const uint16_t* rt = reinterpret_cast<const uint16_t*>(img + IMG);
+    const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls * CT_KT + 8 * (lane >> 4));
+    s16x8 a;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
+      a[i] = (mvalid && (int)rr == m) ? (short)0x3F80 : (short)0;
+    }
+    const bf16x8v af = __builtin_bit_cast(bf16x8v, a);
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img, f * 16, lane), acc[f], 0, 0, 0);
+    if (st + 1 < nsteps) store(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = dst + (direct ? 0 : (int64_t)blockIdx.z * zstride);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rl = wave * 16 + 4 * (lane >> 4) + j;
+    if (rl < nrow) {
+      float* p = out + (int64_t)(row0 + rl) * D + (lane & 15);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        if (direct) p[f * 16] += acc[f][j];
+        else p[f * 16] = acc[f][j];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ token assembly
 // x0[b, 0]   = wpe[T] (+ ctx[b])
 // x0[b, t+1] = (mask ? pad : P[b,t] + act[lab] + hod[.] + how[.] + dow[.]) + wpe[T-1-t]
@@ -410,6 +556,74 @@ extern "C" int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int3
     const int bx = (int)std::min<int64_t>(((int64_t)maxr * D + 255) / 256, 256);
     hipLaunchKernelGGL(seg_tab_reduce_k, dim3(bx, nseg), dim3(256), 0, s, (const float*)workspace, zs, (int)gz, D, dW,
                        st);
+    LTHM_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int lthm_cve_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nmod, const int32_t* mod_slot0,
+                                  const int32_t* mod_nslot, const int32_t* mod_row0, const int32_t* mod_rps,
+                                  const void* dY, int64_t ldy, int64_t n, int32_t D, float* dW, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  LTHM_REQUIRE(n >= 0 && nidx > 0 && nmod > 0 && nmod <= 16);
+  LTHM_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128 || D == 256);
+  if (n == 0) return 0;
+  CveTiles ct;
+  SegTab st;  // the same row ranges, for the partial-sum fold
+  int nt = 0, rtot = 0;
+  for (int j = 0; j < nmod; ++j) {
+    const int s0 = mod_slot0[j], ns = mod_nslot[j], r0 = mod_row0[j], rps = mod_rps[j];
+    LTHM_REQUIRE(s0 >= 0 && ns > 0 && s0 + ns <= nidx && r0 >= 0 && rps > 0 && (int64_t)ns * rps < 65535);
+    for (int k = 0; k < j; ++k)  // module row ranges are disjoint
+      LTHM_REQUIRE(r0 + ns * rps <= mod_row0[k] || mod_row0[k] + mod_nslot[k] * mod_rps[k] <= r0);
+    const int tot = ns * rps;
+    for (int r = 0; r < tot; r += CT_ROWS) {
+      LTHM_REQUIRE(nt < CT_MAXTILE);
+      const int nr = std::min(CT_ROWS, tot - r);
+      ct.row0[nt] = r0 + r;
+      ct.nrow[nt] = nr;
+      ct.sfirst[nt] = s0 + r / rps;
+      ct.nsl[nt] = (r + nr - 1) / rps - r / rps + 1;
+      LTHM_REQUIRE(ct.nsl[nt] <= CT_MAXSL);
+      ct.mrow0[nt] = r0;
+      ct.mslot0[nt] = s0;
+      ct.rps[nt] = rps;
+      st.row0[nt] = r0 + r;
+      st.nrow[nt] = nr;
+      st.slot0[nt] = 0;
+      st.nslot[nt] = 1;
+      ++nt;
+    }
+    rtot = std::max(rtot, r0 + tot);
+  }
+  ct.ntile = nt;
+  st.nseg = nt;
+  const int64_t zbytes = (int64_t)rtot * D * 4;
+  int64_t gz = (512 + nt - 1) / nt;  // ~2 blocks of 512 threads per CU
+  gz = std::min<int64_t>(gz, (n + 1023) / 1024);
+  gz = std::min<int64_t>(gz, workspace ? workspace_bytes / zbytes : (int64_t)1);
+  if (gz < 2) gz = 1;
+  int64_t tpb = (n + gz - 1) / gz;
+  tpb = (tpb + CT_KT - 1) / CT_KT * CT_KT;
+  gz = (n + tpb - 1) / tpb;
+  const int direct = gz == 1;
+  float* dst = direct ? dW : (float*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t sh = 2 * ((size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_KT * 2);
+  dim3 grid(nt, 1, (unsigned)gz);
+  const bf16_t* y = (const bf16_t*)dY;
+  switch (D) {
+    case 16: hipLaunchKernelGGL((cve_tab_bwd_k<16>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+    case 32: hipLaunchKernelGGL((cve_tab_bwd_k<32>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+    case 64: hipLaunchKernelGGL((cve_tab_bwd_k<64>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+    case 128: hipLaunchKernelGGL((cve_tab_bwd_k<128>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+    default: hipLaunchKernelGGL((cve_tab_bwd_k<256>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+  }
+  LTHM_CHECK_LAUNCH();
+  if (!direct) {
+    const int bx = (int)std::min<int64_t>(((int64_t)CT_ROWS * D + 255) / 256, 256);
+    hipLaunchKernelGGL(seg_tab_reduce_k, dim3(bx, nt), dim3(256), 0, s, (const float*)workspace, zbytes / 4, (int)gz, D,
+                       dW, st);
     LTHM_CHECK_LAUNCH();
   }
   return 0;

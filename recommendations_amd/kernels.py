@@ -26,10 +26,15 @@ def kshift_rows(ids: torch.Tensor, P: int, K: int) -> torch.Tensor:
     return rows
 
 
+class OperandError(RuntimeError, ValueError):
+    """Bad op argument, caught on the host before any launch.  A RuntimeError like
+    the reference's own argument errors (transformers/layers.py:26-29)."""
+
+
 def _check(cond, msg):
     """Host-side operand check before a launch: the kernels trust their sizes."""
     if not cond:
-        raise ValueError(msg)
+        raise OperandError(msg)
 
 
 def _need(t, n: int, name: str):
@@ -540,6 +545,31 @@ def quantile_map(x, quantiles, shared):
     B, Fd = x.shape if x.dim() == 2 else (x.numel(), 1)
     out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
     call("lthm_quantile_map", ptr(x), B, Fd, ptr(quantiles), quantiles.shape[-1], int(shared), ptr(out), stream())
+    return out
+
+
+def cve_table_bwd(rows, dY, R, modules, out=None):
+    """MFMA one-hot gradient of CVE-structured tables (include/lthm.h lthm_cve_table_bwd).
+    modules: [(slot0, nslot, row0, rows_per_slot)]; dY bf16 [n, D], D in {16..256} pow2."""
+    import numpy as _np
+    require_gpu(rows, dY, out)
+    n, nidx = rows.shape
+    D = dY.shape[-1]
+    _check(rows.dtype == torch.int16 and dY.dtype == torch.bfloat16 and dY.numel() == n * D,
+           "rows must be int16 [n, nidx] and dY bf16 [n, D]")
+    _check(D in (16, 32, 64, 128, 256), f"cve_table_bwd takes D in 16..256 (power of two), got {D}")
+    _check(0 < len(modules) <= 16, "1..16 modules")
+    for s0, ns, r0, rps in modules:
+        _check(0 <= s0 and ns > 0 and s0 + ns <= nidx, f"module slots ({s0}, {ns}) outside [0, {nidx})")
+        _check(0 <= r0 and rps > 0 and r0 + ns * rps <= R, f"module rows ({r0}, {ns}x{rps}) outside [0, {R})")
+    if out is None:
+        out = zeros((R, D), torch.float32, dY.device)
+    _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
+    ws, wsb = _table_ws(dY.device, n, R, D)
+    m = _np.ascontiguousarray(_np.array(modules, dtype=_np.int32).T)
+    call("lthm_cve_table_bwd", ptr(rows), nidx, m.shape[1], m[0].ctypes.data, m[1].ctypes.data, m[2].ctypes.data,
+         m[3].ctypes.data, ptr(dY), D, n, D, ptr(out), ptr(ws) if ws is not None else None, wsb, stream(),
+         _key="cve_tab_bwd_k", _work=2.0 * n * D * sum(ns * rps for _, ns, _, rps in modules), _unit="flop")
     return out
 
 

@@ -68,13 +68,13 @@ class ProductTowerFn(torch.autograd.Function):
         prod = K.linear_fwd(emb, w_pm_b)
         ctx.save_for_backward(rows, xn, emb, w_pm_b)
         ctx.meta = (R_cve, nb, [t.shape for t in tables], b_map is not None)
-        segs, so = [], 0  # backward segments per CVE module (+ the histogram slot)
+        mods, so = [], 0  # backward layout: per CVE module (slot0, n_proj, row0, nb+1) + the histogram slot
         for j, m in enumerate(cve):
-            segs += K.cve_segments(m.n_proj, m.num_bins + 1, so, d.mod_row_off[j])
+            mods.append((so, m.n_proj, d.mod_row_off[j], m.num_bins + 1))
             so += m.n_proj
         if nb:
-            segs.append((so, 1, R_cve, nb))
-        ctx.segments = segs
+            mods.append((so, 1, R_cve, nb))
+        ctx.modules = mods
         ctx.mark_non_differentiable(mask)
         return emb.view(*ids.shape, Dout), prod.view(*ids.shape, -1), mask.view(ids.shape)
 
@@ -90,7 +90,14 @@ class ProductTowerFn(torch.autograd.Function):
         de = K.linear_dgrad(dpb, w_pm_b, res1=res)  # bf16 total gradient of `emb`
         dw_map = K.linear_wgrad(de, xn)
         db_map = K.colsum(de) if has_b else None
-        dtab = K.segmented_table_bwd(rows, de, R_cve + max(nb, 1), ctx.segments)
+        R = R_cve + max(nb, 1)
+        if Dout in (16, 32, 64, 128, 256) and len(ctx.modules) <= 16:
+            dtab = K.cve_table_bwd(rows, de, R, ctx.modules)
+        else:
+            segs = []
+            for s0, ns, r0, rps in ctx.modules:
+                segs += K.cve_segments(ns, rps, s0, r0)
+            dtab = K.segmented_table_bwd(rows, de, R, segs)
         grads, r = [], 0
         for s in shapes:
             grads.append(dtab[r:r + s[0]])

@@ -133,10 +133,13 @@ def test_attention_vs_oracle(dev, B, T, H, E, causal):
     exp.backward(dout.float())
     dqkv, dtab = K.attn_bwd_qkv(qkv.to(dev), out, dout.to(dev), lse, B, T, H, E, table.to(dev), causal)
     dq, dk, dv = dqkv.float().cpu().view(B, T, 3, H, E).permute(2, 0, 3, 1, 4)
-    assert relerr(dq, q.grad) < 1e-2
-    assert relerr(dk, k.grad) < 1e-2
-    assert relerr(dv, v.grad) < 1e-2
-    assert relerr(dtab, tab.grad[: 2 * T + 1]) < 1e-2
+    # relative Frobenius 1e-2; gradients that are exactly zero (T = 1: softmax over
+    # one key) are checked against an absolute 1e-4 instead
+    for got, want in ((dq, q.grad), (dk, k.grad), (dv, v.grad), (dtab, tab.grad[: 2 * T + 1])):
+        if float(want.norm()) == 0.0:
+            assert float(got.abs().max()) < 1e-4
+        else:
+            assert relerr(got, want) < 1e-2
 
 
 def _cfg(d, H, bias, causal, pos):

@@ -76,6 +76,52 @@ def test_segmented_table_bwd_cve_layout(dev, n, D):
     check(got, ref, mag)
 
 
+def _cve_case(n, D, bins=(2, 4, 8, 12, 16, 20), nproj=32, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mods, cols, so, ro = [], [], 0, 0
+    for nb in bins:
+        rps = nb + 1
+        mods.append((so, nproj, ro, rps))
+        for p in range(nproj):
+            cols.append(ro + p * rps + torch.randint(0, rps, (n,), generator=g))
+        so += nproj
+        ro += rps * nproj
+    mods.append((so, 1, ro, 20))
+    cols.append(ro + torch.randint(0, 20, (n,), generator=g))
+    R = ro + 20
+    rows = torch.stack(cols, 1).to(torch.int32) if n else torch.zeros((0, so + 1), dtype=torch.int32)
+    if n:
+        rows[:, 3][torch.rand(n, generator=g) < 0.25] = 0xFFFF
+        c = min(40, rows.shape[1] - 1)
+        rows[: n // 3, c] = rows[0, c]  # long runs of one bucket
+    dy = torch.randn((n, D), generator=g).to(torch.bfloat16)
+    return rows.to(torch.int16), dy, R, mods
+
+
+@pytest.mark.parametrize("n,D", [(1, 256), (31, 64), (1000, 16), (40000, 256), (70001, 128), (5000, 32)])
+def test_cve_table_bwd_mfma(dev, n, D):
+    rows, dy, R, mods = _cve_case(n, D, seed=n + D)
+    got = K.cve_table_bwd(rows.to(dev), dy.to(dev), R, mods)
+    torch.cuda.synchronize()
+    segs = [(s0, ns, r0, ns * rps) for s0, ns, r0, rps in mods]
+    ref, mag = table_ref(rows, dy, R, segs)
+    check(got, ref, mag)
+
+
+def test_cve_table_bwd_accumulates_and_rejects(dev):
+    rows, dy, R, mods = _cve_case(3000, 64, bins=(4,), nproj=8, seed=7)
+    base = torch.randn((R, 64))
+    got = K.cve_table_bwd(rows.to(dev), dy.to(dev), R, mods, out=base.clone().to(dev))
+    torch.cuda.synchronize()
+    segs = [(s0, ns, r0, ns * rps) for s0, ns, r0, rps in mods]
+    ref, mag = table_ref(rows, dy, R, segs)
+    check(got, ref + base.double(), mag + base.double().abs())
+    with pytest.raises(RuntimeError):
+        K.cve_table_bwd(rows.to(dev), dy.to(dev).float(), R, mods)  # bf16 dY only
+    with pytest.raises(RuntimeError):
+        K.cve_table_bwd(rows.to(dev), dy.to(dev), R, [(0, 8, 0, 5), (8, 1, 20, 20)])  # overlapping rows
+
+
 def test_kshift_sparse_rejects_short_buffers(dev):
     ids = torch.zeros((8, 4), dtype=torch.int64, device=dev)
     dy = torch.zeros((8, 4, 32), dtype=torch.bfloat16, device=dev)
