@@ -113,16 +113,19 @@ def user_context(sd, cfg, cat_ids):
     return ref.mlp_quickgelu(e, ws, bs)
 
 
-def contrastive_loss(next_emb, cur_emb, mask, offsets: np.ndarray, mbs: int, tau: float, ks: List[int]):
-    """wrapper.py:78-245 with beta = 0 (logQ term vanishes), offsets given per mini-batch."""
+def contrastive_loss(next_emb, cur_emb, mask, offsets: np.ndarray, mbs: int, tau: float, ks: List[int],
+                     normalize: bool = True):
+    """wrapper.py:78-245 with beta = 0 (logQ term vanishes), offsets given per mini-batch.
+    ``normalize=False`` takes already-normalised embeddings (kernel-level tests feed
+    the same bf16-rounded unit vectors the GPU path uses)."""
     B = next_emb.shape[0]
     n_mb = (B + mbs - 1) // mbs
     total = 0.0
     stats = []
     for mb in range(n_mb):
         sl = slice(mb * mbs, min((mb + 1) * mbs, B))
-        output_emb = F.normalize(next_emb[sl], p=2.0, dim=-1)
-        input_emb = F.normalize(cur_emb[sl], p=2.0, dim=-1)
+        output_emb = F.normalize(next_emb[sl], p=2.0, dim=-1) if normalize else next_emb[sl]
+        input_emb = F.normalize(cur_emb[sl], p=2.0, dim=-1) if normalize else cur_emb[sl]
         m = mask[sl]
         bsz = output_emb.size(0)
         De = output_emb.size(-1)
