@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
 //           blockIdx.y == 1: key tiles   -> dK and dV.
 // P = exp(S - lse) is recomputed from the forward's LSE; delta = rowsum(dO * O).
 template <int E>
-__global__ __launch_bounds__(256) void attn_bwd_mfma_k(AttnArgs a) {
+__global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NS = E / 32, NE = E / 16;
   const int T = a.T, Tk = (T + 31) & ~31, Tq = (T + 15) & ~15;
@@ -463,13 +463,26 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_k(AttnArgs a) {
   }
   const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
   for (int i = tid; i < Tk; i += 256) lse[i] = i < T ? lse_g[i] : 0.f;
-  // delta[q] = dO[q] . O[q]  (a wave per row, bf16 products in f32)
-  for (int q = wave; q < Tk; q += 4) {
-    float d = 0.f;
-    if (q < T)
-      for (int e = lane; e < E; e += 64) d += bf2f(dog[(int64_t)q * a.o_ts + e]) * bf2f(og[(int64_t)q * a.o_ts + e]);
-    d = wave_sum(d);
-    if (lane == 0) delta[q] = d;
+  // delta[q] = dO[q] . O[q]: one thread per (row, 16-byte chunk), all loads in
+  // flight at once, then a shuffle sum over the E/8 chunk lanes of each row
+  {
+    constexpr int CPR = E / 8;
+    for (int base = 0; base < Tk * CPR; base += 256) {
+      const int idx = base + tid;
+      const int q = idx / CPR, c = idx - q * CPR;
+      float d = 0.f;
+      if (q < T) {
+        const u32x4 u = *reinterpret_cast<const u32x4*>(dog + (int64_t)q * a.o_ts + c * 8);
+        const u32x4 v = *reinterpret_cast<const u32x4*>(og + (int64_t)q * a.o_ts + c * 8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          d += __uint_as_float(u[i] << 16) * __uint_as_float(v[i] << 16) +
+               __uint_as_float(u[i] & 0xffff0000u) * __uint_as_float(v[i] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) d += __shfl_xor(d, o, 64);
+      if (c == 0 && q < Tk) delta[q] = d;
+    }
   }
   __syncthreads();
   float* scr = scr_all + wave * 16 * SCR_LD;
