@@ -121,6 +121,9 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
   int* segs = reinterpret_cast<int*>(smem + (size_t)KB_NP * 8 + (size_t)KB_G_FLOATS * 4);  // NP2+1
   __shared__ int s_nseg;
   __shared__ int s_wsum[4];
+  __shared__ int s_nnew;                    // rows this block touched first (sparse mode)
+  __shared__ unsigned long long s_base;
+  __shared__ int64_t s_new[KB_NP];
 
   const int tid = threadIdx.x;
   for (int64_t base = (int64_t)blockIdx.x * CH; base < n_items; base += (int64_t)gridDim.x * CH) {
@@ -207,7 +210,10 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
     }
     __syncthreads();
     const int nseg = s_nseg;
-    if (tid == 0) segs[nseg] = np;
+    if (tid == 0) {
+      segs[nseg] = np;
+      s_nnew = 0;
+    }
     __syncthreads();
     // 5) one group of lanes per segment: ordered sum, then one f32 add per column
     const int LPR = (D >= 64) ? 64 : D;    // lanes per segment (1 float each per pass)
@@ -227,10 +233,17 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
         atomicAdd(dW + row * D + d, acc);
       }
       if (flags != nullptr && gl == 0) {
-        if (atomicExch(flags + row, 1) == 0) list[atomicAdd(count, 1ull)] = row;
+        if (atomicExch(flags + row, 1) == 0) s_new[atomicAdd(&s_nnew, 1)] = row;
       }
     }
     __syncthreads();
+    if (flags != nullptr) {
+      // one global reservation per block instead of one same-address atomic per row
+      if (tid == 0) s_base = s_nnew ? atomicAdd(count, (unsigned long long)s_nnew) : 0ull;
+      __syncthreads();
+      for (int i = tid; i < s_nnew; i += 256) list[s_base + i] = s_new[i];
+      __syncthreads();
+    }
   }
 }
 

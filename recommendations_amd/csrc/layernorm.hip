@@ -1,7 +1,8 @@
 // LayerNorm forward/backward (commons/transformers/layers.py:142-149, eps 1e-5).
 //
-// One wave per row, the row held in registers (D/64 values per lane, D <= 1024),
-// vectorised loads.  The forward writes y in bf16 (the GEMM operand) plus the
+// One wave per row, the row held in registers (D/64 values per lane, D <= 1024);
+// for D % 4 == 0 each lane owns 4 consecutive columns per 256-column chunk
+// (16-byte f32 / 8-byte bf16 accesses).  The forward writes y in bf16 (the GEMM operand) plus the
 // per-row mean / rstd; the backward fuses the residual-gradient sums of the
 // double-residual encoder (x + block(x), models/lthm/sequence/query_tower.py:
 // 132-137) and emits both the f32 residual gradient and its bf16 copy for the
@@ -121,6 +122,153 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const TDY* __restrict__ dy, cons
   for (int c = threadIdx.x; c < D; c += 256) db_part[(int64_t)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
+// ---- vectorised variants (D % 4 == 0): lane owns columns 4(lane + 64k) .. +3,
+// so every access is one 16-byte (f32) or 8-byte (bf16) transaction per lane.
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float (&v)[4]) { load_vec<T, 4 * (int)sizeof(T)>(p, v); }
+
+template <int NK, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_v4_k(const float* __restrict__ x, int64_t M, int D,
+                                                   const float* __restrict__ w, const float* __restrict__ b,
+                                                   TY* __restrict__ y, float* __restrict__ mean,
+                                                   float* __restrict__ rstd, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float wv[NK][4], bv[NK][4];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = (lane + 64 * k) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { wv[k][i] = 0.f; bv[k][i] = 0.f; }
+    if (c < D) {
+      ld4(w + c, wv[k]);
+      if (b) ld4(b + c, bv[k]);
+    }
+  }
+  for (int64_t r = wave; r < M; r += nw) {
+    const float* xr = x + r * D;
+    float v[NK][4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = (lane + 64 * k) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[k][i] = 0.f;
+      if (c < D) ld4(xr + c, v[k]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s += v[k][i];
+    }
+    s = wave_sum(s);
+    const float mu = s / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = (lane + 64 * k) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = (c < D) ? v[k][i] - mu : 0.f;
+        q += d * d;
+      }
+    }
+    q = wave_sum(q);
+    const float rs = 1.f / sqrtf(q / (float)D + eps);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < D) {
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
+        store_vec<TY, 4>(y + r * D + c, o);
+      }
+    }
+    if (lane == 0) {
+      mean[r] = mu;
+      rstd[r] = rs;
+    }
+  }
+}
+
+template <int NK, typename TDY>
+__global__ __launch_bounds__(256) void ln_bwd_v4_k(const TDY* __restrict__ dy, const float* __restrict__ x, int64_t M,
+                                                   int D, const float* __restrict__ w, const float* __restrict__ mean,
+                                                   const float* __restrict__ rstd, const float* __restrict__ res1,
+                                                   const float* __restrict__ res2, float* __restrict__ dx,
+                                                   bf16_t* __restrict__ dx_bf16, float* __restrict__ dw_part,
+                                                   float* __restrict__ db_part) {
+  const int lane = threadIdx.x & 63;
+  const int wv_ = threadIdx.x >> 6;
+  const int64_t wave = blockIdx.x * 4 + wv_;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float wgt[NK][4], dwa[NK][4], dba[NK][4];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = (lane + 64 * k) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { wgt[k][i] = 0.f; dwa[k][i] = 0.f; dba[k][i] = 0.f; }
+    if (c < D) ld4(w + c, wgt[k]);
+  }
+  for (int64_t r = wave; r < M; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float g[NK][4], xh[NK][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      float d[4] = {0.f, 0.f, 0.f, 0.f}, xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (c < D) {
+        ld4(dy + r * D + c, d);
+        ld4(x + r * D + c, xv);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xh[k][i] = (c < D) ? (xv[i] - mu) * rs : 0.f;
+        g[k][i] = d[i] * wgt[k][i];
+        dwa[k][i] += d[i] * xh[k][i];
+        dba[k][i] += d[i];
+        s1 += g[k][i];
+        s2 += g[k][i] * xh[k][i];
+      }
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < D) {
+        float o[4], r1[4] = {0.f, 0.f, 0.f, 0.f}, r2[4] = {0.f, 0.f, 0.f, 0.f};
+        if (res1) ld4(res1 + r * D + c, r1);
+        if (res2) ld4(res2 + r * D + c, r2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = rs * (g[k][i] - s1 - xh[k][i] * s2) + r1[i] + r2[i];
+        store_vec<float, 4>(dx + r * D + c, o);
+        if (dx_bf16) store_vec<bf16_t, 4>(dx_bf16 + r * D + c, o);
+      }
+    }
+  }
+  __shared__ float red[4][1024];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wv_][c + i] = dwa[k][i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) dw_part[(int64_t)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wv_][c + i] = dba[k][i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) db_part[(int64_t)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
 template <int NPL>
 static int ln_fwd_launch(const float* x, int64_t M, int D, const float* w, const float* b, void* y, int ydt, float* mean,
                          float* rstd, hipStream_t s) {
@@ -158,6 +306,24 @@ extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const fl
   LTHM_REQUIRE(M >= 0 && D > 0 && D <= 1024 && w != nullptr);
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (D % 4 == 0) {
+    const int grid = grid_for(M, 4, 256 * 8);
+#define LTHM_LN_FWD_V4(NK)                                                                                     \
+    if (D <= 256 * NK) {                                                                                       \
+      if (y_dtype == LTHM_BF16)                                                                                \
+        hipLaunchKernelGGL((ln_fwd_v4_k<NK, bf16_t>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (bf16_t*)y,   \
+                           mean, rstd, 1e-5f);                                                                 \
+      else                                                                                                     \
+        hipLaunchKernelGGL((ln_fwd_v4_k<NK, float>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (float*)y,     \
+                           mean, rstd, 1e-5f);                                                                 \
+      LTHM_CHECK_LAUNCH();                                                                                     \
+      return 0;                                                                                                \
+    }
+    LTHM_LN_FWD_V4(1)
+    LTHM_LN_FWD_V4(2)
+    LTHM_LN_FWD_V4(4)
+#undef LTHM_LN_FWD_V4
+  }
   const int npl = (D + 63) / 64;
   if (npl <= 1) return ln_fwd_launch<1>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
   if (npl <= 2) return ln_fwd_launch<2>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
@@ -175,8 +341,27 @@ extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float*
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = grid_for(M, 4, 256 * 4);
-  const int npl = (D + 63) / 64;
   bf16_t* xb = (bf16_t*)dx_bf16;
+  if (D % 4 == 0) {
+    float* dwp = partials;
+    float* dbp = partials + (int64_t)nblk * D;
+#define LTHM_LN_BWD_V4(NK)                                                                                     \
+    if (D <= 256 * NK) {                                                                                       \
+      if (dy_dtype == LTHM_BF16)                                                                               \
+        hipLaunchKernelGGL((ln_bwd_v4_k<NK, bf16_t>), dim3(nblk), dim3(256), 0, s, (const bf16_t*)dy, x, M, D, w, \
+                           mean, rstd, res1, res2, dx, xb, dwp, dbp);                                          \
+      else                                                                                                     \
+        hipLaunchKernelGGL((ln_bwd_v4_k<NK, float>), dim3(nblk), dim3(256), 0, s, (const float*)dy, x, M, D, w,  \
+                           mean, rstd, res1, res2, dx, xb, dwp, dbp);                                          \
+      LTHM_CHECK_LAUNCH();                                                                                     \
+      return 0;                                                                                                \
+    }
+    LTHM_LN_BWD_V4(1)
+    LTHM_LN_BWD_V4(2)
+    LTHM_LN_BWD_V4(4)
+#undef LTHM_LN_BWD_V4
+  }
+  const int npl = (D + 63) / 64;
   if (npl <= 1) return ln_bwd_launch<1>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
   if (npl <= 2) return ln_bwd_launch<2>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
   if (npl <= 4) return ln_bwd_launch<4>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
