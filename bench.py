@@ -27,6 +27,63 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 BF16_PEAK_TFLOPS = 2500.0
 
+# Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
+# named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_KERNELS = {
+    "cl_bwd_k": ["cl_bwd_k<true>", "cl_bwd_k<false>"],
+    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<true>", "cl_stats_k"],
+    "attn_bwd_k": ["attn_bwd_mfma_k<64>"],
+    "attn_fwd_k": ["attn_fwd_mfma_k<64>"],
+    "gemm_k<1,1>": ["gemm_k<true, true>"],
+    "gemm_k<1,0>": ["gemm_k<true, false>"],
+    "gemm_k<0,0>": ["gemm_k<false, false>", "splitk_reduce_k"],
+    "cve_tab_bwd_k": ["cve_tab_bwd_k<256>", "seg_tab_reduce_k"],
+    "lthm_product_tower_fwd": ["ptower_fwd_k<float, unsigned short, 4>"],
+}
+
+
+def pmc_traffic(key):
+    """HBM bytes per call of `key` from the committed PMC summary (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None if the kernel was not profiled."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            pmc = json.load(f)
+    except OSError:
+        return None
+    names = PMC_KERNELS.get(key, [key])
+    vals = [pmc[n]["hbm_bytes"] for n in names if n in pmc and "hbm_bytes" in pmc[n]]
+    return float(sum(vals)) if vals else None
+
+
+def embedding_gather_hbm(dev, P=4_000_000, D=128, K=16, n=524_288, iters=10):
+    """SURVEY §8(d) embedding roofline on a table past the 256 MiB Infinity Cache
+    (P x D bf16 = 1.02 GB): KShift gather + pool fwd, algorithmic bytes per lookup
+    8 + K*D*2 + D*2 (bf16 out) over the HIP-event time of the kernel."""
+    from recommendations_amd import kernels as K_
+    g = torch.Generator(device=dev).manual_seed(7)
+    W = torch.randn((P, D), device=dev, generator=g).to(torch.bfloat16)
+    # non-negative ids: negative int64 ids send every shifted row (c >= 1) to one hot
+    # row (the reference's arithmetic-shift quirk), which caches; these spread all K rows
+    ids = torch.randint(0, 2**62, (n,), device=dev, generator=g, dtype=torch.int64)
+    out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    per = 8 + K * D * 2 + D * 2
+    gbs = n * per / (ms / 1000.0) / 1e9
+    del W, out
+    return {"kernel": "kshift_fwd_k", "table": f"P={P} D={D} bf16 ({P * D * 2 / 1e9:.2f} GB)", "K": K,
+            "ids": "uniform in [0, 2^62)",
+            "lookups": n, "bytes_per_lookup": per, "avg_launch_ms": round(ms, 4), "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 CONFIGS = {
     # BASELINE.json configs[1]: LTHM on 1x MI355X, 32 cat x 1M vocab, seq 128, d 256, 4 layers, bf16, batch 4096
     "c2": dict(B=4096, T=128, d=256, L=4, H=4, n_cat=32, cat_vocab=1_000_000, item_vocab=1_000_000),
@@ -98,6 +155,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-hbm-gather", action="store_true", help="skip the 1 GB-table embedding roofline")
     args = ap.parse_args()
 
     from recommendations_amd import _lib
@@ -200,15 +258,22 @@ def main():
             ach, peak, unit, bound = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
         else:
             ach, peak, unit, bound = per_launch / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s", "mfma"
+        traffic = pmc_traffic(dom)
         res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                           "frac": round(ach / peak, 4), "traffic": None,
+                           "frac": round(ach / peak, 4),
+                           "traffic": round(traffic) if traffic is not None else None,
+                           "traffic_unit": "bytes/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                           "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic is not None else None,
                            "avg_launch_ms": round(s["ms"] / s["calls"], 4)}
         if "kshift_fwd_k" in summ:
             g = summ["kshift_fwd_k"]
-            res["embedding_gather"] = {"kernel": "kshift_fwd_k", "bound": "hbm",
-                                       "achieved": round(g["work"] / (g["ms"] / 1000) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                                       "unit": "GB/s",
-                                       "frac": round(g["work"] / (g["ms"] / 1000) / 1e9 / HBM_PEAK_GBS, 4)}
+            res["embedding_gather_c2"] = {"kernel": "kshift_fwd_k", "bound": "hbm",
+                                          "note": "C2 tables (64 MB item, 32 x 64 MB cat) are Infinity-Cache resident",
+                                          "achieved": round(g["work"] / (g["ms"] / 1000) / 1e9, 1),
+                                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                          "frac": round(g["work"] / (g["ms"] / 1000) / 1e9 / HBM_PEAK_GBS, 4)}
+        if rank == 0 and not args.no_hbm_gather:
+            res["embedding_gather"] = embedding_gather_hbm(dev)
         res["kernels"] = kern
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg, model, cfgd, args.cpu_batch)

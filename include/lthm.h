@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 3 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 4 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -391,9 +391,10 @@ int lthm_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, in
 int lthm_colsum(const void* in, int32_t dtype, int64_t rows, int64_t cols, int64_t ld, float* out,
                 int32_t accumulate, void* stream);
 int lthm_fill_f32(float* p, float value, int64_t n, void* stream);
-/* first column of mask [B, T] (uint8, 1 = pad) holding a non-pad entry (T if none) -> *out
- * (the history trim of query_tower.py:73-86) */
-int lthm_trim_first_valid(const uint8_t* mask, int64_t B, int32_t T, int32_t* out, void* stream);
+/* History-trim statistics of mask [B, T] (uint8, 1 = pad) for query_tower.py:73-86:
+ * work[0] = first column holding a non-pad entry (T if none), work[1] = number of
+ * all-pad columns; work is a device int32 buffer of T + 2 entries (work[2..] scratch). */
+int lthm_trim_stats(const uint8_t* mask, int64_t B, int32_t T, int32_t* work, void* stream);
 /* y = act(x) (dy == NULL) or y = dy * act'(x); act = LTHM_ACT_GELU / LTHM_ACT_QGELU */
 int lthm_activation(const void* x, const void* dy, void* y, int32_t dtype, int64_t n, int32_t act, void* stream);
 

@@ -69,7 +69,8 @@ def lthm_forward_loss(sd: Dict[str, torch.Tensor], cfg, batch: Dict[str, torch.T
     else:
         trim = int(torch.nonzero(((~mask_all_bs).cumsum(dim=0) > 0).squeeze(1)).squeeze(1)[0])
     inp, mask, labels, ts, target, ids = [t[:, trim:] for t in (inp, mask, labels, ts, target, ids)]
-    T = T_full - trim
+    T = inp.shape[1]  # seq_len = x.size(1) (query_tower.py:98); a negative trim keeps the last |trim| columns
+    trim = T_full - T
     # query_tower.py:89-111
     q = "query_tower."
     xq = F.linear(inp, _p(sd, q + "inp_proj.weight"), _p(sd, q + "inp_proj.bias"))

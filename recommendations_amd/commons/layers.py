@@ -113,11 +113,10 @@ class _SparseKShiftFn(torch.autograd.Function):
         mod = ctx.mod
         gy = gy.contiguous()
         if mod.replicated_dp:
-            # data parallel over replicated tables: every rank applies every rank's updates
-            from ..distributed import all_gather_rows
-            ids, gy = all_gather_rows(ids), all_gather_rows(gy)
-            if out is not None:
-                out, norms = all_gather_rows(out), all_gather_rows(norms)
+            # data parallel over replicated tables: every rank applies every rank's
+            # (1/world-scaled) updates, so the replicas stay identical
+            from ..distributed import gather_sparse_grads
+            ids, gy, out, norms = gather_sparse_grads(ids, gy, out, norms)
         mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
         K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
                             mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,

@@ -100,15 +100,26 @@ extern "C" int lthm_fill_f32(float* p, float v, int64_t n, void* stream) {
 // ---------------------------------------------------------------- trim + activations
 namespace lthm {
 // first column t (of T) where some row is not padded -> *out (atomicMin); *out pre-set to T by the host wrapper
-__global__ void first_unmasked_k(const uint8_t* __restrict__ mask, int64_t B, int T, int* __restrict__ out) {
+// colany[t] = 1 iff column t of mask [B, T] holds a non-pad entry
+__global__ void col_any_k(const uint8_t* __restrict__ mask, int64_t B, int T, int* __restrict__ colany) {
   const int64_t n = B * T;
-  int best = T;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int t = (int)(i % T);
-    if (mask[i] == 0 && t < best) best = t;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (mask[i] == 0) colany[i % T] = 1;
+}
+// out[0] = first column with a non-pad entry (T if none), out[1] = number of all-pad columns
+__global__ __launch_bounds__(256) void trim_stats_k(const int* __restrict__ colany, int T, int* __restrict__ out) {
+  __shared__ int s_first, s_cnt;
+  if (threadIdx.x == 0) { s_first = T; s_cnt = 0; }
+  __syncthreads();
+  int first = T, cnt = 0;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    if (colany[t]) first = min(first, t);
+    else cnt += 1;
   }
-  for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMin(out, best);
+  atomicMin(&s_first, first);
+  atomicAdd(&s_cnt, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) { out[0] = s_first; out[1] = s_cnt; }
 }
 __global__ void set_int_k(int* p, int v) { *p = v; }
 
@@ -137,11 +148,13 @@ __global__ __launch_bounds__(256) void act_k(const T* __restrict__ x, const T* _
 }
 }  // namespace lthm
 
-extern "C" int lthm_trim_first_valid(const uint8_t* mask, int64_t B, int32_t T, int32_t* out, void* stream) {
-  LTHM_REQUIRE(B >= 0 && T > 0);
+extern "C" int lthm_trim_stats(const uint8_t* mask, int64_t B, int32_t T, int32_t* work, void* stream) {
+  LTHM_REQUIRE(B >= 0 && T > 0 && work != nullptr);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(set_int_k, dim3(1), dim3(1), 0, s, (int*)out, (int)T);
-  if (B > 0) hipLaunchKernelGGL(first_unmasked_k, dim3(grid_for(B * T, 256, 1024)), dim3(256), 0, s, mask, B, T, (int*)out);
+  int* colany = (int*)work + 2;
+  LTHM_REQUIRE(hipMemsetAsync(colany, 0, (size_t)T * sizeof(int), s) == hipSuccess);
+  if (B > 0) hipLaunchKernelGGL(col_any_k, dim3(grid_for(B * T, 256, 1024)), dim3(256), 0, s, mask, B, T, colany);
+  hipLaunchKernelGGL(trim_stats_k, dim3(1), dim3(256), 0, s, (const int*)colany, (int)T, (int*)work);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

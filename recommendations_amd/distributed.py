@@ -83,6 +83,23 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def gather_sparse_grads(ids: torch.Tensor, gy: torch.Tensor, out: Optional[torch.Tensor] = None,
+                        norms: Optional[torch.Tensor] = None):
+    """Replicated-table DP backward input: every rank's (ids, pooled gradient) pairs
+    in rank order, the gradients scaled by 1/world so the applied row update is
+    the gradient of the rank-averaged loss (the same average GradBucketAllReduce
+    takes for the dense parameters).  ``out``/``norms`` (normalise mode) follow ids."""
+    ws = world_size()
+    if ws == 1:
+        return ids, gy, out, norms
+    ids_all = all_gather_rows(ids)
+    gy_all = all_gather_rows(gy)
+    gy_all.mul_(1.0 / ws)
+    if out is not None:
+        out, norms = all_gather_rows(out), all_gather_rows(norms)
+    return ids_all, gy_all, out, norms
+
+
 def step_flags(stop: bool, loss: torch.Tensor) -> torch.Tensor:
     """[stop, non-finite loss] MAX-reduced over ranks in one collective (no host sync here)."""
     f = torch.stack([torch.tensor(float(stop), device=loss.device), (~torch.isfinite(loss.detach())).float().reshape(())])

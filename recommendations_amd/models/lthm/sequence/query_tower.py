@@ -116,6 +116,14 @@ class OutcomeHeadsFn(torch.autograd.Function):
         return (dx.view(B, Tp, d), doc, None, None, None, *[dw[i * Pe:(i + 1) * Pe] for i in range(NH)])
 
 
+def effective_trim(T: int, export_span: int, first_valid: int, n_all_pad: int) -> int:
+    """Start column kept by query_tower.py:73-86 (``x[:, trim:]`` Python slicing)."""
+    trim = T - export_span if n_all_pad > T - export_span else first_valid
+    if trim < 0:
+        trim = max(0, T + trim)
+    return min(trim, T)
+
+
 class QueryTower(nn.Module):
     def __init__(self, model_config):
         super().__init__()
@@ -162,14 +170,15 @@ class QueryTower(nn.Module):
         return d
 
     def compute_trim(self, mask: torch.Tensor) -> int:
-        """query_tower.py:73-86: drop leading all-pad columns, keep >= export_span."""
+        """query_tower.py:73-86: if the all-pad columns outnumber T - export_span the
+        trim is T - export_span, else the first column with a real token.  The
+        reference slices ``x[:, trim:]`` and re-reads seq_len from the result, so a
+        negative trim (export_span > T) keeps the last |trim| columns."""
         B, T = mask.shape
-        first = torch.empty(1, dtype=torch.int32, device=mask.device)
-        call("lthm_trim_first_valid", ptr(mask), B, T, ptr(first), stream())
-        f = int(first.item())  # one 4-byte device->host read per step (the reference syncs here too)
-        if f > T - self.export_span:  # all-masked columns > T - export_span
-            return T - self.export_span
-        return f
+        work = torch.empty(T + 2, dtype=torch.int32, device=mask.device)
+        call("lthm_trim_stats", ptr(mask), B, T, ptr(work), stream())
+        first, n_all_pad = work[:2].tolist()  # one 8-byte device->host read per step (the reference syncs here too)
+        return effective_trim(T, self.export_span, first, n_all_pad)
 
     def forward(self, input, target, mask_inp, labels, timestamp, ids, ctx: Optional[torch.Tensor] = None,
                 future_outcome: int = 0):
