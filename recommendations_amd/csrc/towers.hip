@@ -153,6 +153,290 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
   }
 }
 
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// swizzled row-major [rows, D] bf16 LDS image (16-byte chunks XOR row group) and
+// its ds_read_tr16_b64 fragment B[k = 8(lane>>4) + i][n = nb + (lane&15)]
+template <int D>
+__device__ __forceinline__ int ct_off(int row, int ch) {
+  constexpr int NC = D / 8;
+  constexpr int RPL = (256 / (2 * D)) > 0 ? 256 / (2 * D) : 1;
+  return row * (2 * D) + ((ch ^ ((row / RPL) & (NC - 1))) << 4);
+}
+
+template <int D>
+__device__ __forceinline__ bf16x8v ct_tr_frag(const unsigned char* img, int nb, int lane) {
+  const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int kr = 8 * gq + q;
+  const int ch = (nb >> 3) + (p >> 1);
+  const unsigned char* a0 = img + ct_off<D>(kr, ch) + 8 * (p & 1);
+  const unsigned char* a1 = img + ct_off<D>(kr + 4, ch) + 8 * (p & 1);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// ------------------------------------------------------------------ product-tower bucket rows
+// Per token: norm, pad mask, x / |x| (bf16 copy for the mapper's weight
+// gradient), CVE input normalised once more (layers.py:464), histogram row.
+// Per (token, projection): z = xn2 . R[:, p] (f32, sequential FMAs), bucketize
+// (right = False) -> table row.  Phase 1 runs a thread per token; phase 2 a
+// thread per projection with its R column and grid in registers, streaming the
+// chunk's xn2 vectors from LDS as broadcast reads.
+constexpr int PR_TOK = 256;
+constexpr int PR_DMAX = 64;  // Din <= 64 (registers sized by the DM = 32 / 64 instance)
+constexpr int PR_NBMAX = 32;
+
+template <typename TX, int DM>
+__global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int total) {
+  constexpr int LD = DM + 4;
+  __shared__ __attribute__((aligned(16))) float xs2[PR_TOK * LD];
+  __shared__ uint8_t msk[PR_TOK];
+  const int tid = threadIdx.x;
+  const int Din = d.Din;
+  // this thread's projection (threads >= #projections only run phase 1)
+  int nb = 0, rbase = 0, mine = 0;
+  float Rc[DM], gr[PR_NBMAX];
+  {
+    int base = 0;
+    for (int m = 0; m < d.n_mod; ++m) {
+      const int npm = d.mod_nproj[m];
+      if (tid >= base && tid < base + npm) {
+        const int p = tid - base;
+        mine = 1;
+        nb = d.mod_nbins[m];
+        rbase = d.mod_row_off[m] + (nb + 1) * p;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) Rc[i] = (i < Din) ? d.proj[d.mod_proj_off[m] + i * npm + p] : 0.f;
+#pragma unroll
+        for (int q = 0; q < PR_NBMAX; ++q) gr[q] = (q < nb) ? d.grids[d.mod_grid_off[m] + q] : INFINITY;
+      }
+      base += npm;
+    }
+  }
+  const TX* x = reinterpret_cast<const TX*>(d.x);
+  for (int64_t t0 = (int64_t)blockIdx.x * PR_TOK; t0 < d.n; t0 += (int64_t)gridDim.x * PR_TOK) {
+    {
+      const int64_t t = t0 + tid;
+      if (t < d.n) {
+        float v[DM];
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+          v[i] = (i < Din) ? Elem<TX>::ld(x + t * Din + i) : 0.f;
+          ss += v[i] * v[i];
+        }
+        const float nrm = sqrtf(ss);
+        const bool masked = (nrm < d.norm_threshold) || (d.ids[t] == 0);
+        const float den = fmaxf(nrm, 1e-12f);
+        float ss2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+          v[i] = v[i] / den;
+          ss2 += v[i] * v[i];
+          if (i < Din && d.xn_out) reinterpret_cast<bf16_t*>(d.xn_out)[t * Din + i] = f2bf(v[i]);
+        }
+        const float den2 = fmaxf(sqrtf(ss2), 1e-12f);
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+          if (i < Din) xs2[tid * LD + i] = v[i] / den2;
+        msk[tid] = masked ? 1 : 0;
+        if (d.mask_out) d.mask_out[t] = masked ? 1 : 0;
+        if (d.norm_bins > 0) {
+          const float f = floorf(nrm * (float)d.norm_bins);  // HistogramEmbedding(0, 1, nbins), clamped
+          const int hbin = (int)fminf(fmaxf(f, 0.f), (float)(d.norm_bins - 1));
+          d.rows_out[t * total + (total - 1)] = masked ? (uint16_t)0xffff : (uint16_t)(d.cve_rows + hbin);
+        }
+      }
+    }
+    __syncthreads();
+    if (mine) {
+      const int cnt = (int)min((int64_t)PR_TOK, d.n - t0);
+      for (int tt = 0; tt < cnt; ++tt) {
+        const float* xr = xs2 + tt * LD;
+        float z = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; i += 4) {
+          if (i < Din) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(xr + i);
+            z = fmaf(q[0], Rc[i], z);
+            if (i + 1 < Din) z = fmaf(q[1], Rc[i + 1], z);
+            if (i + 2 < Din) z = fmaf(q[2], Rc[i + 2], z);
+            if (i + 3 < Din) z = fmaf(q[3], Rc[i + 3], z);
+          }
+        }
+        int bk = 0;
+#pragma unroll
+        for (int q = 0; q < PR_NBMAX; ++q) bk += (gr[q] < z) ? 1 : 0;  // bucketize(right=False)
+        d.rows_out[(t0 + tt) * total + tid] = msk[tt] ? (uint16_t)0xffff : (uint16_t)(rbase + bk);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ product-tower embedding on MFMA
+// emb[t, :] = b + W xn[t] + sum_s Tab[rows[t, s], :]   (rows from the FULL = false pass)
+// The bag sums are a one-hot GEMM  onehot[t, k] . Tab[k, :]  over all R table
+// rows k: A fragments are built from the LDS-staged bucket ids (k belongs to
+// slot sOf[k]; A = [rows[t, sOf[k]] == k], exactly 0/1 in bf16, Tab bf16, f32
+// accumulation), Tab streams through LDS in 32-row slabs read with
+// ds_read_tr16_b64.  The mapper Linear (Din <= 64) runs in f32 on the VALU in the
+// epilogue.  Block = 8 waves = 128 tokens x D columns (D = 16 NF <= 256).
+constexpr int PE_TOK = 128;
+constexpr int PE_MAXR = 4096;  // table rows
+
+template <typename TX, int NF>
+__global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int total, int R) {
+  constexpr int D = 16 * NF;
+  constexpr int SLAB = 32 * D * 2;  // one 32-row bf16 slab
+  constexpr int PD = (32 * D / 8 + 511) / 512;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* slab = smem;                                        // [2][SLAB]
+  float* wN = reinterpret_cast<float*>(smem + 2 * SLAB);            // [D][Din] (nn.Linear layout)
+  float* xs = wN + d.Din * D;                                       // [PE_TOK][Din]
+  uint16_t* rs = reinterpret_cast<uint16_t*>(xs + PE_TOK * d.Din);  // [PE_TOK][total]
+  uint16_t* sOf = rs + PE_TOK * total;                              // [R32]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int Din = d.Din;
+  const int R32 = (R + 31) & ~31;
+  const int64_t t0 = (int64_t)blockIdx.x * PE_TOK;
+  const bf16_t* tab = reinterpret_cast<const bf16_t*>(d.tables);
+  // ---- per-block staging: mapper weights, slot-of-row map, bucket rows, normalised x
+  for (int i = tid; i < Din * D; i += 512) wN[i] = d.w_map[i];
+  for (int k = tid; k < R32; k += 512) {
+    int sl = 0, so = 0;
+    if (k < d.cve_rows) {
+      for (int j = 0; j < d.n_mod; ++j) {
+        const int rps = d.mod_nbins[j] + 1, r0 = d.mod_row_off[j], np = d.mod_nproj[j];
+        if (k >= r0 && k < r0 + np * rps) sl = so + (k - r0) / rps;
+        so += np;
+      }
+    } else {
+      sl = total - 1;  // histogram slot
+    }
+    sOf[k] = (uint16_t)sl;
+  }
+  for (int i = tid; i < PE_TOK * total; i += 512) {
+    const int tt = i / total;
+    rs[i] = (t0 + tt < d.n) ? d.rows_out[t0 * total + i] : (uint16_t)0xffff;
+  }
+  {
+    // xn = x / max(|x|, 1e-12): 8 lanes per token
+    const TX* x = reinterpret_cast<const TX*>(d.x);
+    for (int tb = w * 8 + (lane >> 3); tb < PE_TOK; tb += 64) {
+      const int64_t t = t0 + tb;
+      float v[8];
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = (lane & 7) + 8 * i;
+        v[i] = (t < d.n && c < Din) ? Elem<TX>::ld(x + t * Din + c) : 0.f;
+        ss += v[i] * v[i];
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) ss += __shfl_xor(ss, o, 64);
+      const float den = fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = (lane & 7) + 8 * i;
+        if (c < Din) xs[tb * Din + c] = v[i] / den;
+      }
+    }
+  }
+  // ---- slab pipeline
+  u32x4 pf[PD];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) {
+      const int idx = tid + 512 * q;
+      const int r = idx / (D / 8), c = idx - r * (D / 8);
+      pf[q] = u32x4{0u, 0u, 0u, 0u};
+      if (idx < 32 * D / 8 && k0 + r < R) pf[q] = *reinterpret_cast<const u32x4*>(tab + (int64_t)(k0 + r) * D + c * 8);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) {
+      const int idx = tid + 512 * q;
+      const int r = idx / (D / 8), c = idx - r * (D / 8);
+      if (idx < 32 * D / 8) *reinterpret_cast<u32x4*>(slab + buf * SLAB + ct_off<D>(r, c)) = pf[q];
+    }
+  };
+  fetch(0);
+  store(0);
+  __syncthreads();
+  f32x4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tl = w * 16 + (lane & 15);  // this lane's A row (token)
+  // mapper xn . W^T on MFMA: f32 operands split into bf16 hi + lo, three products
+  // (hi.hi + hi.lo + lo.hi) keep ~16 mantissa bits
+  auto split8 = [](const float* p, int valid, bf16x8v& hi, bf16x8v& lo) {
+    s16x8 h, l;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < valid ? p[i] : 0.f;
+      const uint32_t u = __float_as_uint(v) & 0xffff0000u;
+      h[i] = (short)(u >> 16);
+      l[i] = (short)f2bf(v - __uint_as_float(u));
+    }
+    hi = __builtin_bit_cast(bf16x8v, h);
+    lo = __builtin_bit_cast(bf16x8v, l);
+  };
+  for (int k0 = 0; k0 < Din; k0 += 32) {
+    const int kb = k0 + 8 * (lane >> 4);
+    const int valid = max(0, min(8, Din - kb));
+    bf16x8v xh, xl;
+    split8(xs + tl * Din + kb, valid, xh, xl);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      bf16x8v wh, wl;
+      split8(wN + (f * 16 + (lane & 15)) * Din + kb, valid, wh, wl);
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, wh, acc[f], 0, 0, 0);
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, wl, acc[f], 0, 0, 0);
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, wh, acc[f], 0, 0, 0);
+    }
+  }
+  const uint16_t* myrows = rs + tl * total;
+  const int nslab = R32 / 32;
+  for (int sI = 0; sI < nslab; ++sI) {
+    const int cur = sI & 1, k0 = sI * 32;
+    const bool more = sI + 1 < nslab;
+    if (more) fetch(k0 + 32);
+    s16x8 a;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + 8 * (lane >> 4) + i;
+      a[i] = ((int)myrows[sOf[k]] == k) ? (short)0x3F80 : (short)0;
+    }
+    const bf16x8v af = __builtin_bit_cast(bf16x8v, a);
+    const unsigned char* img = slab + cur * SLAB;
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img, f * 16, lane), acc[f], 0, 0, 0);
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+  // ---- epilogue: + bias, mask fill, bf16 store
+  bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out);
+  float bias[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) bias[f] = d.b_map ? d.b_map[f * 16 + (lane & 15)] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int tb = w * 16 + 4 * (lane >> 4) + j;
+    const int64_t t = t0 + tb;
+    if (t >= d.n) continue;
+    const bool masked = d.mask_out[t] != 0;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) eo[t * D + f * 16 + (lane & 15)] = f2bf(masked ? 0.f : acc[f][j] + bias[f]);
+  }
+}
+
 // ------------------------------------------------------------------ small-table gradient
 // dW[rows[t, i]] += dY[t] for every token t and index slot i (0xffff = skip).
 // The slots are grouped into segments (e.g. a run of CosineVectorEmbedding
@@ -246,10 +530,6 @@ __global__ __launch_bounds__(256) void seg_tab_reduce_k(const float* __restrict_
 // transposed to [slot][token]).  Token chunks (blockIdx.z) write f32 partials
 // that seg_tab_reduce_k folds in a fixed order.  Replaces the LDS-atomic scatter
 // for this layout: LDS float atomics sustain ~1 slot-update per ~190 CU cycles.
-typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-
 constexpr int CT_MAXTILE = 64;
 constexpr int CT_ROWS = 128;   // rows per tile (8 waves x 16)
 constexpr int CT_KT = 32;      // tokens per k-step
@@ -259,26 +539,6 @@ struct CveTiles {
   int row0[CT_MAXTILE], nrow[CT_MAXTILE], sfirst[CT_MAXTILE], nsl[CT_MAXTILE];
   int mrow0[CT_MAXTILE], mslot0[CT_MAXTILE], rps[CT_MAXTILE];
 };
-
-template <int D>
-__device__ __forceinline__ int ct_off(int row, int ch) {
-  constexpr int NC = D / 8;
-  constexpr int RPL = (256 / (2 * D)) > 0 ? 256 / (2 * D) : 1;
-  return row * (2 * D) + ((ch ^ ((row / RPL) & (NC - 1))) << 4);
-}
-
-template <int D>
-__device__ __forceinline__ bf16x8v ct_tr_frag(const unsigned char* img, int nb, int lane) {
-  const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int kr = 8 * gq + q;
-  const int ch = (nb >> 3) + (p >> 1);
-  const unsigned char* a0 = img + ct_off<D>(kr, ch) + 8 * (p & 1);
-  const unsigned char* a1 = img + ct_off<D>(kr + 4, ch) + 8 * (p & 1);
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8v, v);
-}
 
 template <int D>
 __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx,
@@ -493,6 +753,45 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int opl = d->Dout <= 64 ? 1 : d->Dout <= 128 ? 2 : d->Dout <= 256 ? 4 : 8;
   LTHM_REQUIRE(d->Dout % opl == 0);
+  // MFMA path: per-token pass (rows, mask) + one-hot GEMM for the bag sums
+  const int R = d->cve_rows + (d->norm_bins > 0 ? d->norm_bins : 0);
+  const int R32 = (R + 31) & ~31;
+  const int Dm = d->Dout;
+  const size_t sh_mfma = (size_t)2 * 32 * Dm * 2 + (size_t)d->Din * Dm * 4 + (size_t)PE_TOK * d->Din * 4 +
+                         (size_t)PE_TOK * total * 2 + (size_t)R32 * 2;
+  int maxnb = 0, nproj = 0;
+  for (int j = 0; j < d->n_mod; ++j) {
+    maxnb = std::max(maxnb, d->mod_nbins[j]);
+    nproj += d->mod_nproj[j];
+  }
+  const bool mfma = !d->cve_only && d->tab_dtype == LTHM_BF16 && d->emb_dtype == LTHM_BF16 && d->rows_out &&
+                    d->mask_out && d->ids && (Dm == 16 || Dm == 32 || Dm == 64 || Dm == 128 || Dm == 256) && R > 0 &&
+                    R <= PE_MAXR && sh_mfma <= 160 * 1024 && d->Din <= PR_DMAX && d->Din % 4 == 0 &&
+                    maxnb <= PR_NBMAX && nproj <= 256;
+  if (mfma) {
+    const dim3 g1((unsigned)std::min<int64_t>((d->n + PR_TOK - 1) / PR_TOK, 4096));
+    if (d->Din <= 32) {
+      if (d->x_dtype == LTHM_BF16) hipLaunchKernelGGL((ptower_rows_k<bf16_t, 32>), g1, dim3(256), 0, s, *d, total);
+      else hipLaunchKernelGGL((ptower_rows_k<float, 32>), g1, dim3(256), 0, s, *d, total);
+    } else {
+      if (d->x_dtype == LTHM_BF16) hipLaunchKernelGGL((ptower_rows_k<bf16_t, 64>), g1, dim3(256), 0, s, *d, total);
+      else hipLaunchKernelGGL((ptower_rows_k<float, 64>), g1, dim3(256), 0, s, *d, total);
+    }
+    LTHM_CHECK_LAUNCH();
+    const dim3 g2((unsigned)((d->n + PE_TOK - 1) / PE_TOK));
+#define LTHM_PT_EMB(TX)                                                                                     \
+  switch (Dm) {                                                                                             \
+    case 16: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 1>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
+    case 32: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 2>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
+    case 64: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 4>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
+    case 128: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 8>), g2, dim3(512), sh_mfma, s, *d, total, R); break; \
+    default: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 16>), g2, dim3(512), sh_mfma, s, *d, total, R); break; \
+  }
+    if (d->x_dtype == LTHM_BF16) { LTHM_PT_EMB(bf16_t) } else { LTHM_PT_EMB(float) }
+#undef LTHM_PT_EMB
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
 #define LTHM_PT(TX, TT)                                                                                   \
   if (opl == 1) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 1>), dim3(grid), dim3(256), sh, s, *d, total);    \
   else if (opl == 2) hipLaunchKernelGGL((ptower_fwd_k<TX, TT, 2>), dim3(grid), dim3(256), sh, s, *d, total); \
