@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 4 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 5 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -259,13 +259,22 @@ int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nseg, c
  * MFMA: module j covers slots [mod_slot0[j], +mod_nslot[j]) and slot s owns rows
  * [mod_row0[j] + (s - mod_slot0[j]) * mod_rps[j], +mod_rps[j]) (module row ranges
  * disjoint, nmod <= 16, <= 64 tiles of 128 rows).  dY bf16 [n, D] with D in
- * {16, 32, 64, 128, 256}; dW f32 accumulated; workspace as lthm_small_table_bwd.
+ * {16, 32, 64, 128, 256} (f32 dY is split into bf16 hi + lo); dW f32 accumulated;
+ * workspace as lthm_small_table_bwd.
  * (commons/transformers/layers.py:462-471 backward; product_tower.py:43-62).
  * The mod_* arrays are HOST arrays. */
 int lthm_cve_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nmod, const int32_t* mod_slot0,
                        const int32_t* mod_nslot, const int32_t* mod_row0, const int32_t* mod_rps,
-                       const void* dY, int64_t ldy, int64_t n, int32_t D, float* dW, void* workspace,
-                       int64_t workspace_bytes, void* stream);
+                       const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+/* Same one-hot MFMA gradient for a small table of R rows whose nidx <= 8 slots
+ * may each reference any row (0xffff = skip): dW[rows[t, i]] += dY[t, :]
+ * (nn.Embedding / EmbeddingBag-sum backward: the query tower's action, time,
+ * position and pad tables, outcome conditioning).  dY f32 (hi + lo bf16 split)
+ * or bf16 [n, D], D in {16, 32, 64, 128, 256}; R <= 8192. */
+int lthm_table_bwd_mfma(const uint16_t* rows, int32_t nidx, int32_t R, const void* dY, int32_t dy_dtype,
+                        int64_t ldy, int64_t n, int32_t D, float* dW, void* workspace, int64_t workspace_bytes,
+                        void* stream);
 /* QuantileMapper (commons/transformers/layers.py:477-487) on x [B, F]:
  * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
 int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,

@@ -540,16 +540,22 @@ struct CveTiles {
   int mrow0[CT_MAXTILE], mslot0[CT_MAXTILE], rps[CT_MAXTILE];
 };
 
-template <int D>
+// F32: dY is f32, staged as bf16 hi and lo images (two MFMAs per fragment, ~16
+// mantissa bits).  GEN: slots are not tied to row ranges (e.g. a slot that
+// holds either an action row or the pad row); A[m, t] counts the slots of the
+// token whose row is m (<= CT_GENMAX slots, exact small integers in bf16).
+constexpr int CT_GENMAX = 8;
+template <int D, bool F32, bool GEN>
 __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict__ rows, int nidx,
-                                                    const bf16_t* __restrict__ dY, int64_t ldy, int64_t n,
+                                                    const void* __restrict__ dYv, int64_t ldy, int64_t n,
                                                     float* __restrict__ dst, int64_t zstride, int direct,
                                                     int64_t tok_per_block, CveTiles ct) {
   constexpr int NF = D / 16;
-  constexpr int NCH = D / 8;                    // 16-byte chunks per dY row
-  constexpr int IMG = CT_KT * D * 2;            // dY image bytes
+  constexpr int EPC = F32 ? 4 : 8;              // dY elements per 16-byte chunk
+  constexpr int NCH = D / EPC;                  // 16-byte chunks per dY row
+  constexpr int IMG = CT_KT * D * 2;            // one bf16 dY image
   constexpr int RTB = CT_MAXSL * CT_KT * 2;     // bucket-id tile bytes
-  constexpr int BUF = IMG + RTB;
+  constexpr int BUF = (F32 ? 2 : 1) * IMG + RTB;
   constexpr int PD = (CT_KT * NCH + 511) / 512;
   constexpr int PR = (CT_KT * CT_MAXSL + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -561,7 +567,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
   const int ml = wave * 16 + (lane & 15);
   const bool mvalid = ml < nrow;
   const int m = row0 + ml;
-  const int ls = mvalid ? ct.mslot0[tile] + (m - ct.mrow0[tile]) / ct.rps[tile] - sfirst : 0;
+  const int ls = (!GEN && mvalid) ? ct.mslot0[tile] + (m - ct.mrow0[tile]) / ct.rps[tile] - sfirst : 0;
   f32x4 acc[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -573,7 +579,10 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
       const int idx = tid + 512 * k;
       const int r = idx / NCH, c = idx - r * NCH;
       pd[k] = u32x4{0u, 0u, 0u, 0u};
-      if (idx < CT_KT * NCH && tb + r < t1) pd[k] = *reinterpret_cast<const u32x4*>(dY + (tb + r) * ldy + c * 8);
+      if (idx < CT_KT * NCH && tb + r < t1) {
+        if constexpr (F32) pd[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(dYv) + (tb + r) * ldy + c * 4);
+        else pd[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(dYv) + (tb + r) * ldy + c * 8);
+      }
     }
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
@@ -585,12 +594,28 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
   };
   auto store = [&](int buf) {
     unsigned char* img = smem + buf * BUF;
-    uint16_t* rt = reinterpret_cast<uint16_t*>(img + IMG);
+    uint16_t* rt = reinterpret_cast<uint16_t*>(img + (F32 ? 2 : 1) * IMG);
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
       const int idx = tid + 512 * k;
       const int r = idx / NCH, c = idx - r * NCH;
-      if (idx < CT_KT * NCH) *reinterpret_cast<u32x4*>(img + ct_off<D>(r, c)) = pd[k];
+      if (idx < CT_KT * NCH) {
+        if constexpr (F32) {
+          u32x2 hi, lo;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // hi = RNE bf16, lo = RNE bf16 of the remainder (<= 2^-18 rel.)
+            const float v0 = __uint_as_float(pd[k][2 * h]), v1 = __uint_as_float(pd[k][2 * h + 1]);
+            const bf16_t h0 = f2bf(v0), h1 = f2bf(v1);
+            hi[h] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            lo[h] = (uint32_t)f2bf(v0 - bf2f(h0)) | ((uint32_t)f2bf(v1 - bf2f(h1)) << 16);
+          }
+          const int off = ct_off<D>(r, c >> 1) + 8 * (c & 1);
+          *reinterpret_cast<u32x2*>(img + off) = hi;
+          *reinterpret_cast<u32x2*>(img + IMG + off) = lo;
+        } else {
+          *reinterpret_cast<u32x4*>(img + ct_off<D>(r, c)) = pd[k];
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
@@ -609,18 +634,38 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
     const int cur = (int)(st & 1);
     if (st + 1 < nsteps) fetch(t0 + (st + 1) * CT_KT);  // global loads in flight during the MFMAs
     const unsigned char* img = smem + cur * BUF;
-    const uint16_t* rt = reinterpret_cast<const uint16_t*>(img + IMG);
-    const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls * CT_KT + 8 * (lane >> 4));
+    const uint16_t* rt = reinterpret_cast<const uint16_t*>(img + (F32 ? 2 : 1) * IMG);
     s16x8 a;
+    if constexpr (GEN) {
+      int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
-      a[i] = (mvalid && (int)rr == m) ? (short)0x3F80 : (short)0;
+      for (int sl = 0; sl < CT_GENMAX; ++sl) {
+        if (sl < nsl) {
+          const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + sl * CT_KT + 8 * (lane >> 4));
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
+            cnt[i] += ((int)rr == m) ? 1 : 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = mvalid ? (short)f2bf((float)cnt[i]) : (short)0;
+    } else {
+      const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls * CT_KT + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
+        a[i] = (mvalid && (int)rr == m) ? (short)0x3F80 : (short)0;
+      }
     }
     const bf16x8v af = __builtin_bit_cast(bf16x8v, a);
 #pragma unroll
-    for (int f = 0; f < NF; ++f)
+    for (int f = 0; f < NF; ++f) {
       acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img, f * 16, lane), acc[f], 0, 0, 0);
+      if constexpr (F32)
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img + IMG, f * 16, lane), acc[f], 0, 0, 0);
+    }
     if (st + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
   }
@@ -860,11 +905,54 @@ extern "C" int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int3
   return 0;
 }
 
+static int launch_table_mfma(const uint16_t* rows, int32_t nidx, CveTiles& ct, SegTab& st, int rtot, bool gen,
+                             const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
+                             void* workspace, int64_t workspace_bytes, hipStream_t s) {
+  const int nt = ct.ntile;
+  const int64_t zbytes = (int64_t)rtot * D * 4;
+  int64_t gz = (512 + nt - 1) / nt;  // ~2 blocks of 512 threads per CU
+  gz = std::min<int64_t>(gz, (n + 1023) / 1024);
+  gz = std::min<int64_t>(gz, workspace ? workspace_bytes / zbytes : (int64_t)1);
+  if (gz < 2) gz = 1;
+  int64_t tpb = (n + gz - 1) / gz;
+  tpb = (tpb + CT_KT - 1) / CT_KT * CT_KT;
+  gz = (n + tpb - 1) / tpb;
+  const int direct = gz == 1;
+  float* dst = direct ? dW : (float*)workspace;
+  const bool f32 = dy_dtype == LTHM_F32;
+  const size_t sh = 2 * ((f32 ? 2 : 1) * (size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_KT * 2);
+  dim3 grid(nt, 1, (unsigned)gz);
+  const int64_t zs = zbytes / 4;
+#define LTHM_TAB_CASE(DD)                                                                                            \
+  case DD:                                                                                                           \
+    if (f32 && gen) hipLaunchKernelGGL((cve_tab_bwd_k<DD, true, true>), grid, dim3(512), sh, s, rows, nidx, dY, ldy, n, dst, zs, direct, tpb, ct); \
+    else if (f32) hipLaunchKernelGGL((cve_tab_bwd_k<DD, true, false>), grid, dim3(512), sh, s, rows, nidx, dY, ldy, n, dst, zs, direct, tpb, ct); \
+    else if (gen) hipLaunchKernelGGL((cve_tab_bwd_k<DD, false, true>), grid, dim3(512), sh, s, rows, nidx, dY, ldy, n, dst, zs, direct, tpb, ct); \
+    else hipLaunchKernelGGL((cve_tab_bwd_k<DD, false, false>), grid, dim3(512), sh, s, rows, nidx, dY, ldy, n, dst, zs, direct, tpb, ct); \
+    break;
+  switch (D) {
+    LTHM_TAB_CASE(16)
+    LTHM_TAB_CASE(32)
+    LTHM_TAB_CASE(64)
+    LTHM_TAB_CASE(128)
+    LTHM_TAB_CASE(256)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef LTHM_TAB_CASE
+  LTHM_CHECK_LAUNCH();
+  if (!direct) {
+    const int bx = (int)std::min<int64_t>(((int64_t)CT_ROWS * D + 255) / 256, 256);
+    hipLaunchKernelGGL(seg_tab_reduce_k, dim3(bx, nt), dim3(256), 0, s, (const float*)workspace, zs, (int)gz, D, dW, st);
+    LTHM_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 extern "C" int lthm_cve_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nmod, const int32_t* mod_slot0,
                                   const int32_t* mod_nslot, const int32_t* mod_row0, const int32_t* mod_rps,
-                                  const void* dY, int64_t ldy, int64_t n, int32_t D, float* dW, void* workspace,
-                                  int64_t workspace_bytes, void* stream) {
-  LTHM_REQUIRE(n >= 0 && nidx > 0 && nmod > 0 && nmod <= 16);
+                                  const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
+                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  LTHM_REQUIRE(n >= 0 && nidx > 0 && nmod > 0 && nmod <= 16 && (dy_dtype == LTHM_F32 || dy_dtype == LTHM_BF16));
   LTHM_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128 || D == 256);
   if (n == 0) return 0;
   CveTiles ct;
@@ -897,35 +985,40 @@ extern "C" int lthm_cve_table_bwd(const uint16_t* rows, int32_t nidx, int32_t nm
   }
   ct.ntile = nt;
   st.nseg = nt;
-  const int64_t zbytes = (int64_t)rtot * D * 4;
-  int64_t gz = (512 + nt - 1) / nt;  // ~2 blocks of 512 threads per CU
-  gz = std::min<int64_t>(gz, (n + 1023) / 1024);
-  gz = std::min<int64_t>(gz, workspace ? workspace_bytes / zbytes : (int64_t)1);
-  if (gz < 2) gz = 1;
-  int64_t tpb = (n + gz - 1) / gz;
-  tpb = (tpb + CT_KT - 1) / CT_KT * CT_KT;
-  gz = (n + tpb - 1) / tpb;
-  const int direct = gz == 1;
-  float* dst = direct ? dW : (float*)workspace;
-  hipStream_t s = (hipStream_t)stream;
-  const size_t sh = 2 * ((size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_KT * 2);
-  dim3 grid(nt, 1, (unsigned)gz);
-  const bf16_t* y = (const bf16_t*)dY;
-  switch (D) {
-    case 16: hipLaunchKernelGGL((cve_tab_bwd_k<16>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
-    case 32: hipLaunchKernelGGL((cve_tab_bwd_k<32>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
-    case 64: hipLaunchKernelGGL((cve_tab_bwd_k<64>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
-    case 128: hipLaunchKernelGGL((cve_tab_bwd_k<128>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
-    default: hipLaunchKernelGGL((cve_tab_bwd_k<256>), grid, dim3(512), sh, s, rows, nidx, y, ldy, n, dst, zbytes / 4, direct, tpb, ct); break;
+  return launch_table_mfma(rows, nidx, ct, st, rtot, false, dY, dy_dtype, ldy, n, D, dW, workspace, workspace_bytes,
+                           (hipStream_t)stream);
+}
+
+extern "C" int lthm_table_bwd_mfma(const uint16_t* rows, int32_t nidx, int32_t R, const void* dY, int32_t dy_dtype,
+                                   int64_t ldy, int64_t n, int32_t D, float* dW, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
+  LTHM_REQUIRE(n >= 0 && nidx > 0 && nidx <= CT_GENMAX && R > 0 && R < 0xffff &&
+               (dy_dtype == LTHM_F32 || dy_dtype == LTHM_BF16));
+  LTHM_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128 || D == 256);
+  LTHM_REQUIRE((R + CT_ROWS - 1) / CT_ROWS <= CT_MAXTILE);
+  if (n == 0) return 0;
+  CveTiles ct;
+  SegTab st;
+  int nt = 0;
+  for (int r = 0; r < R; r += CT_ROWS) {
+    const int nr = std::min(CT_ROWS, R - r);
+    ct.row0[nt] = r;
+    ct.nrow[nt] = nr;
+    ct.sfirst[nt] = 0;
+    ct.nsl[nt] = nidx;
+    ct.mrow0[nt] = 0;
+    ct.mslot0[nt] = 0;
+    ct.rps[nt] = 1;
+    st.row0[nt] = r;
+    st.nrow[nt] = nr;
+    st.slot0[nt] = 0;
+    st.nslot[nt] = 1;
+    ++nt;
   }
-  LTHM_CHECK_LAUNCH();
-  if (!direct) {
-    const int bx = (int)std::min<int64_t>(((int64_t)CT_ROWS * D + 255) / 256, 256);
-    hipLaunchKernelGGL(seg_tab_reduce_k, dim3(bx, nt), dim3(256), 0, s, (const float*)workspace, zbytes / 4, (int)gz, D,
-                       dW, st);
-    LTHM_CHECK_LAUNCH();
-  }
-  return 0;
+  ct.ntile = nt;
+  st.nseg = nt;
+  return launch_table_mfma(rows, nidx, ct, st, R, true, dY, dy_dtype, ldy, n, D, dW, workspace, workspace_bytes,
+                           (hipStream_t)stream);
 }
 
 extern "C" int lthm_small_table_bwd(const uint16_t* rows, int32_t nidx, const void* dY, int32_t dy_dtype, int64_t ldy,

@@ -412,11 +412,18 @@ def small_table_bwd(rows, dY, R, out=None):
     D = dY.shape[-1]
     _check(rows.dtype == torch.int16 and dY.numel() == n * D, "rows must be int16 [n, nidx] and dY [n, D]")
     _check(0 < nidx <= 64 and 0 < R < 0xFFFF, f"small_table_bwd takes nidx <= 64 slots and R < 65535 rows")
-    _check(R * 64 * 4 <= 160 * 1024, f"R={R} rows exceed the LDS slice; use segmented_table_bwd")
+    mfma = D in (16, 32, 64, 128, 256) and nidx <= 8 and R <= 8192
+    _check(mfma or R * 64 * 4 <= 160 * 1024, f"R={R} rows exceed the LDS slice; use segmented_table_bwd")
     if out is None:
         out = torch.zeros((R, D), dtype=torch.float32, device=dY.device)
     _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
     ws, wsb = _table_ws(dY.device, n, R, D)
+    if mfma:
+        # one-hot MFMA reduction (f32 dY split into bf16 hi + lo): no LDS atomics
+        call("lthm_table_bwd_mfma", ptr(rows), nidx, R, ptr(dY), dcode(dY), D, n, D, ptr(out),
+             ptr(ws) if ws is not None else None, wsb, stream(), _key="table_bwd_mfma_k",
+             _work=2.0 * n * D * R * (2 if dY.dtype == torch.float32 else 1), _unit="flop")
+        return out
     call("lthm_small_table_bwd", ptr(rows), nidx, ptr(dY), dcode(dY), D, n, R, D, ptr(out),
          ptr(ws) if ws is not None else None, wsb, stream(), _key="small_tab_bwd_k",
          _work=float(n) * D * dY.element_size(), _unit="byte")
@@ -550,13 +557,13 @@ def quantile_map(x, quantiles, shared):
 
 def cve_table_bwd(rows, dY, R, modules, out=None):
     """MFMA one-hot gradient of CVE-structured tables (include/lthm.h lthm_cve_table_bwd).
-    modules: [(slot0, nslot, row0, rows_per_slot)]; dY bf16 [n, D], D in {16..256} pow2."""
+    modules: [(slot0, nslot, row0, rows_per_slot)]; dY bf16 or f32 [n, D], D in {16..256} pow2."""
     import numpy as _np
     require_gpu(rows, dY, out)
     n, nidx = rows.shape
     D = dY.shape[-1]
-    _check(rows.dtype == torch.int16 and dY.dtype == torch.bfloat16 and dY.numel() == n * D,
-           "rows must be int16 [n, nidx] and dY bf16 [n, D]")
+    _check(rows.dtype == torch.int16 and dY.dtype in (torch.bfloat16, torch.float32) and dY.numel() == n * D,
+           "rows must be int16 [n, nidx] and dY bf16 / f32 [n, D]")
     _check(D in (16, 32, 64, 128, 256), f"cve_table_bwd takes D in 16..256 (power of two), got {D}")
     _check(0 < len(modules) <= 16, "1..16 modules")
     for s0, ns, r0, rps in modules:
@@ -568,7 +575,7 @@ def cve_table_bwd(rows, dY, R, modules, out=None):
     ws, wsb = _table_ws(dY.device, n, R, D)
     m = _np.ascontiguousarray(_np.array(modules, dtype=_np.int32).T)
     call("lthm_cve_table_bwd", ptr(rows), nidx, m.shape[1], m[0].ctypes.data, m[1].ctypes.data, m[2].ctypes.data,
-         m[3].ctypes.data, ptr(dY), D, n, D, ptr(out), ptr(ws) if ws is not None else None, wsb, stream(),
+         m[3].ctypes.data, ptr(dY), dcode(dY), D, n, D, ptr(out), ptr(ws) if ws is not None else None, wsb, stream(),
          _key="cve_tab_bwd_k", _work=2.0 * n * D * sum(ns * rps for _, ns, _, rps in modules), _unit="flop")
     return out
 
