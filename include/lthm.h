@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 5 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 6 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -406,6 +406,30 @@ int lthm_fill_f32(float* p, float value, int64_t n, void* stream);
 int lthm_trim_stats(const uint8_t* mask, int64_t B, int32_t T, int32_t* work, void* stream);
 /* y = act(x) (dy == NULL) or y = dy * act'(x); act = LTHM_ACT_GELU / LTHM_ACT_QGELU */
 int lthm_activation(const void* x, const void* dy, void* y, int32_t dtype, int64_t n, int32_t act, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Id ingest — commons/feature_utils.py (host CPU unless noted)              */
+/* ------------------------------------------------------------------------- */
+/* xxHash32 / xxHash64 of a byte string (python-xxhash intdigest()) */
+uint32_t lthm_xxh32(const void* data, int64_t len, uint32_t seed);
+uint64_t lthm_xxh64(const void* data, int64_t len, uint64_t seed);
+/* hash_string_to_long (feature_utils.py:40-46) over n packed UTF-8 strings
+ * bytes[offsets[i] .. offsets[i+1]): out[i] = xxh64(s_i, seed) - 2^63.  With
+ * to_lower, ASCII letters are lowered here; strings holding non-ASCII bytes are
+ * flagged in needs_unicode_lower[i] (may be NULL) and left for the caller
+ * (Python str.lower()).  Returns the number flagged, or -1 on bad arguments. */
+int64_t lthm_hash_strings(const uint8_t* bytes, const int64_t* offsets, int64_t n, uint64_t seed, int32_t to_lower,
+                          int64_t* out, uint8_t* needs_unicode_lower);
+/* hash_string_to_long(str(v), seed) for int64 values v (decimal str(), no lowering) */
+int lthm_hash_int64_str(const int64_t* vals, int64_t n, uint64_t seed, int64_t* out);
+/* the same on the GPU: device pointers, stream-ordered */
+int lthm_hash_int64_str_dev(const int64_t* vals, int64_t n, uint64_t seed, int64_t* out, void* stream);
+/* handle_categorical_history_feature / pad_array (feature_utils.py:21-25, 149-183):
+ * row r = items[row_offsets[r] .. row_offsets[r+1]) (already hashed), optionally
+ * dropping entries equal to history_id[r], capped to `length`, right-padded with
+ * `pad` -> out [n_rows, length]. */
+int lthm_history_pad(const int64_t* items, const int64_t* row_offsets, int64_t n_rows, const int64_t* history_id,
+                     int32_t remove_history_id, int32_t length, int64_t pad, int64_t* out);
 
 #ifdef __cplusplus
 }

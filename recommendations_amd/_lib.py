@@ -52,7 +52,8 @@ def parse_header(path: str = HEADER) -> Dict[str, Tuple[str, List[str]]]:
     text = re.sub(r"//[^\n]*", " ", text)
     text = re.sub(r"#[^\n]*", " ", text)
     protos = {}
-    for m in re.finditer(r"\b(int|void|int64_t|double|float)\s+(lthm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+    for m in re.finditer(r"\b(int|void|int64_t|uint32_t|uint64_t|double|float)\s+(lthm_\w+)\s*\(([^)]*)\)\s*;",
+                         text, flags=re.S):
         ret, name, args = m.group(1), m.group(2), m.group(3).strip()
         types = []
         if args and args != "void":
@@ -115,8 +116,8 @@ def load() -> ctypes.CDLL:
     protos = parse_header()
     for name, (ret, args) in protos.items():
         fn = getattr(lib, name)
-        fn.restype = {"int": ctypes.c_int, "void": None, "int64_t": ctypes.c_int64,
-                      "double": ctypes.c_double, "float": ctypes.c_float}[ret]
+        fn.restype = {"int": ctypes.c_int, "void": None, "int64_t": ctypes.c_int64, "uint32_t": ctypes.c_uint32,
+                      "uint64_t": ctypes.c_uint64, "double": ctypes.c_double, "float": ctypes.c_float}[ret]
         fn.argtypes = [_CTYPE[a] for a in args]
     _LIB, _PROTOS = lib, protos
     return lib
