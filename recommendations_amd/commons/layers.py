@@ -16,14 +16,55 @@ import torch.nn as nn
 from .. import kernels as K
 
 
-class KShiftEmbedding(nn.Module):
+class _SparseRowsMixin:
+    """Persistent f32 gradient + touched-row list of a KShift table trained with
+    a row-wise optimizer (optim.SparseRowAdamW / SparseRowAdagrad): no [P, D]
+    gradient is materialised or zeroed per step.  Needs ``weight``, ``_F``,
+    ``_num_embeddings``, ``_num_shifts``, ``_mode``, ``_out_dtype``,
+    ``_gather_dtype`` on the module."""
+
+    def _init_sparse_state(self):
+        self._shadow = None
+        self._shadow_version = -1
+        self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
+        self.sparse_pending = 0
+        self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
+
+    def _ensure_sparse_state(self, max_new_rows: int):
+        w = self.weight
+        if self.sparse_grad is None or self.sparse_grad.device != w.device:
+            self.sparse_grad = K.zeros(w.shape, torch.float32, w.device)
+            self.sparse_flags = torch.zeros(w.shape[0], dtype=torch.int32, device=w.device)
+            self.sparse_count = torch.zeros(1, dtype=torch.int64, device=w.device)
+            self.sparse_rows = torch.empty(0, dtype=torch.int64, device=w.device)
+        need = min(self.sparse_pending + max_new_rows, w.shape[0])
+        if self.sparse_rows.numel() < need:
+            new = torch.empty(max(need, 2 * self.sparse_rows.numel()), dtype=torch.int64, device=w.device)
+            if self.sparse_rows.numel():
+                new[: self.sparse_rows.numel()].copy_(self.sparse_rows)
+            self.sparse_rows = new
+
+    def gather_weight(self):
+        if self._gather_dtype == torch.float32:
+            return self.weight
+        if self._shadow is None or self._shadow_version != self.weight._version or \
+                self._shadow.device != self.weight.device:
+            self._shadow = K.cast(self.weight.detach(), self._gather_dtype)
+            self._shadow_version = self.weight._version
+        return self._shadow
+
+
+class KShiftEmbedding(_SparseRowsMixin, nn.Module):
     """commons/layers.py:125-185.
 
     ``num_embeddings`` rows (P) of ``emb_dim`` (D); each id reads K rows at
     ``get_row_idx(id, c)`` (the reference's arithmetic-shift "rotation",
     reproduced bit-exactly), sums them in order in fp32, then scales by
-    1/sqrt(K) or L2-normalises.  Extra keyword ``out_dtype`` (default: the
-    table dtype) lets a bf16 table feed bf16 activations.
+    1/sqrt(K) or L2-normalises.  ``sparse=True`` (the reference's sparse
+    nn.Embedding gradient) accumulates row-wise gradients for
+    ``optim.SparseRowAdagrad`` / ``SparseRowAdamW``.  Extra keyword
+    ``out_dtype`` (default: the table dtype) lets a bf16 table feed bf16
+    activations.
     """
 
     def __init__(self, num_embeddings: int, emb_dim: int, num_shifts: int = 8,
@@ -35,12 +76,24 @@ class KShiftEmbedding(nn.Module):
         self._num_bits = 64
         self._normalize_output = normalize_output
         self._out_dtype = out_dtype
+        self._F = 1
+        self._mode = K.KSHIFT_NORMALIZE if normalize_output else K.KSHIFT_SCALE
+        self._gather_dtype = torch.float32
+        self.sparse = sparse
+        self._init_sparse_state()
         if num_shifts > 64:
             raise ValueError("num_shifts must be <= 64 (64-bit ids)")
 
+    @property
+    def weight(self) -> torch.Tensor:
+        return self.emb.weight
+
     def forward(self, id_: torch.Tensor) -> torch.Tensor:
-        mode = K.KSHIFT_NORMALIZE if self._normalize_output else K.KSHIFT_SCALE
-        return K.kshift(id_, self.emb.weight, self._num_embeddings, self._num_shifts, mode,
+        if self.sparse and self.emb.weight.requires_grad and torch.is_grad_enabled():
+            if self._out_dtype is None:
+                self._out_dtype = self.emb.weight.dtype
+            return _SparseKShiftFn.apply(id_.contiguous(), self.emb.weight, self, self.gather_weight())
+        return K.kshift(id_, self.emb.weight, self._num_embeddings, self._num_shifts, self._mode,
                         out_dtype=self._out_dtype)
 
     def get_row_idx(self, x: torch.Tensor, col_idx: int) -> torch.Tensor:
@@ -125,7 +178,7 @@ class _SparseKShiftFn(torch.autograd.Function):
         return None, None, None, None
 
 
-class TableBatchedKShiftEmbedding(nn.Module):
+class TableBatchedKShiftEmbedding(_SparseRowsMixin, nn.Module):
     """F KShift tables of P rows stored as one [F*P, D] weight (TorchRec-style
     table batching): ids [..., F] -> [..., F, D].  ``sparse=True`` keeps a
     persistent gradient + touched-row list for ``optim.SparseRowAdamW``;
@@ -143,34 +196,7 @@ class TableBatchedKShiftEmbedding(nn.Module):
         self._gather_dtype = gather_dtype
         self.weight = nn.Parameter(torch.randn(num_features * num_embeddings, emb_dim))
         self.sparse = sparse
-        self._shadow = None
-        self._shadow_version = -1
-        self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
-        self.sparse_pending = 0
-        self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
-
-    def _ensure_sparse_state(self, max_new_rows: int):
-        w = self.weight
-        if self.sparse_grad is None or self.sparse_grad.device != w.device:
-            self.sparse_grad = K.zeros(w.shape, torch.float32, w.device)
-            self.sparse_flags = torch.zeros(w.shape[0], dtype=torch.int32, device=w.device)
-            self.sparse_count = torch.zeros(1, dtype=torch.int64, device=w.device)
-            self.sparse_rows = torch.empty(0, dtype=torch.int64, device=w.device)
-        need = min(self.sparse_pending + max_new_rows, w.shape[0])
-        if self.sparse_rows.numel() < need:
-            new = torch.empty(max(need, 2 * self.sparse_rows.numel()), dtype=torch.int64, device=w.device)
-            if self.sparse_rows.numel():
-                new[: self.sparse_rows.numel()].copy_(self.sparse_rows)
-            self.sparse_rows = new
-
-    def gather_weight(self):
-        if self._gather_dtype == torch.float32:
-            return self.weight
-        if self._shadow is None or self._shadow_version != self.weight._version or \
-                self._shadow.device != self.weight.device:
-            self._shadow = K.cast(self.weight.detach(), self._gather_dtype)
-            self._shadow_version = self.weight._version
-        return self._shadow
+        self._init_sparse_state()
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         ids = ids.contiguous()
