@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 6 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 7 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -65,6 +65,12 @@ int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* 
                           int32_t w_dtype, int64_t P, int32_t D, int32_t K, int32_t mode,
                           void* out, int32_t out_dtype, float* norms, void* stream);
 
+/* Pool K rows of a gathered buffer W [R, D] given explicit row indices
+ * rows [n, K] (< R): same in-order f32 sum and finalisation as lthm_kshift_fwd.
+ * The row-sharded item table (C3) pools the rows its all_to_all exchange
+ * returned with it, bit-identical to the unsharded gather. */
+int lthm_gather_pool(const int64_t* rows, int64_t n, int32_t K, const void* W, int32_t w_dtype, int64_t R, int32_t D,
+                     int32_t mode, void* out, int32_t out_dtype, float* norms, void* stream);
 /* Backward of lthm_kshift_fwd(_multi) into a dense f32 gradient dW [F*P, D]
  * (accumulated, caller zeroes).  LDS-staged dedup: each workgroup sorts its
  * (row, id) pairs in LDS, reduces duplicate rows wave-segment-wise, and emits

@@ -206,6 +206,59 @@ class TableBatchedKShiftEmbedding(_SparseRowsMixin, nn.Module):
                         out_dtype=self._out_dtype or self.weight.dtype)
 
 
+class RowShardedKShiftEmbedding(nn.Module):
+    """Forward-only KShift table row-sharded over the data-parallel ranks (the
+    C3 100M-row item table; the LTHM item table is frozen,
+    product_tower.py:47).  Global row r lives on rank r % world (interleaved:
+    the KShift hot rows P-1, P-2, ... spread over ranks) at local index r // world.
+    forward: K row indices per id (kernel) -> dedup -> all_to_all of row ids ->
+    owners gather -> all_to_all of rows back -> in-order f32 pool of the
+    gathered rows (kernel), bit-identical to the unsharded KShiftEmbedding."""
+
+    def __init__(self, num_embeddings: int, emb_dim: int, num_shifts: int = 8, normalize_output: bool = False, *,
+                 rank: Optional[int] = None, world: Optional[int] = None, dtype=torch.bfloat16,
+                 out_dtype=torch.float32):
+        super().__init__()
+        from ..distributed import world_size
+        import torch.distributed as dist
+        self._world = world if world is not None else world_size()
+        self._rank = rank if rank is not None else (dist.get_rank() if dist.is_initialized() else 0)
+        self._num_embeddings = num_embeddings
+        self._num_shifts = num_shifts
+        self._mode = K.KSHIFT_NORMALIZE if normalize_output else K.KSHIFT_SCALE
+        self._out_dtype = out_dtype
+        n_local = (num_embeddings - self._rank + self._world - 1) // self._world
+        # allocated uninitialised and filled N(0, 1) on first use, on the device it
+        # then lives on (a 100M-row table is not drawn on the host); trained tables
+        # arrive through load_full_weight / load_state_dict
+        self.shard = nn.Parameter(torch.empty(n_local, emb_dim, dtype=dtype), requires_grad=False)
+        self._needs_init = True
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self._needs_init = False
+
+    @torch.no_grad()
+    def load_full_weight(self, weight: torch.Tensor):
+        """Take this rank's rows (r % world == rank) of a full [P, D] table."""
+        self.shard.data.copy_(weight[self._rank::self._world].to(self.shard.dtype))
+        self._needs_init = False
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        from ..distributed import exchange_rows
+        if self._needs_init:
+            g = torch.Generator(device=self.shard.device).manual_seed(1234 + self._rank)
+            self.shard.data.normal_(generator=g)
+            self._needs_init = False
+        flat = ids.reshape(-1).contiguous()
+        rows = K.kshift_rows(flat, self._num_embeddings, self._num_shifts)  # [N, K] global rows
+        uniq, inv = torch.unique(rows.view(-1), return_inverse=True)
+        vals = exchange_rows(uniq, self.shard)
+        out = K.gather_pool(inv.view(flat.shape[0], self._num_shifts), vals, self._mode, out_dtype=self._out_dtype)
+        return out.view(*ids.shape, vals.shape[1])
+
+
 # ------------------------------------------------------------------ feature interaction
 class QuickGELU(nn.Module):
     """commons/layers.py:9-11."""

@@ -30,7 +30,8 @@ __global__ __launch_bounds__(256) void kshift_rows_k(const int64_t* __restrict__
 template <typename TW, typename TO, int VB>
 __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
     const int64_t* __restrict__ ids, int64_t n_items, int F, const TW* __restrict__ W, int64_t P,
-    int D, int K, int mode, float scale, TO* __restrict__ out, float* __restrict__ norms, int LPR_LOG2) {
+    int D, int K, int mode, float scale, TO* __restrict__ out, float* __restrict__ norms, int LPR_LOG2,
+    const int64_t* __restrict__ xrows) {
   constexpr int NE = VB / (int)sizeof(TW);  // elements per lane
   __shared__ int64_t rows_lds[KS_BLOCK / 64][KS_ROWS_LDS];
   const int LPR = 1 << LPR_LOG2;
@@ -45,12 +46,14 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
     const int64_t item = base + wave * IPW + gi;
     const bool valid = item < n_items;
     int64_t id = 0, rbase = 0;
-    if (valid) {
+    if (valid && xrows == nullptr) {
       id = ids[item];
       rbase = (F > 1) ? (int64_t)(item % F) * P : 0;
     }
-    // rows for this item, spread over the group's lanes
-    for (int c = gl; c < K; c += LPR) rows_lds[wave][gi * K + c] = valid ? rbase + kshift_row(id, c, P) : 0;
+    // rows for this item (computed, or explicit rows [n, K] for gathered buffers),
+    // spread over the group's lanes
+    for (int c = gl; c < K; c += LPR)
+      rows_lds[wave][gi * K + c] = !valid ? 0 : (xrows ? xrows[item * K + c] : rbase + kshift_row(id, c, P));
     __syncthreads();
     float acc[NE];
 #pragma unroll
@@ -262,7 +265,7 @@ static int pick_vb(int D, int esz, int* lpr_log2) {
 
 template <typename TW, typename TO>
 static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W, int64_t P, int D, int K,
-                      int mode, void* out, float* norms, hipStream_t s) {
+                      int mode, void* out, float* norms, hipStream_t s, const int64_t* xrows = nullptr) {
   int l2 = 0;
   const int vb = pick_vb(D, (int)sizeof(TW), &l2);
   LTHM_REQUIRE(vb > 0);
@@ -274,13 +277,13 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
   const float scale = (float)__builtin_sqrt((double)K);
   if (vb == 16)
     hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 16>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
-                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2, xrows);
   else if (vb == 8)
     hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 8>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
-                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2, xrows);
   else if (vb == 4)
     hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 4>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
-                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2);
+                       (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2, xrows);
   else
     return (int)hipErrorInvalidValue;
   LTHM_CHECK_LAUNCH();
@@ -329,19 +332,20 @@ int lthm_kshift_rows(const int64_t* ids, int64_t n, int64_t P, int32_t K, int64_
 }
 
 static int kshift_fwd_impl(const int64_t* ids, int64_t n_items, int F, const void* W, int w_dtype, int64_t P,
-                           int D, int K, int mode, void* out, int out_dtype, float* norms, void* stream) {
+                           int D, int K, int mode, void* out, int out_dtype, float* norms, void* stream,
+                           const int64_t* xrows = nullptr) {
   LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n_items >= 0 && F >= 1);
   LTHM_REQUIRE(mode >= 0 && mode <= 2);
   if (n_items == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (w_dtype == LTHM_F32 && out_dtype == LTHM_F32)
-    return launch_fwd<float, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+    return launch_fwd<float, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
   if (w_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
-    return launch_fwd<float, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+    return launch_fwd<float, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
   if (w_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
-    return launch_fwd<bf16_t, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+    return launch_fwd<bf16_t, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
   if (w_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
-    return launch_fwd<bf16_t, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s);
+    return launch_fwd<bf16_t, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
   return (int)hipErrorInvalidValue;
 }
 
@@ -359,6 +363,12 @@ int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* 
                           int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, float* norms,
                           void* stream) {
   return kshift_fwd_impl(ids, n * (int64_t)F, F, W, w_dtype, P, D, K, mode, out, out_dtype, norms, stream);
+}
+
+int lthm_gather_pool(const int64_t* rows, int64_t n, int32_t K, const void* W, int32_t w_dtype, int64_t R, int32_t D,
+                     int32_t mode, void* out, int32_t out_dtype, float* norms, void* stream) {
+  LTHM_REQUIRE(rows != nullptr || n == 0);
+  return kshift_fwd_impl(nullptr, n, 1, W, w_dtype, R, D, K, mode, out, out_dtype, norms, stream, rows);
 }
 
 int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,

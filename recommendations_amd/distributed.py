@@ -100,6 +100,33 @@ def gather_sparse_grads(ids: torch.Tensor, gy: torch.Tensor, out: Optional[torch
     return ids_all, gy_all, out, norms
 
 
+def exchange_rows(uniq: torch.Tensor, shard: torch.Tensor) -> torch.Tensor:
+    """Row-sharded table lookup: global row r lives on rank
+    r % world at local index r // world.  ``uniq`` are this rank's deduplicated
+    global rows; returns their values [len(uniq), D] in the same order.
+    Two all_to_all_single exchanges: row ids out (int64), row values back
+    (the shard dtype, bf16 for the frozen item table); one host read of the
+    per-peer counts."""
+    ws = world_size()
+    if ws == 1:
+        return shard.index_select(0, uniq)
+    owner = torch.remainder(uniq, ws)
+    order = torch.argsort(owner, stable=True)
+    send_rows = uniq.index_select(0, order)
+    send_counts = torch.bincount(owner, minlength=ws)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    recv_rows = torch.empty(sum(rc), dtype=torch.int64, device=uniq.device)
+    dist.all_to_all_single(recv_rows, send_rows, rc, sc)
+    vals = shard.index_select(0, torch.div(recv_rows, ws, rounding_mode="floor"))
+    back = torch.empty((sum(sc),) + tuple(shard.shape[1:]), dtype=shard.dtype, device=shard.device)
+    dist.all_to_all_single(back, vals, sc, rc)
+    out = torch.empty_like(back)
+    out.index_copy_(0, order, back)
+    return out
+
+
 def step_flags(stop: bool, loss: torch.Tensor) -> torch.Tensor:
     """[stop, non-finite loss] MAX-reduced over ranks in one collective (no host sync here)."""
     f = torch.stack([torch.tensor(float(stop), device=loss.device), (~torch.isfinite(loss.detach())).float().reshape(())])

@@ -104,6 +104,20 @@ def kshift(ids, weight, P: int, K: int, mode: int, F: int = 1, out_dtype=None):
     return KShiftFn.apply(ids.contiguous(), weight, P, K, mode, F, out_dtype)
 
 
+def gather_pool(rows: torch.Tensor, W: torch.Tensor, mode: int, out_dtype=torch.float32):
+    """out[i] = finalize(sum_c W[rows[i, c]]) (include/lthm.h lthm_gather_pool): rows [n, K] int64 < W.shape[0]."""
+    require_gpu(rows, W)
+    _check(rows.dtype == torch.int64 and rows.dim() == 2, "rows must be int64 [n, K]")
+    n, Kk = rows.shape
+    _check(0 < Kk <= 64, "K must be in 1..64")
+    D = W.shape[1]
+    out = torch.empty((n, D), dtype=out_dtype, device=W.device)
+    call("lthm_gather_pool", ptr(rows), n, Kk, ptr(W), dcode(W), W.shape[0], D, mode, ptr(out), dcode(out), None,
+         stream(), _key="kshift_fwd_k", _work=n * (8 * Kk + Kk * D * W.element_size() + D * out.element_size()),
+         _unit="byte")
+    return out
+
+
 # ----------------------------------------------------------------- helpers
 def cast(x: torch.Tensor, dtype) -> torch.Tensor:
     """dtype cast in a HIP kernel (f32 <-> bf16)."""

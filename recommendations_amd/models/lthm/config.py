@@ -91,6 +91,9 @@ class LTHMModelConfig(BaseModel):
     metrics_k_all: List[int] = [1, 5, 20, 50]
     categorical: CategoricalContextConfig = Field(default_factory=CategoricalContextConfig)
     item_table_bf16: bool = True
+    # build-defined: row-shard the frozen item KShift table over
+    # the data-parallel ranks (r on rank r % world) instead of replicating it
+    item_table_sharded: bool = False
     seed: int = 1234
 
     @property

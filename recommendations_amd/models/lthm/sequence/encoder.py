@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from .... import kernels as K
 from ....commons.functional import cap_gradients
-from ....commons.layers import KShiftEmbedding, MLP, TableBatchedKShiftEmbedding
+from ....commons.layers import KShiftEmbedding, MLP, RowShardedKShiftEmbedding, TableBatchedKShiftEmbedding
 from .product_tower import ProductTower
 from .query_tower import QueryTower
 
@@ -48,11 +48,18 @@ class Encoder(nn.Module):
         lm = pt.latent_model_config
         # fp32 output: the CVE bucketize downstream is discontinuous, a bf16-rounded
         # input would flip ~1% of the bucket decisions relative to the reference
-        self.product_emb_module = KShiftEmbedding(lm.vocab_size_latent, pt.inp_emb_dim, num_shifts=lm.num_shifts_latent,
-                                                  normalize_output=lm.normalize_embedding, out_dtype=torch.float32)
-        if model_config.item_table_bf16:
-            self.product_emb_module.emb.weight.data = self.product_emb_module.emb.weight.data.to(torch.bfloat16)
-        self.product_emb_module.emb.weight.requires_grad_(False)  # detached by product_tower.py:47
+        if model_config.item_table_sharded:
+            self.product_emb_module = RowShardedKShiftEmbedding(
+                lm.vocab_size_latent, pt.inp_emb_dim, num_shifts=lm.num_shifts_latent,
+                normalize_output=lm.normalize_embedding,
+                dtype=torch.bfloat16 if model_config.item_table_bf16 else torch.float32, out_dtype=torch.float32)
+        else:
+            self.product_emb_module = KShiftEmbedding(lm.vocab_size_latent, pt.inp_emb_dim,
+                                                      num_shifts=lm.num_shifts_latent,
+                                                      normalize_output=lm.normalize_embedding, out_dtype=torch.float32)
+            if model_config.item_table_bf16:
+                self.product_emb_module.emb.weight.data = self.product_emb_module.emb.weight.data.to(torch.bfloat16)
+            self.product_emb_module.emb.weight.requires_grad_(False)  # detached by product_tower.py:47
         self.product_tower = ProductTower(model_config)
         self.query_tower = QueryTower(model_config)
         self.user_context = UserContext(model_config.categorical, model_config.emb_dim) \

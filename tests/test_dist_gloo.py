@@ -121,3 +121,29 @@ def _gather_rows(rank, world):
 def test_all_gather_rows_rank_order():
     for out in spawn(_gather_rows):
         assert torch.equal(out, torch.cat([torch.arange(6).view(3, 2), torch.arange(6).view(3, 2) + 100]))
+
+
+def _sharded_lookup(rank, world):
+    """Row-sharded table (r on rank r % world): every rank exchanges its own
+    deduplicated KShift rows and gets exactly the full table's rows back."""
+    from recommendations_amd.distributed import exchange_rows
+    from oracle.ref import kshift_rows, kshift_fwd_c
+    P, D, Kk = 1000, 8, 16
+    W = torch.from_numpy(np.random.default_rng(5).standard_normal((P, D)).astype(np.float32))
+    shard = W[rank::world].contiguous()
+    g = np.random.default_rng(40 + rank)
+    ids = g.integers(-2**63, 2**63 - 1, size=300 + 50 * rank, dtype=np.int64)
+    rows = torch.from_numpy(kshift_rows(ids, P, Kk))
+    uniq, inv = torch.unique(rows.view(-1), return_inverse=True)
+    vals = exchange_rows(uniq, shard)
+    exact = torch.equal(vals, W.index_select(0, uniq))
+    # in-order pool of the exchanged rows == the unsharded gather (oracle)
+    pooled = vals[inv.view(-1, Kk)].sum(dim=1)
+    ref = torch.from_numpy(kshift_fwd_c(ids, W.numpy(), Kk, 2))
+    return exact, float((pooled - ref).abs().max())
+
+
+def test_row_sharded_exchange():
+    for exact, err in spawn(_sharded_lookup):
+        assert exact
+        assert err < 1e-5

@@ -85,3 +85,20 @@ def test_empty_and_errors(dev):
         K.kshift(torch.zeros(3, dtype=torch.int64, device=dev), W, 10, 65, K.KSHIFT_SCALE)
     with pytest.raises(RuntimeError):
         K.kshift(torch.zeros(3, dtype=torch.int64), W.cpu(), 10, 4, K.KSHIFT_SCALE)
+
+
+@pytest.mark.parametrize("normalize", [False, True])
+def test_row_sharded_single_rank_bit_exact(dev, normalize):
+    """RowShardedKShiftEmbedding at world 1 (exchange = local gather) equals KShiftEmbedding bit for bit."""
+    from recommendations_amd.commons.layers import KShiftEmbedding, RowShardedKShiftEmbedding
+    torch.manual_seed(3)
+    full = KShiftEmbedding(50000, 32, num_shifts=16, normalize_output=normalize, out_dtype=torch.float32)
+    full.emb.weight.data = full.emb.weight.data.to(torch.bfloat16)
+    sh = RowShardedKShiftEmbedding(50000, 32, num_shifts=16, normalize_output=normalize, rank=0, world=1)
+    sh.load_full_weight(full.emb.weight.data)
+    full, sh = full.to(dev), sh.to(dev)
+    ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (4096, 8), dtype=torch.int64).to(dev)
+    with torch.no_grad():
+        a = full(ids)
+        b = sh(ids)
+    assert torch.equal(a, b)
