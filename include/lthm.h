@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 7 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 8 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -332,9 +332,12 @@ int lthm_outcome_fwd(const float* x, const int64_t* labels, int64_t B, int32_t T
 /* ------------------------------------------------------------------------- */
 /* In-batch contrastive loss (models/lthm/sequence/wrapper.py:114-245)        */
 /* ------------------------------------------------------------------------- */
-/* F.normalize of rows: out bf16 [rows, D], norms f32 [rows] (wrapper.py:118-119) */
+/* F.normalize of rows: out bf16 [rows, D], norms f32 [rows] (wrapper.py:118-119).
+ * row_mask (may be NULL): rows r with row_mask[(r / mask_group) * mask_stride + r % mask_group]
+ * set get a zero output row (the loss zeroes the `in` rows of pad positions, which
+ * every logit of them excludes; their norm is still written). */
 int lthm_rownorm(const void* x, int32_t x_dtype, int64_t rows, int32_t D, void* out_bf16, float* norms,
-                 void* stream);
+                 const uint8_t* row_mask, int64_t mask_group, int64_t mask_stride, void* stream);
 /* backward of lthm_rownorm: dx = (g - y (y.g)) / |x|; writes dx_bf16 and/or dx_f32 */
 int lthm_rownorm_bwd(const void* x, int32_t x_dtype, const float* norms, const float* g, int64_t rows,
                      int32_t D, void* dx_bf16, float* dx_f32, void* stream);
@@ -358,7 +361,8 @@ typedef struct lthm_contrastive_desc {
   float* pos;
   int32_t* cnt;
   int32_t* rank;
-  float* diag;
+  float* diag;            /* forward: positive logit (-inf: pad row / r >= n);
+                             backward: scratch for the per-row exp2 shift */
   float* w;               /* row weights, written by the forward, read by the backward */
   const float* gscale;    /* device scalar: upstream gradient of the loss (backward) */
   float* d_out;           /* f32 [B, T+1, n_heads, De] (rows of this head written) */

@@ -15,6 +15,16 @@ namespace lthm {
 
 typedef uint16_t bf16_t;
 
+// ---- XCD-aware block order ----
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch): remap the linear block id so that each XCD walks a contiguous range
+// of logical ids (neighbouring tiles share its L2).  Bijective for any nwg; a
+// speed choice only, never needed for correctness.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // ---- bf16 <-> f32 (round-to-nearest-even, NaN stays NaN; identical to torch) ----
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);

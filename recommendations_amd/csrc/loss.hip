@@ -23,6 +23,13 @@ namespace lthm {
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// two f32 -> packed bf16 pair, round-to-nearest-even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+}
 
 constexpr int DE = 128;  // product_emb_dim (model/lthm.yaml:22)
 
@@ -34,7 +41,8 @@ __device__ __forceinline__ int ks_off256(int row, int ch) {
 // out[r] = bf16(x[r] / max(|x[r]|, 1e-12)), norms[r] = |x[r]|   (F.normalize, wrapper.py:118-119)
 template <typename TX>
 __global__ __launch_bounds__(256) void rownorm_k(const TX* __restrict__ x, int64_t rows, int D, bf16_t* __restrict__ out,
-                                                 float* __restrict__ norms) {
+                                                 float* __restrict__ norms, const uint8_t* __restrict__ mask,
+                                                 int64_t mgroup, int64_t mstride) {
   const int lane = threadIdx.x & 63;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
     float v[4];
@@ -47,10 +55,11 @@ __global__ __launch_bounds__(256) void rownorm_k(const TX* __restrict__ x, int64
     }
     const float nrm = sqrtf(wave_sum(ss));
     const float den = fmaxf(nrm, 1e-12f);
+    const bool zero = mask && mask[(r / mgroup) * mstride + r % mgroup];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = lane + 64 * i;
-      if (c < D) out[r * D + c] = f2bf(v[i] / den);
+      if (c < D) out[r * D + c] = zero ? (bf16_t)0 : f2bf(v[i] / den);
     }
     if (lane == 0) norms[r] = nrm;
   }
@@ -81,6 +90,106 @@ __global__ __launch_bounds__(256) void rownorm_bwd_k(const TX* __restrict__ x, c
         const float o = (nrm > 1e-12f) ? (gv[i] - y[i] * dot) / nrm : gv[i] / 1e-12f;
         if (dx_bf) dx_bf[r * D + c] = f2bf(o);
         if (dx_f) dx_f[r * D + c] = o;
+      }
+    }
+  }
+}
+
+// Vectorised forms (D % 8 == 0, D <= 256): 16 lanes per row, 8 contiguous
+// elements (16 B of bf16 / 32 B of f32) per lane and pass, NC passes.
+template <typename TX>
+__device__ __forceinline__ void ld8(const TX* p, float* v) {
+  if constexpr (sizeof(TX) == 2) {
+    load_vec<TX, 16>(p, v);
+  } else {
+    load_vec<TX, 16>(p, v);
+    load_vec<TX, 16>(p + 4, v + 4);
+  }
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// rows whose mask byte mask[(r / mgroup) * mstride + r % mgroup] is set get a zero
+// output row (their norm is still written, for the backward)
+template <typename TX, int NC>
+__global__ __launch_bounds__(256) void rownorm_v8_k(const TX* __restrict__ x, int64_t rows, int D,
+                                                    bf16_t* __restrict__ out, float* __restrict__ norms,
+                                                    const uint8_t* __restrict__ mask, int64_t mgroup,
+                                                    int64_t mstride) {
+  const int sub = threadIdx.x & 15;
+  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < rows; r += (int64_t)gridDim.x * 16) {
+    float v[NC][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int e = (sub + 16 * c) * 8;
+      if (e < D) ld8(x + r * D + e, v[c]);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+    const float nrm = sqrtf(group16_sum(ss));
+    const float den = fmaxf(nrm, 1e-12f);
+    const bool zero = mask && mask[(r / mgroup) * mstride + r % mgroup];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int e = (sub + 16 * c) * 8;
+      if (e < D) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = zero ? 0.f : v[c][i] / den;
+        store_vec<bf16_t, 8>(out + r * D + e, o);
+      }
+    }
+    if (sub == 0) norms[r] = nrm;
+  }
+}
+
+template <typename TX, int NC>
+__global__ __launch_bounds__(256) void rownorm_bwd_v8_k(const TX* __restrict__ x, const float* __restrict__ norms,
+                                                        const float* __restrict__ g, int64_t rows, int D,
+                                                        bf16_t* __restrict__ dx_bf, float* __restrict__ dx_f) {
+  const int sub = threadIdx.x & 15;
+  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < rows; r += (int64_t)gridDim.x * 16) {
+    const float nrm = norms[r];
+    const float den = fmaxf(nrm, 1e-12f);
+    float y[NC][8], gv[NC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int e = (sub + 16 * c) * 8;
+      if (e < D) {
+        ld8(x + r * D + e, y[c]);
+        ld8(g + r * D + e, gv[c]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[c][i] = gv[c][i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        y[c][i] /= den;
+        dot += y[c][i] * gv[c][i];
+      }
+    }
+    dot = group16_sum(dot);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int e = (sub + 16 * c) * 8;
+      if (e < D) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (nrm > 1e-12f) ? (gv[c][i] - y[c][i] * dot) / nrm : gv[c][i] / 1e-12f;
+        if (dx_bf) store_vec<bf16_t, 8>(dx_bf + r * D + e, o);
+        if (dx_f) {
+          store_vec<float, 4>(dx_f + r * D + e, o);
+          store_vec<float, 4>(dx_f + r * D + e + 4, o + 4);
+        }
       }
     }
   }
@@ -159,17 +268,34 @@ __device__ __forceinline__ void reg_frags(bf16x8v (&f)[4], int lane, int cnt, in
   }
 }
 
-// diag[r] = out_r . in_r / tau (fp32 dot of the bf16 operands), per (mb, row)
+// diag[r] = out_r . in_r / tau (fp32 dot of the bf16 operands), per (mb, row);
+// -inf for pad rows and for the rows n <= r < n_max (the forward reads the
+// diag of its columns as their pad flag)
 __global__ __launch_bounds__(256) void cl_diag_k(ClArgs a) {
   const int mb = blockIdx.y;
   const Geo g = geo(a, mb);
   const int lane = threadIdx.x & 63;
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < g.n; r += gridDim.x * 4) {
-    const bf16_t* o = out_row(a, g, r);
-    const bf16_t* i = in_row(a, g, r);
-    float s = bf2f(o[lane]) * bf2f(i[lane]) + bf2f(o[lane + 64]) * bf2f(i[lane + 64]);
-    s = wave_sum(s);
-    if (lane == 0) a.diag[(int64_t)mb * a.n_max + r] = s / a.tau;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < a.n_max; r += gridDim.x * 4) {
+    float s = -INFINITY;
+    if (r < g.n && !pad_of(a, g, r)) {
+      const bf16_t* o = out_row(a, g, r);
+      const bf16_t* i = in_row(a, g, r);
+      s = bf2f(o[lane]) * bf2f(i[lane]) + bf2f(o[lane + 64]) * bf2f(i[lane + 64]);
+      s = wave_sum(s) / a.tau;
+    }
+    if (lane == 0) a.diag[(int64_t)mb * a.n_max + r] = s;
+  }
+}
+
+// backward prologue: shift[r] = log2 w_r - lse_r log2 e (-inf where w_r = 0 or r >= n),
+// the exp2 shift that folds the row weight into dS = w (e^(S/tau - lse) - [r == c])
+__global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ shift) {
+  const int mb = blockIdx.y;
+  const Geo g = geo(a, mb);
+  const int64_t base = (int64_t)mb * a.n_max;
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < a.n_max; r += gridDim.x * 256) {
+    const float wv = r < g.n ? a.w[base + r] : 0.f;
+    shift[base + r] = wv != 0.f ? __log2f(wv) - a.lse[base + r] * 1.4426950408889634f : -INFINITY;
   }
 }
 
@@ -280,36 +406,81 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a, float* __restrict__ 
 
 // ---------------------------------------------------------------- tile engine
 // 128 register rows per block (each wave: 32 rows = two 16-row MFMA tiles),
-// 64-row column tiles staged through LDS with register prefetch (one barrier
-// per tile), per-tile column metadata in LDS.  Rows are L2-normalised, so every
-// logit lies in [-1/tau, 1/tau] (up to bf16 rounding): with 2/tau <= 80 the
-// softmax shift is the constant 1/tau (no running max, exp never under- or
-// overflows); smaller tau falls back to a per-tile online max.
+// 64-row column tiles streamed into a 3-deep LDS ring by LDS-DMA
+// (global_load_lds_dwordx4): tile t + 2 is issued right after the barrier that
+// opens tile t, so two tiles of loads are in flight behind the math; a counted
+// `s_waitcnt vmcnt` plus a raw `s_barrier` retire tile t (no vmcnt(0) drain).
+// The DMA's LDS destination is lane-linear, so the ks_off256 swizzle is applied
+// to the source chunk.  Rows beyond n are read from a zero row; the wrapper
+// zeroes the normalised `in` rows of pad positions, so pad columns of the
+// forward / dOut images are zero rows too.
+//
+// Rows are L2-normalised, so every logit lies in [-1/tau, 1/tau] (up to bf16
+// rounding): with 2/tau <= 80 the softmax shift is the constant 1/tau (no
+// running max, exp never under- or overflows); smaller tau falls back to a
+// per-tile online max.
+//
+// Clean tiles.  With the fixed shift, a column tile that holds no column of
+// the sequences of the block's rows (no same-sequence exclusion, no diagonal)
+// needs no per-element masking: pad columns are zero image rows with a -inf
+// exponent shift (forward: their logit 0 is removed from the rank by count),
+// so an element costs one fma + one v_exp (+ one compare for the rank).  Only
+// the <= 3-4 tiles that meet the block's own sequences take the masked path.
+// Exponentials are exp2 with log2(e) folded into the scale and the row weights
+// folded into the shift (w e^t = 2^(t log2 e + log2 w)).
 constexpr int CL_ROWS = 128;
+constexpr int CL_NBUF = 3;
+constexpr float LOG2E = 1.4426950408889634f;
 
 struct ClTile {
-  unsigned char img[2][64 * 256];
-  int seq[2][64];     // sequence id of each tile row (-1: beyond n)
-  float lse[2][64];   // COLS pass: LSE of the image rows
-  float w[2][64];     // COLS pass: weights of the image rows
-  uint8_t pad[2][64];
+  unsigned char img[CL_NBUF][64 * 256];
+  float m0[CL_NBUF][4][64];  // per-wave copies of a per-column vector (fwd: diag; bwd COLS: shift)
+  float m1[CL_NBUF][4][64];  // bwd COLS: row weights of the image rows
 };
 
-template <typename RowFn>
-__device__ __forceinline__ void cl_fetch(u32x4 (&pf)[4], int tid, int cnt, RowFn rowp) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int idx = tid + 256 * k;
-    const int row = idx >> 4, ch = idx & 15;
-    pf[k] = u32x4{0u, 0u, 0u, 0u};
-    if (row < cnt) pf[k] = *reinterpret_cast<const u32x4*>(rowp(row) + ch * 8);
-  }
+__device__ __attribute__((aligned(16))) unsigned char cl_zero_row[256];
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// LDS-DMA issued as asm: the compiler neither counts these loads nor guards LDS
+// reads against them (the builtin makes it drain vmcnt(0) before unrelated LDS
+// reads); the kernels retire them with explicit counted waits + a barrier.
+// Ordinary loads stay correct: in-order vmcnt only makes their waits stricter.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)p);
 }
-__device__ __forceinline__ void cl_store(unsigned char* img, int tid, const u32x4 (&pf)[4]) {
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// retire every ordinary load issued so far, visibly to the compiler's own wait
+// bookkeeping (vmcnt(0), expcnt / lgkmcnt untouched): issued before the DMA
+// prologue, so no first use inside the tile loop drains the DMA ring
+__device__ __forceinline__ void retire_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// image rows [0, 64) of a tile: wave w stages rows 16w .. 16w + 15 with four
+// DMAs of 4 rows x 256 B; lane l lands at row 4k + l/16, slot l%16 and loads
+// chunk slot ^ swz(row), which puts chunk ch at ks_off256(row, ch)
+template <typename RowFn>
+__device__ __forceinline__ void stage_img(unsigned char* img, int w, int lane, int cnt, RowFn rowp) {
+  const int slot = lane & 15;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int idx = tid + 256 * k;
-    *reinterpret_cast<u32x4*>(img + ks_off256(idx >> 4, idx & 15)) = pf[k];
+    const int row = 16 * w + 4 * k + (lane >> 4);
+    const int ch = slot ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    const void* src = row < cnt ? (const void*)(rowp(row) + ch * 8) : (const void*)(cl_zero_row + 16 * slot);
+    glds16(src, img + (16 * w + 4 * k) * 256);
   }
 }
 
@@ -346,22 +517,57 @@ __device__ __forceinline__ void st_tile(f32x4 (&acc)[2][4], const bf16x8v (&qf)[
     }
 }
 
+// this lane's 16 per-column values v[yb*16 + rg + j] of a 64-entry LDS row
+__device__ __forceinline__ void col_vals(float (&o)[4][4], const float* v, int rg) {
+#pragma unroll
+  for (int yb = 0; yb < 4; ++yb) {
+    const float4 q = *reinterpret_cast<const float4*>(v + yb * 16 + rg);
+    o[yb][0] = q.x; o[yb][1] = q.y; o[yb][2] = q.z; o[yb][3] = q.w;
+  }
+}
+
+// the column range [lo, hi) of the sequences that the block's rows [x0, x0 + 128) touch
+__device__ __forceinline__ void own_cols(const Geo& g, int x0, int& lo, int& hi) {
+  const int xe = min(x0 + CL_ROWS, g.n) - 1;
+  lo = (x0 / g.L) * g.L;
+  hi = (xe / g.L + 1) * g.L;
+}
+
+__device__ __forceinline__ float next_up(float t) {
+  if (t != t || t == INFINITY) return t;
+  if (t == 0.f) return __int_as_float(1);
+  const int b = __float_as_int(t);
+  return __int_as_float(t > 0.f ? b + 1 : b - 1);
+}
+// the largest float t with fl(t * it) <= dg, so that (a > t) == (fl(a * it) > dg)
+// for every float a (a -> fl(a * it) is monotone for it > 0)
+__device__ __forceinline__ float rank_threshold(float dg, float it, float tau) {
+  float t = dg * tau;
+  for (int k = 0; k < 16 && t * it > dg; ++k) t = -next_up(-t);
+  for (int k = 0; k < 16 && next_up(t) * it <= dg; ++k) t = next_up(t);
+  return t;
+}
+
 template <bool FIXED>
 __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
   __shared__ __attribute__((aligned(16))) ClTile sh;
-  const int mb = blockIdx.y;
+  const int bid = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int mb = bid / gridDim.x;
   const Geo g = geo(a, mb);
-  const int r0 = blockIdx.x * CL_ROWS;
+  const int r0 = (bid - mb * gridDim.x) * CL_ROWS;
   if (r0 >= g.n) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, rg = 4 * (lane >> 4);
+  const int64_t base = (int64_t)mb * a.n_max;
   bf16x8v qf[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
     reg_frags(qf[mi], lane, g.n, r0 + 32 * w + 16 * mi, [&](int r) { return out_row(a, g, r); });
-  const float it = 1.f / a.tau;
+  const float it = 1.f / a.tau, c1 = it * LOG2E, cs = -it * LOG2E;
+  int spec_lo, spec_hi;
+  own_cols(g, r0, spec_lo, spec_hi);
   // this lane's rows: r = r0 + 32 w + 16 mi + col  (one per mi)
-  float m[2], l[2], pv[2], dg[2];
+  float m[2], l[2], pv[2], dg[2], thr[2];
   int cn[2], rk[2], rsq[2], rr[2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
@@ -369,77 +575,101 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
     rr[mi] = r;
     m[mi] = FIXED ? it : -INFINITY;
     l[mi] = 0.f; pv[mi] = -INFINITY; cn[mi] = 0; rk[mi] = 0;
-    dg[mi] = (r < g.n) ? a.diag[(int64_t)mb * a.n_max + r] : 0.f;
+    dg[mi] = (r < g.n) ? a.diag[base + r] : 0.f;
+    thr[mi] = rank_threshold(dg[mi], it, a.tau);
     rsq[mi] = (r < g.n) ? r / g.L : -2;
   }
   const int ntile = (g.n + 63) / 64;
-  u32x4 pf[4];
-  cl_fetch(pf, tid, g.n, [&](int i) { return in_row(a, g, i); });
-  cl_store(sh.img[0], tid, pf);
-  if (tid < 64) {
-    sh.seq[0][tid] = tid < g.n ? tid / g.L : -1;
-    sh.pad[0][tid] = tid < g.n ? (pad_of(a, g, tid) ? 1 : 0) : 1;
-  }
-  __syncthreads();
+  // 5 DMAs per wave and tile: 4 image pieces + the diag (pad flag) of the tile's columns
+  auto stage = [&](int t) {
+    const int buf = t % CL_NBUF, c0 = t * 64;
+    stage_img(sh.img[buf], w, lane, g.n - c0, [&](int i) { return in_row(a, g, c0 + i); });
+    glds4(a.diag + base + c0 + lane, sh.m0[buf][w]);
+  };
+  retire_loads();
+  stage(0);
+  if (ntile > 1) stage(1);
   for (int tI = 0; tI < ntile; ++tI) {
-    const int cur = tI & 1, c0 = tI * 64;
-    const bool more = tI + 1 < ntile;
-    if (more) cl_fetch(pf, tid, g.n - c0 - 64, [&](int i) { return in_row(a, g, c0 + 64 + i); });
+    const int cur = tI % CL_NBUF, c0 = tI * 64;
+    if (tI + 1 < ntile) wait_vm<5>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (tI + 2 < ntile) stage(tI + 2);
     f32x4 acc[2][4];
     st_tile(acc, qf, sh.img[cur], lane);
-    int csq[4][4];
-    bool cok[4][4];
+    const float* cdg = sh.m0[cur][w];  // -inf: pad column or beyond n
+    const bool special = !FIXED || (c0 < spec_hi && c0 + 64 > spec_lo);
+    if (!special) {
+      float cb[4][4];
+      col_vals(cb, cdg, rg);
 #pragma unroll
-    for (int yb = 0; yb < 4; ++yb)
+      for (int yb = 0; yb < 4; ++yb)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int cl = yb * 16 + rg + j;
-        csq[yb][j] = sh.seq[cur][cl];
-        cok[yb][j] = !sh.pad[cur][cl];
+        for (int j = 0; j < 4; ++j) cb[yb][j] = cb[yb][j] == -INFINITY ? -INFINITY : cs;
+      const int np = __popcll(__ballot(cdg[lane] == -INFINITY));
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        int k = 0;
+#pragma unroll
+        for (int yb = 0; yb < 4; ++yb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            l[mi] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, cb[yb][j]));
+            k += acc[mi][yb][j] > thr[mi] ? 1 : 0;
+          }
+        // the zero pad / beyond-n rows give logit 0: count them once per row (lane group 0)
+        if (rg == 0) {
+          cn[mi] += 64 - np;
+          k -= (0.f > thr[mi]) ? np : 0;
+        }
+        rk[mi] += k;
       }
+    } else {
+      int csq[4][4];
+      bool cok[4][4];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int r = rr[mi];
-      if constexpr (!FIXED) {
-        float bm = -INFINITY;
+      for (int yb = 0; yb < 4; ++yb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cl = yb * 16 + rg + j;
+          cok[yb][j] = cdg[cl] != -INFINITY;
+          csq[yb][j] = (c0 + cl) / g.L;
+        }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int r = rr[mi];
+        if constexpr (!FIXED) {
+          float bm = -INFINITY;
+#pragma unroll
+          for (int yb = 0; yb < 4; ++yb)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int c = c0 + yb * 16 + rg + j;
+              if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) bm = fmaxf(bm, acc[mi][yb][j] * it);
+            }
+          bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+          bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+          const float mn = fmaxf(m[mi], bm);
+          if (mn != -INFINITY) {
+            l[mi] *= (m[mi] == -INFINITY) ? 0.f : __expf(m[mi] - mn);
+            m[mi] = mn;
+          }
+        }
 #pragma unroll
         for (int yb = 0; yb < 4; ++yb)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int c = c0 + yb * 16 + rg + j;
-            if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) bm = fmaxf(bm, acc[mi][yb][j] * it);
+            const float v = acc[mi][yb][j] * it;
+            if (c == r) pv[mi] = v;
+            if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) {
+              l[mi] += __expf(v - m[mi]);
+              cn[mi] += 1;
+              rk[mi] += (c != r && v > dg[mi]) ? 1 : 0;
+            }
           }
-        bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-        const float mn = fmaxf(m[mi], bm);
-        if (mn != -INFINITY) {
-          l[mi] *= (m[mi] == -INFINITY) ? 0.f : __expf(m[mi] - mn);
-          m[mi] = mn;
-        }
-      }
-#pragma unroll
-      for (int yb = 0; yb < 4; ++yb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = c0 + yb * 16 + rg + j;
-          const float v = acc[mi][yb][j] * it;
-          if (c == r) pv[mi] = v;
-          if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) {
-            l[mi] += __expf(v - m[mi]);
-            cn[mi] += 1;
-            rk[mi] += (c != r && v > dg[mi]) ? 1 : 0;
-          }
-        }
-    }
-    if (more) {
-      cl_store(sh.img[cur ^ 1], tid, pf);
-      if (tid < 64) {
-        const int c = c0 + 64 + tid;
-        sh.seq[cur ^ 1][tid] = c < g.n ? c / g.L : -1;
-        sh.pad[cur ^ 1][tid] = c < g.n ? (pad_of(a, g, c) ? 1 : 0) : 1;
       }
     }
-    __syncthreads();
   }
   // combine the 4 lane groups that share each row
 #pragma unroll
@@ -462,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
     }
     const int r = rr[mi];
     if (rg == 0 && r < g.n) {
-      const int64_t o = (int64_t)mb * a.n_max + r;
+      const int64_t o = base + r;
       a.lse[o] = (cc > 0) ? mm + __logf(ll) : -INFINITY;
       a.pos[o] = pp;
       a.cnt[o] = cc;
@@ -475,17 +705,26 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
 // ROWS = false: register rows are `in` cols c, image rows are `out` rows r  -> dIn
 // The S^T tile leaves dS in the A-operand lanes of dS . img (k order matched by
 // trp_frag), so no LDS round trip is needed between the two MFMAs.
-template <bool ROWS>
+// dS[r][c] = w_r (exp(S[r][c] / tau - lse_r) - [r == c]) on kept (r, c), computed
+// as 2^(S c1 + shift_r) - w_r [r == c] (shift from cl_shift_k, in a.diag).
+// ROWS: pad columns are zero image rows, so their dS never reaches dOut (with a
+// running shift the exponent is capped at log2 w_r, where every kept dS lies,
+// so it stays finite).
+template <bool ROWS, bool FIXED>
 __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   __shared__ __attribute__((aligned(16))) ClTile sh;
-  const int mb = blockIdx.y;
+  const int bid = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int mb = bid / gridDim.x;
   const Geo g = geo(a, mb);
-  const int x0 = blockIdx.x * CL_ROWS;
+  const int x0 = (bid - mb * gridDim.x) * CL_ROWS;
   if (x0 >= g.n) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, rg = 4 * (lane >> 4);
   const int64_t base = (int64_t)mb * a.n_max;
-  const float it = 1.f / a.tau;
+  const float* shift = a.diag;
+  const float it = 1.f / a.tau, c1 = it * LOG2E;
+  int spec_lo, spec_hi;
+  own_cols(g, x0, spec_lo, spec_hi);
   bf16x8v qf[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
@@ -493,7 +732,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     else reg_frags(qf[mi], lane, g.n, x0 + 32 * w + 16 * mi, [&](int c) { return in_row(a, g, c); });
   }
   // this lane's register row per mi (x = x0 + 32 w + 16 mi + col)
-  float xl_[2], xw[2];
+  float xsh[2], xw[2], xcap[2];
   bool xpad[2];
   int xsq[2], xx[2];
 #pragma unroll
@@ -501,8 +740,9 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     const int x = x0 + 32 * w + 16 * mi + col;
     const bool in = x < g.n;
     xx[mi] = x;
-    xl_[mi] = (ROWS && in) ? a.lse[base + x] : 0.f;
     xw[mi] = (ROWS && in) ? a.w[base + x] : 0.f;
+    xsh[mi] = (ROWS && in) ? shift[base + x] : -INFINITY;
+    xcap[mi] = xw[mi] != 0.f ? __log2f(xw[mi]) : -INFINITY;
     xpad[mi] = in ? (ROWS ? false : pad_of(a, g, x)) : true;
     xsq[mi] = in ? x / g.L : -2;
   }
@@ -511,63 +751,92 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int i = 0; i < 8; ++i) dacc[mi][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto img_row = [&](int i) { return ROWS ? in_row(a, g, i) : out_row(a, g, i); };
-  auto meta = [&](int buf, int y) {
-    const bool in = y < g.n;
-    const int t = y & 63;
-    sh.seq[buf][t] = in ? y / g.L : -1;
-    sh.pad[buf][t] = in ? (pad_of(a, g, y) ? 1 : 0) : 1;
-    sh.lse[buf][t] = (!ROWS && in) ? a.lse[base + y] : 0.f;
-    sh.w[buf][t] = (!ROWS && in) ? a.w[base + y] : 0.f;
-  };
   const int ntile = (g.n + 63) / 64;
-  u32x4 pf[4];
-  cl_fetch(pf, tid, g.n, img_row);
-  cl_store(sh.img[0], tid, pf);
-  if (tid < 64) meta(0, tid);
-  __syncthreads();
+  // ROWS: 4 image DMAs per wave and tile; COLS: + shift and weight of the image rows
+  auto stage = [&](int t) {
+    const int buf = t % CL_NBUF, y0 = t * 64;
+    if (ROWS) {
+      stage_img(sh.img[buf], w, lane, g.n - y0, [&](int i) { return in_row(a, g, y0 + i); });
+    } else {
+      stage_img(sh.img[buf], w, lane, g.n - y0, [&](int i) { return out_row(a, g, y0 + i); });
+      glds4(shift + base + y0 + lane, sh.m0[buf][w]);
+      glds4(a.w + base + y0 + lane, sh.m1[buf][w]);
+    }
+  };
+  retire_loads();
+  stage(0);
+  if (ntile > 1) stage(1);
   for (int tI = 0; tI < ntile; ++tI) {
-    const int cur = tI & 1, y0 = tI * 64;
-    const bool more = tI + 1 < ntile;
-    if (more) cl_fetch(pf, tid, g.n - y0 - 64, [&](int i) { return img_row(y0 + 64 + i); });
+    const int cur = tI % CL_NBUF, y0 = tI * 64;
+    if (tI + 1 < ntile) {
+      if (ROWS) wait_vm<4>();
+      else wait_vm<6>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (tI + 2 < ntile) stage(tI + 2);
     const unsigned char* img = sh.img[cur];
     f32x4 acc[2][4];
     st_tile(acc, qf, img, lane);
+    const bool special = !FIXED || (y0 < spec_hi && y0 + 64 > spec_lo);
     // dS in place: acc[mi][yb][j] <- dS[x][y],  y = y0 + yb*16 + rg + j
+    if (!special) {
+      if (ROWS) {
 #pragma unroll
-    for (int yb = 0; yb < 4; ++yb)
+        for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int yl = yb * 16 + rg + j, y = y0 + yl;
-        const bool ypad = sh.pad[cur][yl];
-        const int ysq = sh.seq[cur][yl];
-        const float ylse = sh.lse[cur][yl], yw = sh.w[cur][yl];
+          for (int yb = 0; yb < 4; ++yb)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const int x = xx[mi];
-          float ds = 0.f;
-          if (ROWS) {
-            const bool ok = !ypad && (ysq != xsq[mi] || x == y) && xw[mi] != 0.f;
-            if (ok) ds = xw[mi] * (__expf(acc[mi][yb][j] * it - xl_[mi]) - (x == y ? 1.f : 0.f));
-          } else {
-            const bool ok = !xpad[mi] && (ysq != xsq[mi] || x == y) && yw != 0.f;
-            if (ok) ds = yw * (__expf(acc[mi][yb][j] * it - ylse) - (x == y ? 1.f : 0.f));
-          }
-          acc[mi][yb][j] = ds;
-        }
+            for (int j = 0; j < 4; ++j)
+              acc[mi][yb][j] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, xsh[mi]));
+      } else {
+        float ysh[4][4];
+        col_vals(ysh, sh.m0[cur][w], rg);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int yb = 0; yb < 4; ++yb)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[mi][yb][j] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, ysh[yb][j]));
       }
+    } else {
+#pragma unroll
+      for (int yb = 0; yb < 4; ++yb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int yl = yb * 16 + rg + j, y = y0 + yl;
+          const int ysq = y < g.n ? y / g.L : -1;
+          const float ysh = ROWS ? 0.f : sh.m0[cur][w][yl], yw = ROWS ? 0.f : sh.m1[cur][w][yl];
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi) {
+            const int x = xx[mi];
+            float ds = 0.f;
+            const bool keep = (ysq != xsq[mi] || x == y);
+            if (ROWS) {
+              if (keep && xw[mi] != 0.f) {
+                float t = __builtin_fmaf(acc[mi][yb][j], c1, xsh[mi]);
+                if (!FIXED) t = fminf(t, xcap[mi]);
+                ds = __builtin_amdgcn_exp2f(t) - (x == y ? xw[mi] : 0.f);
+              }
+            } else {
+              if (!xpad[mi] && keep && yw != 0.f)
+                ds = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, ysh)) - (x == y ? yw : 0.f);
+            }
+            acc[mi][yb][j] = ds;
+          }
+        }
+    }
     // dacc[32 x 128] += dS[32 x 64] . img[64 x 128]   (k = y, in trp_frag order)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8v af[2];
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
-        s16x8 h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          h[i] = (short)f2bf(acc[mi][2 * ks][i]);
-          h[4 + i] = (short)f2bf(acc[mi][2 * ks + 1][i]);
-        }
+        const f32x4& p = acc[mi][2 * ks];
+        const f32x4& q = acc[mi][2 * ks + 1];
+        const u32x4 h = {pk_bf16(p[0], p[1]), pk_bf16(p[2], p[3]), pk_bf16(q[0], q[1]), pk_bf16(q[2], q[3])};
         af[mi] = __builtin_bit_cast(bf16x8v, h);
       }
 #pragma unroll
@@ -578,13 +847,9 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
           dacc[mi][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr, dacc[mi][nd], 0, 0, 0);
       }
     }
-    if (more) {
-      cl_store(sh.img[cur ^ 1], tid, pf);
-      if (tid < 64) meta(cur ^ 1, y0 + 64 + tid);
-    }
-    __syncthreads();
   }
   // write: dacc[mi][nd][j] = d[x = x0 + 32 w + 16 mi + rg + j][e = nd*16 + col]
+  // (COLS: pad `in` rows get no gradient; their dacc is not written)
   const float gs = (a.gscale ? *a.gscale : 1.f) * it;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -593,6 +858,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
       const int x = x0 + 32 * w + 16 * mi + rg + j;
       if (x >= g.n) continue;
       const int b = x / g.L, t = x - (x / g.L) * g.L;
+      if (!ROWS && pad_of(a, g, x)) continue;
       float* dst = ROWS ? a.d_out + (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE
                         : a.d_in + ((g.b0 + b) * a.T + t + g.off) * DE;
 #pragma unroll
@@ -626,16 +892,46 @@ static int cl_check(const lthm_contrastive_desc* d) {
   return 0;
 }
 
+template <typename TX>
+static void launch_rownorm(const TX* x, int64_t rows, int D, bf16_t* out, float* norms, const uint8_t* mask,
+                           int64_t mgroup, int64_t mstride, hipStream_t s) {
+  if (D % 8 == 0) {
+    const int grid = grid_for(rows, 16, 256 * 8);
+    if (D <= 128)
+      hipLaunchKernelGGL((rownorm_v8_k<TX, 1>), dim3(grid), dim3(256), 0, s, x, rows, D, out, norms, mask, mgroup, mstride);
+    else
+      hipLaunchKernelGGL((rownorm_v8_k<TX, 2>), dim3(grid), dim3(256), 0, s, x, rows, D, out, norms, mask, mgroup, mstride);
+  } else {
+    hipLaunchKernelGGL((rownorm_k<TX>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, x, rows, D, out, norms,
+                       mask, mgroup, mstride);
+  }
+}
+
+template <typename TX>
+static void launch_rownorm_bwd(const TX* x, const float* norms, const float* g, int64_t rows, int D, bf16_t* dx_bf,
+                               float* dx_f, hipStream_t s) {
+  if (D % 8 == 0) {
+    const int grid = grid_for(rows, 16, 256 * 8);
+    if (D <= 128)
+      hipLaunchKernelGGL((rownorm_bwd_v8_k<TX, 1>), dim3(grid), dim3(256), 0, s, x, norms, g, rows, D, dx_bf, dx_f);
+    else
+      hipLaunchKernelGGL((rownorm_bwd_v8_k<TX, 2>), dim3(grid), dim3(256), 0, s, x, norms, g, rows, D, dx_bf, dx_f);
+  } else {
+    hipLaunchKernelGGL((rownorm_bwd_k<TX>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, x, norms, g, rows, D,
+                       dx_bf, dx_f);
+  }
+}
+
 extern "C" int lthm_rownorm(const void* x, int32_t x_dtype, int64_t rows, int32_t D, void* out_bf16, float* norms,
-                            void* stream) {
+                            const uint8_t* row_mask, int64_t mask_group, int64_t mask_stride, void* stream) {
   LTHM_REQUIRE(rows >= 0 && D > 0 && D <= 256);
+  LTHM_REQUIRE(!row_mask || (mask_group > 0 && mask_stride >= mask_group));
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for(rows, 4, 256 * 8);
   if (x_dtype == LTHM_BF16)
-    hipLaunchKernelGGL((rownorm_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, rows, D, (bf16_t*)out_bf16, norms);
+    launch_rownorm((const bf16_t*)x, rows, D, (bf16_t*)out_bf16, norms, row_mask, mask_group, mask_stride, s);
   else
-    hipLaunchKernelGGL((rownorm_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, rows, D, (bf16_t*)out_bf16, norms);
+    launch_rownorm((const float*)x, rows, D, (bf16_t*)out_bf16, norms, row_mask, mask_group, mask_stride, s);
   LTHM_CHECK_LAUNCH();
   return 0;
 }
@@ -645,13 +941,10 @@ extern "C" int lthm_rownorm_bwd(const void* x, int32_t x_dtype, const float* nor
   LTHM_REQUIRE(rows >= 0 && D > 0 && D <= 256);
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for(rows, 4, 256 * 8);
   if (x_dtype == LTHM_BF16)
-    hipLaunchKernelGGL((rownorm_bwd_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, norms, g, rows, D,
-                       (bf16_t*)dx_bf16, dx_f32);
+    launch_rownorm_bwd((const bf16_t*)x, norms, g, rows, D, (bf16_t*)dx_bf16, dx_f32, s);
   else
-    hipLaunchKernelGGL((rownorm_bwd_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, norms, g, rows, D,
-                       (bf16_t*)dx_bf16, dx_f32);
+    launch_rownorm_bwd((const float*)x, norms, g, rows, D, (bf16_t*)dx_bf16, dx_f32, s);
   LTHM_CHECK_LAUNCH();
   return 0;
 }
@@ -675,13 +968,21 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
 }
 
 extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream) {
-  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->d_out && d->d_in);
+  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->diag && d->d_out && d->d_in);
   ClArgs a = cl_args(d);
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
-  hipLaunchKernelGGL((cl_bwd_k<true>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb), dim3(256), 0, s, a, d->diag);
   LTHM_CHECK_LAUNCH();
-  hipLaunchKernelGGL((cl_bwd_k<false>), grid, dim3(256), 0, s, a);
+  dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
+  if (2.f / d->tau <= 80.f) {
+    hipLaunchKernelGGL((cl_bwd_k<true, true>), grid, dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((cl_bwd_k<false, true>), grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((cl_bwd_k<true, false>), grid, dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((cl_bwd_k<false, false>), grid, dim3(256), 0, s, a);
+  }
   LTHM_CHECK_LAUNCH();
   return 0;
 }

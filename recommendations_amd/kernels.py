@@ -444,11 +444,19 @@ def small_table_bwd(rows, dY, R, out=None):
     return out
 
 
-def rownorm(x2d):
+def rownorm(x2d, row_mask=None):
+    """F.normalize rows -> (bf16 rows, f32 norms).  ``row_mask`` (uint8 [G, >= rows / G],
+    any row stride): rows r with row_mask[r // G, r % G] set get a zero output row."""
     rows, D = x2d.shape
     out = torch.empty((rows, D), dtype=torch.bfloat16, device=x2d.device)
     norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
-    call("lthm_rownorm", ptr(x2d), dcode(x2d), rows, D, ptr(out), ptr(norms), stream())
+    mg = ms = 0
+    if row_mask is not None:
+        _check(row_mask.dtype == torch.uint8 and row_mask.dim() == 2 and row_mask.stride(1) == 1,
+               "row_mask must be uint8 [G, n] with unit column stride")
+        mg, ms = row_mask.shape[1], row_mask.stride(0)
+        _check(mg > 0 and rows % mg == 0 and rows // mg <= row_mask.shape[0], "row_mask shape does not cover the rows")
+    call("lthm_rownorm", ptr(x2d), dcode(x2d), rows, D, ptr(out), ptr(norms), ptr(row_mask), mg, ms, stream())
     return out, norms
 
 

@@ -47,7 +47,9 @@ class ContrastiveLossFn(torch.autograd.Function):
         yc = y.contiguous()
         tc = target.contiguous()
         yn, ynorm = K.rownorm(yc.view(-1, De))
-        tn, tnorm = K.rownorm(tc.view(-1, De))
+        # pad positions of `in` are zero rows: every logit against them is excluded
+        # anyway, and the loss kernels then need no per-element pad test
+        tn, tnorm = K.rownorm(tc.view(-1, De), row_mask=mask)
         f32 = dict(dtype=torch.float32, device=dev)
         lse = torch.empty((NH, n_mb, n_max), **f32)
         pos = torch.empty((NH, n_mb, n_max), **f32)
@@ -69,7 +71,7 @@ class ContrastiveLossFn(torch.autograd.Function):
         loss = torch.empty(1, **f32)
         call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
         loss = loss / n_mb
-        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, mask, offsets_dev)
+        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev)
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
         ctx.flops = cfg["flops"]
@@ -87,7 +89,7 @@ class ContrastiveLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dloss):
-        yc, tc, yn, tn, ynorm, tnorm, lse, w, mask, offsets_dev = ctx.saved_tensors
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev = ctx.saved_tensors
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         dev = yc.device
         g = dloss.contiguous().float()
@@ -95,7 +97,7 @@ class ContrastiveLossFn(torch.autograd.Function):
         d_in = K.zeros((B, T, De), torch.float32, dev)
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
-                                        lse[h], None, None, None, None, w[h])
+                                        lse[h], None, None, None, diag[h], w[h])  # diag: shift scratch
             d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
             call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
                  _work=4.0 * ctx.flops[h], _unit="flop")
