@@ -40,16 +40,22 @@ struct GemmArgs {
   int res1_dt, res2_dt;
   int out_dt;
   float* ws;           // split-K slabs [splits][M][N] f32 (when splits > 1)
+  bool fast_ok;        // 16-B aligned operands and leading dims (interior-tile fast path)
 };
 
+// tanh(u) = 1 - 2 / (e^(2u) + 1): one v_exp + one v_rcp (|error| ~ 1e-7 absolute,
+// saturating correctly at +-1 for large |u|)
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.f);
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float kb = 0.7978845608028654f, kk = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(kb * (x + kk * x * x * x)));
+  return 0.5f * x * (1.f + fast_tanh(kb * (x + kk * x * x * x)));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float kb = 0.7978845608028654f, kk = 0.044715f;
   const float x2 = x * x;
-  const float t = tanhf(kb * (x + kk * x2 * x));
+  const float t = fast_tanh(kb * (x + kk * x2 * x));
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kb * (1.f + 3.f * kk * x2);
 }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
@@ -212,6 +218,24 @@ __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t 
   }
 }
 
+// interior tiles (whole tile inside the operand, K % 64 == 0): per-thread chunk
+// pointers are computed once per tile and advanced by one K-tile per step, no
+// bounds tests
+template <bool KCONTIG>
+__device__ __forceinline__ void chunk_ptrs(const bf16_t* (&p)[4], const bf16_t* __restrict__ P, int64_t ld,
+                                           int64_t r0, int64_t k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 256 * i;
+    if constexpr (KCONTIG) p[i] = P + (r0 + (idx >> 3)) * ld + k0 + (idx & 7) * 8;
+    else p[i] = P + (k0 + (idx >> 4)) * ld + r0 + (idx & 15) * 8;
+  }
+}
+__device__ __forceinline__ void load_fast(const bf16_t* const (&p)[4], int64_t off, u32x4 (&reg)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) reg[i] = *reinterpret_cast<const u32x4*>(p[i] + off);
+}
+
 template <bool KCONTIG>
 __device__ __forceinline__ void store_tile(unsigned char* lds, int tid, const u32x4 (&reg)[4]) {
 #pragma unroll
@@ -251,7 +275,9 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs g, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile = blockIdx.x;
+  // XCD-aware order: the tiles_n column tiles of one row panel land on one XCD, so
+  // the panel of A is fetched from HBM once and re-read from that XCD's L2
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
   const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
   const int64_t b = blockIdx.y;
@@ -268,19 +294,41 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs g, int tiles_n) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[4], rb[4];
+  // interior fast path: 16-B aligned chunks everywhere, no tails
+  const bool fast = (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((k1 - k0) % BK == 0) && g.fast_ok;
+  const bf16_t* pa[4];
+  const bf16_t* pb[4];
+  if (fast) {
+    chunk_ptrs<KA>(pa, A, g.lda, m0, k0, tid);
+    chunk_ptrs<KB>(pb, B, g.ldb, n0, k0, tid);
+  }
+  const int64_t sta = KA ? BK : BK * g.lda, stb = KB ? BK : BK * g.ldb;  // elements per K-tile
   if (k0 < k1) {
-    load_tile<KA>(A, g.lda, g.M, m0, k0, k1, tid, ra);
-    load_tile<KB>(B, g.ldb, g.N, n0, k0, k1, tid, rb);
+    if (fast) {
+      load_fast(pa, 0, ra);
+      load_fast(pb, 0, rb);
+    } else {
+      load_tile<KA>(A, g.lda, g.M, m0, k0, k1, tid, ra);
+      load_tile<KB>(B, g.ldb, g.N, n0, k0, k1, tid, rb);
+    }
     store_tile<KA>(smem, tid, ra);
     store_tile<KB>(smem + TILE_BYTES, tid, rb);
   }
   __syncthreads();
   int cur = 0;
+  int64_t oa = 0, ob = 0;
   for (int64_t kt = k0; kt < k1; kt += BK) {
     const bool has_next = kt + BK < k1;
     if (has_next) {
-      load_tile<KA>(A, g.lda, g.M, m0, kt + BK, k1, tid, ra);
-      load_tile<KB>(B, g.ldb, g.N, n0, kt + BK, k1, tid, rb);
+      if (fast) {
+        oa += sta;
+        ob += stb;
+        load_fast(pa, oa, ra);
+        load_fast(pb, ob, rb);
+      } else {
+        load_tile<KA>(A, g.lda, g.M, m0, kt + BK, k1, tid, ra);
+        load_tile<KB>(B, g.ldb, g.N, n0, kt + BK, k1, tid, rb);
+      }
     }
     const unsigned char* sa = smem + cur * 2 * TILE_BYTES;
     const unsigned char* sb = sa + TILE_BYTES;
@@ -388,12 +436,14 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   g.res1 = d->res1; g.res2 = d->res2; g.ldr1 = d->ldr1 > 0 ? d->ldr1 : d->N; g.ldr2 = d->ldr2 > 0 ? d->ldr2 : d->N;
   g.res1_dt = d->res1_dtype; g.res2_dt = d->res2_dtype; g.out_dt = d->out_dtype;
   g.ws = (splits > 1) ? d->workspace : nullptr;
+  g.fast_ok = ((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0 && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
+              d->sA % 8 == 0 && d->sB % 8 == 0;
   if (splits > 1) {
     LTHM_REQUIRE(d->workspace_bytes >= (size_t)splits * d->batch * d->M * d->N * 4);
   }
   const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
-  dim3 grid(tiles_m * tiles_n, d->batch, splits);
   hipStream_t s = (hipStream_t)stream;
+  dim3 grid(tiles_m * tiles_n, d->batch, splits);
   const size_t shmem = 4 * TILE_BYTES;
   if (ka && kb) hipLaunchKernelGGL((gemm_k<true, true>), grid, dim3(256), shmem, s, g, tiles_n);
   else if (ka && !kb) hipLaunchKernelGGL((gemm_k<true, false>), grid, dim3(256), shmem, s, g, tiles_n);

@@ -33,9 +33,20 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 
 constexpr int DE = 128;  // product_emb_dim (model/lthm.yaml:22)
 
-__device__ __forceinline__ int ks_off256(int row, int ch) {
-  return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+// 256-B rows of 16 x 16-B chunks, chunk ch of row r at slot ch ^ swz(r), swz a
+// permutation of row & 15 chosen (by exhaustive search) so that both read
+// patterns are bank-conflict-free under gfx950's lane groups
+// (MI355X_MICROARCH.md, LDS table):
+//  * row fragments, ds_read_b128: lane l reads row l & 15, chunk c + (l >> 4);
+//    groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32) need 16 distinct slots;
+//  * transposed fragments, ds_read_b64_tr_b16: lanes 0-31 read rows 0-7 (32-63:
+//    rows 8-15) x one 32-B chunk pair, so swz >> 1 must differ within each 8 rows.
+// swz = 0 2 4 6 8 10 12 14 | 9 11 13 15 1 3 5 7
+__device__ __forceinline__ int swz(int row) {
+  const int h = (row >> 3) & 1;
+  return ((((row & 7) << 1) + (h << 3)) & 15) | h;
 }
+__device__ __forceinline__ int ks_off256(int row, int ch) { return row * 256 + ((ch ^ swz(row)) << 4); }
 
 // ---------------------------------------------------------------- row normalisation
 // out[r] = bf16(x[r] / max(|x[r]|, 1e-12)), norms[r] = |x[r]|   (F.normalize, wrapper.py:118-119)
@@ -242,18 +253,6 @@ __device__ __forceinline__ bool pad_of(const ClArgs& a, const Geo& g, int c) {
 
 __device__ __forceinline__ bf16x8v row_frag(const unsigned char* img, int row, int chunk) {
   return __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ks_off256(row, chunk)));
-}
-// transposed (k = image row) fragment: B[k = kb + 8*(lane>>4) + j][n = nb + (lane&15)]
-__device__ __forceinline__ bf16x8v tr_frag(const unsigned char* img, int kb, int nb, int lane) {
-  const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int kr = kb + 8 * gq + q;
-  const int ch = (nb >> 3) + (p >> 1);
-  const unsigned char* a0 = img + ks_off256(kr, ch) + 8 * (p & 1);
-  const unsigned char* a1 = img + ks_off256(kr + 4, ch) + 8 * (p & 1);
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8v, v);
 }
 
 // load this wave's 16 register rows as 4 k32 A fragments
@@ -469,31 +468,69 @@ __device__ __forceinline__ void wait_vm() {
 // prologue, so no first use inside the tile loop drains the DMA ring
 __device__ __forceinline__ void retire_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-// image rows [0, 64) of a tile: wave w stages rows 16w .. 16w + 15 with four
-// DMAs of 4 rows x 256 B; lane l lands at row 4k + l/16, slot l%16 and loads
-// chunk slot ^ swz(row), which puts chunk ch at ks_off256(row, ch)
-template <typename RowFn>
-__device__ __forceinline__ void stage_img(unsigned char* img, int w, int lane, int cnt, RowFn rowp) {
-  const int slot = lane & 15;
+// Image-row staging.  Wave w stages rows 16w .. 16w + 15 of every tile with four
+// DMAs of 4 rows x 256 B; lane l lands at row 16w + 4k + l/16, slot l%16 and so
+// loads chunk slot ^ swz(row), which puts chunk ch at ks_off256(row, ch).  The
+// source row of column c = (b, t) (sequence b of the mini-batch, position t) sits
+// at base + b * sb + t * st elements; the cursor advances (b, t) by 64 columns a
+// tile without a division.
+struct RowCursor {
+  const bf16_t* base;
+  int sb, st, L, q64, r64;
+  int b[4], t[4], choff[4];
+  int c;  // column of this lane's k = 0 row in the next tile to stage
+  __device__ __forceinline__ void init(const bf16_t* base_, int sb_, int st_, int L_, int w, int lane) {
+    base = base_; sb = sb_; st = st_; L = L_;
+    q64 = 64 / L; r64 = 64 - q64 * L;
+    c = 16 * w + (lane >> 4);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int row = 16 * w + 4 * k + (lane >> 4);
-    const int ch = slot ^ (((row & 3) << 2) | ((row >> 2) & 3));
-    const void* src = row < cnt ? (const void*)(rowp(row) + ch * 8) : (const void*)(cl_zero_row + 16 * slot);
-    glds16(src, img + (16 * w + 4 * k) * 256);
+    for (int k = 0; k < 4; ++k) {
+      const int row = c + 4 * k;
+      b[k] = row / L;
+      t[k] = row - b[k] * L;
+      choff[k] = ((lane & 15) ^ swz(row)) * 8;
+    }
   }
-}
+  // stage the next tile into img (the tile's 64-row image), then advance by 64 columns
+  __device__ __forceinline__ void stage(unsigned char* img, int n, int w, int lane) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const void* src = (c + 4 * k < n) ? (const void*)(base + (b[k] * sb + t[k] * st + choff[k]))
+                                        : (const void*)(cl_zero_row + 16 * (lane & 15));
+      glds16(src, img + (16 * w + 4 * k) * 256);
+      t[k] += r64;
+      b[k] += q64;
+      if (t[k] >= L) { t[k] -= L; b[k] += 1; }
+    }
+    c += 64;
+  }
+};
 
 // transposed-k fragment: B[k][n = nb + (lane&15)] with k = 0..3 -> image rows
 // kb + 4(lane>>4) + k and k = 4..7 -> rows kb + 16 + 4(lane>>4) + k-4, i.e. the k
 // order in which a transposed S^T tile's C registers already sit per lane.
-__device__ __forceinline__ bf16x8v trp_frag(const unsigned char* img, int kb, int nb, int lane) {
+// Since swz(row) depends only on row & 15, the byte offset splits into a per-lane
+// part for each 16-column block nd (trp_offsets, loop invariant) plus kb * 256 and
+// 16 * 256 for the upper 4 k, which become ds_read immediates.
+__device__ __forceinline__ void trp_offsets(int (&off)[8], int lane) {
   const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int ch = (nb >> 3) + (p >> 1);
-  const unsigned char* a0 = img + ks_off256(kb + 4 * gq + q, ch) + 8 * (p & 1);
-  const unsigned char* a1 = img + ks_off256(kb + 16 + 4 * gq + q, ch) + 8 * (p & 1);
+  const int row = 4 * gq + q;
+#pragma unroll
+  for (int nd = 0; nd < 8; ++nd) off[nd] = row * 256 + (((2 * nd + (p >> 1)) ^ swz(row)) << 4) + 8 * (p & 1);
+}
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+// per-tile base of column block nd, laundered through an empty asm so the compiler
+// cannot re-associate it with the kb / k offsets (which then fold into ds_read
+// immediates instead of costing two VALU adds per read)
+__device__ __forceinline__ lds_u8* trp_base(const unsigned char* img, int off) {
+  lds_u8* p = (lds_u8*)img + off;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+__device__ __forceinline__ bf16x8v trp_frag(lds_u8* base, int kb) {
+  lds_u8* a0 = base + kb * 256;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0 + 16 * 256));
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8v, v);
 }
@@ -556,7 +593,7 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
   const Geo g = geo(a, mb);
   const int r0 = (bid - mb * gridDim.x) * CL_ROWS;
   if (r0 >= g.n) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, rg = 4 * (lane >> 4);
   const int64_t base = (int64_t)mb * a.n_max;
   bf16x8v qf[2][4];
@@ -581,10 +618,12 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
   }
   const int ntile = (g.n + 63) / 64;
   // 5 DMAs per wave and tile: 4 image pieces + the diag (pad flag) of the tile's columns
+  RowCursor cur_in;
+  cur_in.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
   auto stage = [&](int t) {
-    const int buf = t % CL_NBUF, c0 = t * 64;
-    stage_img(sh.img[buf], w, lane, g.n - c0, [&](int i) { return in_row(a, g, c0 + i); });
-    glds4(a.diag + base + c0 + lane, sh.m0[buf][w]);
+    const int buf = t % CL_NBUF;
+    cur_in.stage(sh.img[buf], g.n, w, lane);
+    glds4(a.diag + base + t * 64 + lane, sh.m0[buf][w]);
   };
   retire_loads();
   stage(0);
@@ -718,7 +757,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   const Geo g = geo(a, mb);
   const int x0 = (bid - mb * gridDim.x) * CL_ROWS;
   if (x0 >= g.n) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, rg = 4 * (lane >> 4);
   const int64_t base = (int64_t)mb * a.n_max;
   const float* shift = a.diag;
@@ -751,14 +790,18 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int i = 0; i < 8; ++i) dacc[mi][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int toff[8];
+  trp_offsets(toff, lane);
   const int ntile = (g.n + 63) / 64;
   // ROWS: 4 image DMAs per wave and tile; COLS: + shift and weight of the image rows
+  RowCursor cur_img;
+  if (ROWS) cur_img.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
+  else cur_img.init(a.out_n + (g.b0 * (a.T + 1) * a.NH + a.head) * DE, (a.T + 1) * a.NH * DE, a.NH * DE, g.L, w,
+                    lane);
   auto stage = [&](int t) {
     const int buf = t % CL_NBUF, y0 = t * 64;
-    if (ROWS) {
-      stage_img(sh.img[buf], w, lane, g.n - y0, [&](int i) { return in_row(a, g, y0 + i); });
-    } else {
-      stage_img(sh.img[buf], w, lane, g.n - y0, [&](int i) { return out_row(a, g, y0 + i); });
+    cur_img.stage(sh.img[buf], g.n, w, lane);
+    if (!ROWS) {
       glds4(shift + base + y0 + lane, sh.m0[buf][w]);
       glds4(a.w + base + y0 + lane, sh.m1[buf][w]);
     }
@@ -829,6 +872,9 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
         }
     }
     // dacc[32 x 128] += dS[32 x 64] . img[64 x 128]   (k = y, in trp_frag order)
+    lds_u8* tb[8];
+#pragma unroll
+    for (int nd = 0; nd < 8; ++nd) tb[nd] = trp_base(img, toff[nd]);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8v af[2];
@@ -841,7 +887,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
       }
 #pragma unroll
       for (int nd = 0; nd < 8; ++nd) {
-        const bf16x8v bfr = trp_frag(img, ks * 32, nd * 16, lane);
+        const bf16x8v bfr = trp_frag(tb[nd], ks * 32);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
           dacc[mi][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr, dacc[mi][nd], 0, 0, 0);
@@ -888,6 +934,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
 static int cl_check(const lthm_contrastive_desc* d) {
   if (!d || d->De != DE || d->B <= 0 || d->T <= 0 || d->mb_size <= 0 || d->n_mb <= 0) return 1;
   if ((int64_t)d->mb_size * d->T > d->n_max || d->n_max > 4096) return 1;
+  if ((int64_t)d->mb_size * (d->T + 1) * d->n_heads * DE >= (1ll << 31)) return 1;  // RowCursor offsets
   if (d->head < 0 || d->head >= d->n_heads) return 1;
   return 0;
 }

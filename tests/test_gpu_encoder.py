@@ -83,6 +83,54 @@ def test_gemm_wgrad_splitk_large(dev):
     assert relerr(out, exp) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,Kd,act", [(65573, 768, 256, 0), (65573, 768, 256, 1), (50001, 200, 72, 2),
+                                         (40000, 1024, 1024, 0)])
+def test_gemm_persistent_nt(dev, M, N, Kd, act):
+    """Shapes with >= 512 tiles take the persistent LDS-DMA kernel (ragged M / N,
+    a partial K-tile, the residual and both activations)."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + N + Kd)
+    A = bf(torch.randn(M, Kd, generator=g))
+    W = bf(torch.randn(N, Kd, generator=g) / math.sqrt(Kd))
+    bias = torch.randn(N, generator=g)
+    res = bf(torch.randn(M, N, generator=g))
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    out = K.linear_fwd(A.to(dev), W.to(dev), bias=bias.to(dev), act=act, aux_out=pre if act else None,
+                       res1=res.to(dev), out_dtype=torch.float32)
+    z = A.float() @ W.float().T + bias
+    exp = {0: z, 1: F.gelu(z, approximate="tanh"), 2: ref.quick_gelu(z)}[act] + res.float()
+    assert relerr(out, exp) < 1e-5
+    if act:
+        assert (pre.float().cpu() - z).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("M,N,Kd", [(70001, 768, 256), (30000, 256, 1024)])
+def test_gemm_persistent_dgrad(dev, M, N, Kd):
+    """dX = dY W (K-strided B) on the persistent kernel, with the GELU-grad epilogue."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + Kd)
+    dy = bf(torch.randn(M, N, generator=g))
+    W = bf(torch.randn(N, Kd, generator=g))
+    pre = bf(torch.randn(M, Kd, generator=g))
+    dx = K.linear_dgrad(dy.to(dev), W.to(dev), out_dtype=torch.float32)
+    ref_dx = dy.float() @ W.float()
+    assert relerr(dx, ref_dx) < 1e-5
+    dxg = K.linear_dgrad(dy.to(dev), W.to(dev), act_grad=K.ACT_GELU_GRAD, aux=pre.to(dev), out_dtype=torch.float32)
+    p = pre.float().requires_grad_(True)
+    F.gelu(p, approximate="tanh").backward(ref_dx)
+    assert relerr(dxg, p.grad) < 1e-5
+
+
+def test_gemm_persistent_batched(dev):
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(11)
+    Bt, M, N, Kd = 3, 20000, 256, 128
+    A = bf(torch.randn(Bt, M, Kd, generator=g))
+    Bm = bf(torch.randn(Bt, N, Kd, generator=g))
+    out = K.gemm(A.to(dev), Bm.to(dev), M, N, Kd, batch=Bt, sA=M * Kd, sB=N * Kd, out_dtype=torch.float32, alpha=0.5)
+    assert relerr(out, 0.5 * A.float() @ Bm.float().transpose(1, 2)) < 1e-5
+
+
 def test_gemm_batched(dev):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(5)

@@ -26,8 +26,9 @@ def timeit(fn, iters=20):
 def main():
     dev = torch.device("cuda")
     M = 4096 * 129
-    shapes = [("qkv", M, 768, 256), ("proj", M, 256, 256), ("fc", M, 1024, 256), ("fc2", M, 256, 1024),
-              ("sq4096", 4096, 4096, 4096)]
+    shapes = [("qkv", M, 768, 256), ("proj", M, 256, 256), ("fc", M, 1024, 256), ("fc2", M, 256, 1024)]
+    if os.environ.get("GEMM_BENCH_SQUARE"):
+        shapes.append(("sq4096", 4096, 4096, 4096))
     for name, m, n, k in shapes:
         a = torch.randn(m, k, device=dev).to(torch.bfloat16)
         w = torch.randn(n, k, device=dev).to(torch.bfloat16)
@@ -39,7 +40,9 @@ def main():
         t3 = timeit(lambda: K.linear_dgrad(dy, w))
         t4 = timeit(lambda: K.linear_wgrad(dy, a), iters=5)
         t5 = timeit(lambda: torch.matmul(dy.T, a), iters=5)
-        print(f"{name:7s} M={m} N={n} K={k}: fwd {t0:.3f} ms ({fl / t0 / 1e9:.0f} TF)  +gelu {t1:.3f}  "
+        byts = 2.0 * (m * k + n * k + m * n)  # bf16 A + W + C, each once
+        print(f"{name:7s} M={m} N={n} K={k}: fwd {t0:.3f} ms ({fl / t0 / 1e9:.0f} TF, "
+              f"{byts / t0 / 1e6:.0f} GB/s)  +gelu {t1:.3f}  "
               f"hipblaslt {t2:.3f} ({fl / t2 / 1e9:.0f} TF) | dgrad {t3:.3f} ({fl / t3 / 1e9:.0f} TF) | "
               f"wgrad {t4:.3f} ({fl / t4 / 1e9:.0f} TF) hipblaslt {t5:.3f}", flush=True)
 
