@@ -85,8 +85,8 @@ def test_gemm_wgrad_splitk_large(dev):
 
 @pytest.mark.parametrize("M,N,Kd,act", [(65573, 768, 256, 0), (65573, 768, 256, 1), (50001, 200, 72, 2),
                                          (40000, 1024, 1024, 0)])
-def test_gemm_persistent_nt(dev, M, N, Kd, act):
-    """Shapes with >= 512 tiles take the persistent LDS-DMA kernel (ragged M / N,
+def test_gemm_large_nt(dev, M, N, Kd, act):
+    """Step-sized shapes (thousands of tiles: interior fast path + ragged edge tiles,
     a partial K-tile, the residual and both activations)."""
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(M + N + Kd)
@@ -105,8 +105,8 @@ def test_gemm_persistent_nt(dev, M, N, Kd, act):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(70001, 768, 256), (30000, 256, 1024)])
-def test_gemm_persistent_dgrad(dev, M, N, Kd):
-    """dX = dY W (K-strided B) on the persistent kernel, with the GELU-grad epilogue."""
+def test_gemm_large_dgrad(dev, M, N, Kd):
+    """dX = dY W (K-strided B) at step size, with the GELU-grad epilogue."""
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(M + Kd)
     dy = bf(torch.randn(M, N, generator=g))
@@ -121,7 +121,7 @@ def test_gemm_persistent_dgrad(dev, M, N, Kd):
     assert relerr(dxg, p.grad) < 1e-5
 
 
-def test_gemm_persistent_batched(dev):
+def test_gemm_large_batched(dev):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(11)
     Bt, M, N, Kd = 3, 20000, 256, 128
