@@ -26,14 +26,17 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 // ---- bf16 <-> f32 (round-to-nearest-even, NaN stays NaN; identical to torch) ----
+// f32 -> bf16 is gfx950's v_cvt_pk_bf16_f32 (RNE, two values per instruction).
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float f32x2_hw __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_hw{lo, hi}, bf16x2_hw));
+}
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  return (bf16_t)(pack_bf16x2(f, 0.f) & 0xffffu);
 }
 
 // generic element load/store as f32
@@ -108,12 +111,12 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
     if constexpr (N == 8) {
       u32x4 w;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+      for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
       *reinterpret_cast<u32x4*>(p) = w;
     } else if constexpr (N == 4) {
       u32x2 w;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+      for (int i = 0; i < 2; ++i) w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
       *reinterpret_cast<u32x2*>(p) = w;
     } else {
 #pragma unroll
@@ -169,6 +172,36 @@ __device__ __host__ __forceinline__ int64_t pymod64(int64_t a, int64_t b) {
   if (r != 0 && ((r < 0) != (b < 0))) r += b;
   return r;
 }
+
+// ---- LDS-DMA (global_load_lds_dwordx4) ----
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// LDS-DMA issued as asm: the compiler neither counts these loads nor guards LDS
+// reads against them (the builtin makes it drain vmcnt(0) before unrelated LDS
+// reads); the kernels retire them with explicit counted waits + a barrier.
+// Ordinary loads stay correct: in-order vmcnt only makes their waits stricter.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)p);
+}
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// retire every ordinary load issued so far, visibly to the compiler's own wait
+// bookkeeping (vmcnt(0), expcnt / lgkmcnt untouched): issued before the DMA
+// prologue, so no first use inside the tile loop drains the DMA ring
+__device__ __forceinline__ void retire_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __host__ __forceinline__ int grid_for(int64_t work, int per_block, int cap = 256 * 16) {
   int64_t g = (work + per_block - 1) / per_block;

@@ -43,20 +43,21 @@ struct GemmArgs {
   bool fast_ok;        // 16-B aligned operands and leading dims (interior-tile fast path)
 };
 
-// tanh(u) = 1 - 2 / (e^(2u) + 1): one v_exp + one v_rcp (|error| ~ 1e-7 absolute,
-// saturating correctly at +-1 for large |u|)
-__device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.f);
+// tanh-GELU through r = 1 / (e^(2u) + 1), u = sqrt(2/pi) (x + 0.044715 x^3):
+// tanh(u) = 1 - 2r, so gelu(x) = 0.5 x (1 + tanh u) = x (1 - r) and
+// gelu'(x) = (1 - r) (1 + 2 sqrt(2/pi) x r (1 + 3 * 0.044715 x^2)).
+// One v_exp + one v_rcp per element (|error| ~ 1e-7 absolute); saturates
+// correctly for large |x| (exp2 -> inf gives r = 0, exp2 -> 0 gives r = 1).
+__device__ __forceinline__ float gelu_r(float x) {
+  constexpr float kb2 = 2.f * 1.4426950408889634f * 0.7978845608028654f;   // 2 log2(e) sqrt(2/pi)
+  constexpr float kk2 = kb2 * 0.044715f;
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * __builtin_fmaf(kk2, x * x, kb2)) + 1.f);
 }
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float kb = 0.7978845608028654f, kk = 0.044715f;
-  return 0.5f * x * (1.f + fast_tanh(kb * (x + kk * x * x * x)));
-}
+__device__ __forceinline__ float gelu_tanh(float x) { return __builtin_fmaf(-x, gelu_r(x), x); }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float kb = 0.7978845608028654f, kk = 0.044715f;
-  const float x2 = x * x;
-  const float t = fast_tanh(kb * (x + kk * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kb * (1.f + 3.f * kk * x2);
+  constexpr float kb = 0.7978845608028654f, k3 = 3.f * 0.044715f;
+  const float r = gelu_r(x);
+  return (1.f - r) * __builtin_fmaf(2.f * kb * x * r, __builtin_fmaf(k3, x * x, 1.f), 1.f);
 }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 __device__ __forceinline__ float qgelu(float x) { return x * sigmoidf_(1.702f * x); }
@@ -402,9 +403,291 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs g, int splits, i
   }
 }
 
+// ---------------------------------------------------------------- persistent ring GEMM
+// The encoder's forward / dgrad GEMMs are tall and skinny (M = B*T' = 528k rows,
+// N <= 1024, K 256..1024): HBM-bound on the A stream and the C writes, and with
+// only K/64 = 4 K-tiles per output tile the one-tile-at-a-time kernel above spends
+// most of a tile's life waiting on the load latency of its first K-tile and on its
+// epilogue.  This kernel keeps the A stream in flight across tile boundaries:
+//
+//  * one workgroup per CU, persistent: 4 compute waves (2x2, 64x64 each) and 4
+//    loader waves that only issue LDS-DMA (global_load_lds_dwordx4) into a 4-deep
+//    ring of 64-k stages; a stage is retired by a counted `s_waitcnt vmcnt` in the
+//    loaders + a raw s_barrier, so three stages stay in flight behind the MFMAs and
+//    behind the previous tile's epilogue;
+//  * each workgroup owns ONE 128-column tile of C for the whole launch and walks
+//    row panels: with K <= 256 its B slab (128 x K, <= 64 KiB) is loaded into LDS
+//    once (BRES), otherwise B k-tiles ride the ring with A;
+//  * XCD-aware: workgroup w runs on XCD w % 8; the tiles_n column owners of one
+//    XCD walk the same row panels (p = xcd + 8 (r + R i)) in step, so each A panel
+//    is fetched from HBM once and re-read from that XCD's L2;
+//  * the epilogue is per wave (no block barrier) and compiled per form (EPI): the
+//    bias is held in registers for the whole launch, the residual / pre-activation
+//    loads of a 16-row slice are issued one slice ahead, so the in-order vmcnt
+//    never waits on this wave's own earlier C stores; slices of the wave's 64x64
+//    accumulator are restaged through a wave-private LDS strip and finished 8
+//    columns per lane with 16-B loads / stores.
+// Requires: A K-contiguous, K % 64 == 0, batch 1, no split-K, 16-B aligned
+// operands, leading dims % 8 == 0, N % 8 == 0.
+constexpr int PS_NST = 4;
+constexpr int PS_LD = 68;  // staging row pitch (floats): conflict-free C-layout writes
+constexpr int PS_NLW = 4;  // loader waves
+constexpr int PS_THREADS = 64 * (4 + PS_NLW);
+// epilogue forms
+constexpr int EPI_PLAIN = 0;  // (+ bias)
+constexpr int EPI_ACT = 1;    // (+ bias), GELU / QuickGELU, optional pre-activation store
+constexpr int EPI_GRAD = 2;   // * act'(aux)
+constexpr int EPI_RES1 = 3;   // (+ bias) + res1 (f32)
+constexpr int EPI_RES2 = 4;   // (+ bias) + res1 + res2 (f32)
+__device__ __attribute__((aligned(16))) unsigned char gemm_zero16[16];
+
+template <bool BRES>
+struct PsSmem {
+  unsigned char ring[PS_NST][BRES ? TILE_BYTES : 2 * TILE_BYTES];
+  unsigned char bslab[BRES ? 4 : 1][BRES ? TILE_BYTES : 16];
+  float stg[4][16 * PS_LD];
+};
+
+// DMA pieces [d0, d0 + ND) (1 KiB each) of a 128 x 64 k-tile of a K-contiguous operand
+template <int ND>
+__device__ __forceinline__ void ps_dma_kc(unsigned char* img, const bf16_t* P, int64_t ld, int64_t rows, int64_t r0,
+                                          int64_t k, int lane, int d0) {
+#pragma unroll
+  for (int d = d0; d < d0 + ND; ++d) {
+    const int row = 8 * d + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);  // lane-linear slot -> kc_off swizzle
+    const int64_t gr = r0 + row;
+    const void* src = gr < rows ? (const void*)(P + gr * ld + k + ch * 8) : (const void*)gemm_zero16;
+    glds16(src, img + d * 1024);
+  }
+}
+// ... of a K-strided operand [64 k][128 cols] (256-B rows, ks_off swizzle)
+template <int ND>
+__device__ __forceinline__ void ps_dma_ks(unsigned char* img, const bf16_t* P, int64_t ld, int64_t cols, int64_t c0,
+                                          int64_t k, int lane, int d0) {
+#pragma unroll
+  for (int d = d0; d < d0 + ND; ++d) {
+    const int kr = 4 * d + (lane >> 4);
+    const int ch = (lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+    const int64_t gc = c0 + ch * 8;
+    const void* src = gc < cols ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
+    glds16(src, img + d * 1024);
+  }
+}
+
+// epilogue inputs of one 16-row slice (the lane's 2 chunks of 8 columns)
+template <int EPI>
+struct PsIn {
+  float x[EPI == EPI_GRAD || EPI == EPI_RES1 || EPI == EPI_RES2 ? 2 : 1][8];
+  float y[EPI == EPI_RES2 ? 2 : 1][8];
+};
+template <int EPI>
+__device__ __forceinline__ void ps_epi_load(const GemmArgs& g, PsIn<EPI>& in, int64_t r0, int64_t col0) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t row = min(r0 + 8 * u, g.M - 1);  // clamped: the store is predicated
+    if constexpr (EPI == EPI_GRAD) load_vec<bf16_t, 16>(g.aux + row * g.ldaux + col0, in.x[u]);
+    if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
+      const float* p = reinterpret_cast<const float*>(g.res1) + row * g.ldr1 + col0;
+      load_vec<float, 16>(p, in.x[u]);
+      load_vec<float, 16>(p + 4, in.x[u] + 4);
+    }
+    if constexpr (EPI == EPI_RES2) {
+      const float* p = reinterpret_cast<const float*>(g.res2) + row * g.ldr2 + col0;
+      load_vec<float, 16>(p, in.y[u]);
+      load_vec<float, 16>(p + 4, in.y[u] + 4);
+    }
+  }
+}
+
+template <bool KB, bool BRES, int EPI>
+__global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles_m, int tiles_n, int R) {
+  __shared__ __attribute__((aligned(16))) PsSmem<BRES> sh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int nt = jj % tiles_n, r = jj / tiles_n;
+  const int64_t n0 = (int64_t)nt * BN;
+  const int NK = (int)(g.K / BK);
+  const int first = xcd + 8 * r;
+  const int ntile = first < tiles_m ? (tiles_m - 1 - first) / (8 * R) + 1 : 0;
+  const int S = ntile * NK;
+  if (S == 0) return;  // uniform over the workgroup
+  const bool loader = wave >= 4;
+
+  if constexpr (BRES) {  // the workgroup's B slab, once
+    if (!loader) {
+      u32x4 rb[4];
+      for (int kk = 0; kk < NK; ++kk) {
+        load_tile<KB>(g.B, g.ldb, g.N, n0, (int64_t)kk * BK, g.K, tid, rb);
+        store_tile<KB>(sh.bslab[kk], tid, rb);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (loader) {
+    // loader waves: each stages a quarter of A's (and B's, BRES off) 16 1-KiB pieces
+    constexpr int ND = 16 / PS_NLW;
+    constexpr int DPS = (BRES ? 1 : 2) * ND;  // DMAs per stage and loader wave
+    const int d0 = (wave - 4) * ND;
+    auto issue = [&](int s) {
+      const int i = s / NK, kk = s - i * NK;
+      const int64_t m0 = (int64_t)(first + 8 * R * i) * BM;
+      unsigned char* st = sh.ring[s % PS_NST];
+      ps_dma_kc<ND>(st, g.A, g.lda, g.M, m0, (int64_t)kk * BK, lane, d0);
+      if constexpr (!BRES) {
+        if constexpr (KB) ps_dma_kc<ND>(st + TILE_BYTES, g.B, g.ldb, g.N, n0, (int64_t)kk * BK, lane, d0);
+        else ps_dma_ks<ND>(st + TILE_BYTES, g.B, g.ldb, g.N, n0, (int64_t)kk * BK, lane, d0);
+      }
+    };
+    retire_loads();
+    for (int s = 0; s < PS_NST && s < S; ++s) issue(s);
+    for (int s = 0; s < S; ++s) {
+      // stages issued so far: 0 .. min(S-1, s == 0 ? NST-1 : s+NST-2); step s must have landed
+      const int behind = min(S - 1, s == 0 ? PS_NST - 1 : s + PS_NST - 2) - s;
+      if (behind >= 3) wait_vm<3 * DPS>();
+      else if (behind == 2) wait_vm<2 * DPS>();
+      else if (behind == 1) wait_vm<DPS>();
+      else wait_vm<0>();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s >= 1 && s + PS_NST - 1 < S) issue(s + PS_NST - 1);  // into the stage step s-1 freed
+    }
+    return;
+  }
+
+  // ---------------- compute waves
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t col0 = n0 + wn * 64 + (lane & 7) * 8;  // this lane's 8 epilogue columns (fixed)
+  const int64_t colc = col0 < g.N ? col0 : 0;           // clamped for loads
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+  if (g.bias && EPI != EPI_GRAD) load_vec<float, 16>(g.bias + colc, bias), load_vec<float, 16>(g.bias + colc + 4, bias + 4);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* stg = sh.stg[wave];
+
+  int kk = 0, ti = 0;
+  for (int s = 0; s < S; ++s) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const unsigned char* sa = sh.ring[s % PS_NST];
+    const unsigned char* sb = BRES ? sh.bslab[kk] : sa + TILE_BYTES;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8v af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<true>(sa, wm * 64 + i * 16, s2, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<KB>(sb, wn * 64 + j * 16, s2, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (++kk < NK) continue;
+    // ---- tile done: per-wave epilogue, 16 rows at a time through the wave's strip
+    kk = 0;
+    const int64_t rbase = (int64_t)(first + 8 * R * ti) * BM + wm * 64 + (lane >> 3);  // + 16 i + 8 u
+    ++ti;
+    PsIn<EPI> in[2];
+    ps_epi_load<EPI>(g, in[0], rbase, colc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) ps_epi_load<EPI>(g, in[(i + 1) & 1], rbase + 16 * (i + 1), colc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) stg[((lane >> 4) * 4 + rr) * PS_LD + j * 16 + (lane & 15)] = acc[i][j][rr];
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int lr = (lane >> 3) + 8 * u;
+        const int64_t row = rbase + 16 * i + 8 * u;
+        float v[8];
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + lr * PS_LD + (lane & 7) * 8);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + lr * PS_LD + (lane & 7) * 8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        const PsIn<EPI>& q = in[i & 1];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = g.alpha * v[e] + bias[e];
+        const bool ok = row < g.M && col0 < g.N;
+        if constexpr (EPI == EPI_ACT) {
+          if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, v);
+          if (g.act == LTHM_ACT_GELU) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = qgelu(v[e]);
+          }
+        }
+        if constexpr (EPI == EPI_GRAD) {
+          if (g.act == LTHM_ACT_GELU_GRAD) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(q.x[u][e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(q.x[u][e]);
+          }
+        }
+        if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += q.x[u][e];
+        }
+        if constexpr (EPI == EPI_RES2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += q.y[u][e];
+        }
+        if (ok) {
+          if (g.out_dt == LTHM_F32) {
+            float* o = reinterpret_cast<float*>(g.C) + row * g.ldc + col0;
+            *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+          } else {
+            store_vec<bf16_t, 8>(reinterpret_cast<bf16_t*>(g.C) + row * g.ldc + col0, v);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
+
+static int lthm_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// 0: never, 1: when eligible (default), set by LTHM_GEMM_PS
+static int lthm_gemm_ps_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("LTHM_GEMM_PS");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode;
+}
 
 extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   LTHM_REQUIRE(d != nullptr);
@@ -443,6 +726,45 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   }
   const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
   hipStream_t s = (hipStream_t)stream;
+  const int per_xcd = lthm_cu_count() / 8;
+  int epi = -1;
+  {
+    const bool a16 = ((uintptr_t)d->C % 16) == 0 && d->ldc % 8 == 0 && ((uintptr_t)d->bias % 16) == 0;
+    const bool r1 = d->res1 && d->res1_dtype == LTHM_F32 && ((uintptr_t)d->res1 % 16) == 0 && g.ldr1 % 8 == 0;
+    const bool r2 = d->res2 && d->res2_dtype == LTHM_F32 && ((uintptr_t)d->res2 % 16) == 0 && g.ldr2 % 8 == 0;
+    const bool ax = ((uintptr_t)d->aux % 16) == 0 && ((uintptr_t)d->aux_out % 16) == 0 && g.ldaux % 8 == 0;
+    const int act = d->act;
+    if (!a16 || !ax) epi = -1;
+    else if (act == LTHM_ACT_NONE && !d->res1 && !d->res2) epi = EPI_PLAIN;
+    else if ((act == LTHM_ACT_GELU || act == LTHM_ACT_QGELU) && !d->res1 && !d->res2) epi = EPI_ACT;
+    else if ((act == LTHM_ACT_GELU_GRAD || act == LTHM_ACT_QGELU_GRAD) && !d->bias && !d->res1 && !d->res2) epi = EPI_GRAD;
+    else if (act == LTHM_ACT_NONE && r1 && !d->res2) epi = EPI_RES1;
+    else if (act == LTHM_ACT_NONE && r1 && r2) epi = EPI_RES2;
+  }
+  if (lthm_gemm_ps_mode() && epi >= 0 && ka && splits == 1 && d->batch == 1 && g.fast_ok && d->K % BK == 0 &&
+      d->K > 0 && d->N % 8 == 0 && tiles_n <= per_xcd && (int64_t)tiles_m * tiles_n >= 4 * 8 * per_xcd) {
+    const int R = per_xcd / tiles_n;  // row-panel walkers per column tile and XCD
+    dim3 grid(8 * R * tiles_n);
+    const bool bres = d->K <= 4 * BK;
+#define LTHM_PS(KB_, BRES_, EPI_) \
+  hipLaunchKernelGGL((gemm_ps_k<KB_, BRES_, EPI_>), grid, dim3(PS_THREADS), 0, s, g, tiles_m, tiles_n, R)
+#define LTHM_PS_EPI(KB_, BRES_)                        \
+  switch (epi) {                                       \
+    case EPI_PLAIN: LTHM_PS(KB_, BRES_, EPI_PLAIN); break; \
+    case EPI_ACT: LTHM_PS(KB_, BRES_, EPI_ACT); break;     \
+    case EPI_GRAD: LTHM_PS(KB_, BRES_, EPI_GRAD); break;   \
+    case EPI_RES1: LTHM_PS(KB_, BRES_, EPI_RES1); break;   \
+    default: LTHM_PS(KB_, BRES_, EPI_RES2); break;         \
+  }
+    if (bres && kb) { LTHM_PS_EPI(true, true) }
+    else if (bres) { LTHM_PS_EPI(false, true) }
+    else if (kb) { LTHM_PS_EPI(true, false) }
+    else { LTHM_PS_EPI(false, false) }
+#undef LTHM_PS_EPI
+#undef LTHM_PS
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid(tiles_m * tiles_n, d->batch, splits);
   const size_t shmem = 4 * TILE_BYTES;
   if (ka && kb) hipLaunchKernelGGL((gemm_k<true, true>), grid, dim3(256), shmem, s, g, tiles_n);

@@ -439,34 +439,6 @@ struct ClTile {
 
 __device__ __attribute__((aligned(16))) unsigned char cl_zero_row[256];
 
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-// LDS-DMA issued as asm: the compiler neither counts these loads nor guards LDS
-// reads against them (the builtin makes it drain vmcnt(0) before unrelated LDS
-// reads); the kernels retire them with explicit counted waits + a barrier.
-// Ordinary loads stay correct: in-order vmcnt only makes their waits stricter.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)p);
-}
-__device__ __forceinline__ void glds16(const void* src, void* lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
-}
-__device__ __forceinline__ void glds4(const void* src, void* lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// retire every ordinary load issued so far, visibly to the compiler's own wait
-// bookkeeping (vmcnt(0), expcnt / lgkmcnt untouched): issued before the DMA
-// prologue, so no first use inside the tile loop drains the DMA ring
-__device__ __forceinline__ void retire_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // Image-row staging.  Wave w stages rows 16w .. 16w + 15 of every tile with four
 // DMAs of 4 rows x 256 B; lane l lands at row 16w + 4k + l/16, slot l%16 and so
