@@ -271,6 +271,27 @@ __device__ __forceinline__ void stage_img(unsigned char* img, const bf16_t* __re
   }
 }
 
+// the same image by LDS-DMA (global_load_lds_dwordx4): 1-KiB pieces, wave w
+// issues pieces w, w + 4, ...; the DMA's lane-linear destination slot loads the
+// chunk that img_off's swizzle puts there.  Rows >= T read a zero chunk.  All
+// pieces of every image are in flight together; the caller retires them with
+// wait_vm<0>() + __syncthreads().
+__device__ __attribute__((aligned(16))) unsigned char attn_zero16[16];
+template <int E>
+__device__ __forceinline__ void stage_img_dma(unsigned char* img, const bf16_t* __restrict__ src, int64_t ts, int T,
+                                              int Tk, int wave, int lane) {
+  constexpr int NC = E / 8;                                   // 16-B chunks per row
+  constexpr int RPP = 1024 / (2 * E);                         // rows per 1-KiB piece
+  constexpr int RPL = (256 / (2 * E)) > 0 ? 256 / (2 * E) : 1;
+  const int npieces = Tk / RPP;
+  for (int d = wave; d < npieces; d += 4) {
+    const int row = RPP * d + lane / NC, slot = lane % NC;
+    const int ch = slot ^ ((row / RPL) & (NC - 1));
+    const void* p = row < T ? (const void*)(src + (int64_t)row * ts + ch * 8) : (const void*)attn_zero16;
+    glds16(p, img + d * 1024);
+  }
+}
+
 // row fragment: B[k = 32s + 8(l>>4) + i][n = row0 + (l&15)] = img[row0 + (l&15)][32s + ...]
 template <int E>
 __device__ __forceinline__ bf16x8v img_row_frag(const unsigned char* img, int row0, int s, int lane) {
@@ -330,6 +351,31 @@ __device__ __forceinline__ void c_to_a_split(float* scr, const f32x4& c0, const 
   lo = __builtin_bit_cast(bf16x8v, l);
 }
 
+// C-layout pair (cols 0..15, 16..31 of a 16-row tile) -> 16-B bf16 row stores:
+// lane l writes row r0 + (l & 15), columns 8 (l >> 4) .. + 7 of the 32 (scaled by
+// `scale`); rows >= T are skipped.  One 1-KiB store instruction instead of eight
+// 2-byte scatters per lane.
+__device__ __forceinline__ void c_store_rows(float* scr, const f32x4& c0, const f32x4& c1, float scale, int lane,
+                                             bf16_t* __restrict__ base, int64_t ts, int r0, int T) {
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    scr[(rg + j) * SCR_LD + col] = c0[j];
+    scr[(rg + j) * SCR_LD + 16 + col] = c1[j];
+  }
+  __builtin_amdgcn_wave_barrier();
+  const float* rp = scr + (lane & 15) * SCR_LD + 8 * (lane >> 4);
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp);
+  const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + 4);
+  __builtin_amdgcn_wave_barrier();
+  const int r = r0 + (lane & 15);
+  if (r < T) {
+    const float v[8] = {x0[0] * scale, x0[1] * scale, x0[2] * scale, x0[3] * scale,
+                        x1[0] * scale, x1[1] * scale, x1[2] * scale, x1[3] * scale};
+    store_vec<bf16_t, 8>(base + (int64_t)r * ts + 8 * (lane >> 4), v);
+  }
+}
+
 __device__ __forceinline__ float row16_max(float v) {
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -339,6 +385,29 @@ __device__ __forceinline__ float row16_sum(float v) {
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Longest-processing-time assignment of the 16-row tiles of one head to the 4
+// waves (the same deterministic schedule in every wave; ntiles <= 16).  With
+// causal masking a query tile q0 costs ceil((q0 + 16) / 32) key blocks and a key
+// tile k0 costs (Tk - (k0 & ~31)) / 32 query blocks, so the round-robin deal
+// (tile t -> wave t % 4) leaves the wave holding the ragged last tile (T' = 129:
+// one valid row, every key block) ~40 % behind the others.
+__device__ __forceinline__ uint32_t lpt_tiles(int ntiles, int Tk, bool causal, bool key_tiles, int wave) {
+  int load[4] = {0, 0, 0, 0};
+  uint32_t mine = 0;
+  for (int i = 0; i < ntiles; ++i) {
+    const int t = key_tiles ? i : ntiles - 1 - i;  // descending cost
+    const int c0 = 16 * t;
+    const int nb = !causal ? Tk / 32 : key_tiles ? (Tk - (c0 & ~31)) / 32 : min(Tk, (c0 + 16 + 31) & ~31) / 32;
+    int w = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (load[j] < load[w]) w = j;
+    load[w] += nb + 1;
+    if (w == wave) mine |= 1u << t;
+  }
+  return mine;
 }
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
@@ -354,15 +423,18 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
   float* scr_all = bias + ((2 * T + 4) & ~3);                 // [4][16][SCR_LD], 16 B aligned
   const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  stage_img<E>(Ki, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, T, Tk, tid);
-  stage_img<E>(Vi, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, T, Tk, tid);
+  stage_img_dma<E>(Ki, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, T, Tk, wave, lane);
+  stage_img_dma<E>(Vi, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, T, Tk, wave, lane);
   for (int i = tid; i <= 2 * T; i += 256) bias[i] = a.table ? a.table[(int64_t)i * a.H + h] : 0.f;
+  wait_vm<0>();
   __syncthreads();
   float* scr = scr_all + wave * 16 * SCR_LD;
   const float rs = rsqrtf((float)E);
   const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
   const int col = lane & 15, rg = (lane >> 4) * 4;
-  for (int q0 = wave * 16; q0 < Tq; q0 += 64) {
+  const uint32_t mine = lpt_tiles(Tq / 16, Tk, a.causal, false, wave);
+  for (int q0 = 0; q0 < Tq; q0 += 16) {
+    if (!((mine >> (q0 >> 4)) & 1u)) continue;
     bf16x8v qf[NS];
     glob_row_frags<E>(qf, qg, a.q_ts, q0, T, lane);
     f32x4 o[NE];
@@ -417,13 +489,13 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int q = q0 + rg + j;
       const float lt = row16_sum(l[j]);
-      if (q < T) {
-        const float inv = 1.f / lt;
+      const float inv = 1.f / lt;
 #pragma unroll
-        for (int e = 0; e < NE; ++e) og[(int64_t)q * a.o_ts + e * 16 + col] = f2bf(o[e][j] * inv);
-        if (col == 0) a.lse[((int64_t)b * a.H + h) * T + q] = m[j] + __logf(lt);
-      }
+      for (int e = 0; e < NE; ++e) o[e][j] *= inv;
+      if (q < T && col == 0) a.lse[((int64_t)b * a.H + h) * T + q] = m[j] + __logf(lt);
     }
+#pragma unroll
+    for (int e = 0; e < NE; e += 2) c_store_rows(scr, o[e], o[e + 1], 1.f, lane, og + e * 16, a.o_ts, q0, T);
   }
 }
 
@@ -451,45 +523,56 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
   const bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
   const bf16_t* dog = a.dout + b * a.o_bs + h * a.o_hs;
   if (rows_pass) {
-    stage_img<E>(I0, kg, a.k_ts, T, Tk, tid);
-    stage_img<E>(I1, vg, a.v_ts, T, Tk, tid);
+    stage_img_dma<E>(I0, kg, a.k_ts, T, Tk, wave, lane);
+    stage_img_dma<E>(I1, vg, a.v_ts, T, Tk, wave, lane);
   } else {
-    stage_img<E>(I0, qg, a.q_ts, T, Tk, tid);
-    stage_img<E>(I1, dog, a.o_ts, T, Tk, tid);
+    stage_img_dma<E>(I0, qg, a.q_ts, T, Tk, wave, lane);
+    stage_img_dma<E>(I1, dog, a.o_ts, T, Tk, wave, lane);
   }
-  for (int i = tid; i < 2 * T + 2; i += 256) {
-    bias[i] = (a.table && i <= 2 * T) ? a.table[(int64_t)i * a.H + h] : 0.f;
-    dbias[i] = 0.f;
-  }
+  for (int i = tid; i < 2 * T + 2; i += 256) bias[i] = (a.table && i <= 2 * T) ? a.table[(int64_t)i * a.H + h] : 0.f;
+  for (int i = tid; i < 2 * T + 2; i += 256) dbias[i] = 0.f;
   const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
   for (int i = tid; i < Tk; i += 256) lse[i] = i < T ? lse_g[i] : 0.f;
-  // delta[q] = dO[q] . O[q]: one thread per (row, 16-byte chunk), all loads in
-  // flight at once, then a shuffle sum over the E/8 chunk lanes of each row
+  // delta[q] = dO[q] . O[q]: one thread per (row, 16-byte chunk), the loads of
+  // four passes in flight at once, then a shuffle sum over the E/8 chunk lanes
   {
     constexpr int CPR = E / 8;
-    for (int base = 0; base < Tk * CPR; base += 256) {
-      const int idx = base + tid;
-      const int q = idx / CPR, c = idx - q * CPR;
-      float d = 0.f;
-      if (q < T) {
-        const u32x4 u = *reinterpret_cast<const u32x4*>(dog + (int64_t)q * a.o_ts + c * 8);
-        const u32x4 v = *reinterpret_cast<const u32x4*>(og + (int64_t)q * a.o_ts + c * 8);
+    for (int base = 0; base < Tk * CPR; base += 4 * 256) {
+      u32x4 u[4], v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          d += __uint_as_float(u[i] << 16) * __uint_as_float(v[i] << 16) +
-               __uint_as_float(u[i] & 0xffff0000u) * __uint_as_float(v[i] & 0xffff0000u);
+      for (int it = 0; it < 4; ++it) {
+        const int idx = base + it * 256 + tid;
+        const int q = idx / CPR, c = idx - q * CPR;
+        u[it] = v[it] = u32x4{0u, 0u, 0u, 0u};
+        if (q < T) {
+          u[it] = *reinterpret_cast<const u32x4*>(dog + (int64_t)q * a.o_ts + c * 8);
+          v[it] = *reinterpret_cast<const u32x4*>(og + (int64_t)q * a.o_ts + c * 8);
+        }
       }
 #pragma unroll
-      for (int o = 1; o < CPR; o <<= 1) d += __shfl_xor(d, o, 64);
-      if (c == 0 && q < Tk) delta[q] = d;
+      for (int it = 0; it < 4; ++it) {
+        const int idx = base + it * 256 + tid;
+        const int q = idx / CPR, c = idx - q * CPR;
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          d += __uint_as_float(u[it][i] << 16) * __uint_as_float(v[it][i] << 16) +
+               __uint_as_float(u[it][i] & 0xffff0000u) * __uint_as_float(v[it][i] & 0xffff0000u);
+#pragma unroll
+        for (int o = 1; o < CPR; o <<= 1) d += __shfl_xor(d, o, 64);
+        if (c == 0 && q < Tk) delta[q] = d;
+      }
     }
   }
+  wait_vm<0>();
   __syncthreads();
   float* scr = scr_all + wave * 16 * SCR_LD;
   const float rs = rsqrtf((float)E);
   const int col = lane & 15, rg = (lane >> 4) * 4;
   if (rows_pass) {
-    for (int q0 = wave * 16; q0 < Tq; q0 += 64) {
+    const uint32_t mine = lpt_tiles(Tq / 16, Tk, a.causal, false, wave);
+    for (int q0 = 0; q0 < Tq; q0 += 16) {
+      if (!((mine >> (q0 >> 4)) & 1u)) continue;
       bf16x8v qf[NS], df[NS];
       glob_row_frags<E>(qf, qg, a.q_ts, q0, T, lane);
       glob_row_frags<E>(df, dog, a.o_ts, q0, T, lane);
@@ -517,13 +600,30 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
           const bool vb = q < T && kb < T && (!a.causal || kb <= q);
           const float da = va ? __expf(s0[j] * rs + bias[q - ka + T] - lq[j]) * (p0[j] - dl[j]) : 0.f;
           const float db = vb ? __expf(s1[j] * rs + bias[q - kb + T] - lq[j]) * (p1[j] - dl[j]) : 0.f;
-          if (va) atomicAdd(&dbias[q - ka + T], da);
-          if (vb) atomicAdd(&dbias[q - kb + T], db);
           s0[j] = da;
           s1[j] = db;
         }
         bf16x8v gh, gl;
         c_to_a_split(scr, s0, s1, lane, gh, gl);
+        if (a.dtable_part) {
+          // bias gradient: the tile's dS is still in the wave's scratch; lane l
+          // sums diagonal r - c = l - 31 of the 16 x 32 tile, so one LDS atomic
+          // per lane and tile (distinct addresses within the instruction)
+          // replaces eight colliding per-element atomics
+          const int dd = lane - 31;
+          const int idx = q0 - k0 + T + dd;
+          if (lane < 47 && idx >= 0 && idx <= 2 * T) {
+            float sum = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int c = r - dd;
+              if (c >= 0 && c < 32) sum += scr[r * SCR_LD + c];
+            }
+            atomicAdd(&dbias[idx], sum);
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+        }
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const bf16x8v kf = img_tr_frag<E>(I0, k0, e * 16, lane);
@@ -533,18 +633,15 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
       }
       bf16_t* dqg = a.dq + b * a.q_bs + h * a.q_hs;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = q0 + rg + j;
-        if (q < T)
-#pragma unroll
-          for (int e = 0; e < NE; ++e) dqg[(int64_t)q * a.q_ts + e * 16 + col] = f2bf(dq[e][j] * rs);
-      }
+      for (int e = 0; e < NE; e += 2) c_store_rows(scr, dq[e], dq[e + 1], rs, lane, dqg + e * 16, a.q_ts, q0, T);
     }
     __syncthreads();
     if (a.dtable_part)
       for (int i = tid; i <= 2 * T; i += 256) a.dtable_part[((int64_t)b * (2 * T + 1) + i) * a.H + h] = dbias[i];
   } else {
-    for (int k0 = wave * 16; k0 < Tq; k0 += 64) {
+    const uint32_t mine = lpt_tiles(Tq / 16, Tk, a.causal, true, wave);
+    for (int k0 = 0; k0 < Tq; k0 += 16) {
+      if (!((mine >> (k0 >> 4)) & 1u)) continue;
       bf16x8v kf[NS], vf[NS];
       glob_row_frags<E>(kf, kg, a.k_ts, k0, T, lane);
       glob_row_frags<E>(vf, vg, a.v_ts, k0, T, lane);
@@ -593,14 +690,9 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
       bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
       bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + rg + j;
-        if (k < T)
-#pragma unroll
-          for (int e = 0; e < NE; ++e) {
-            dkg[(int64_t)k * a.k_ts + e * 16 + col] = f2bf(dk[e][j] * rs);
-            dvg[(int64_t)k * a.v_ts + e * 16 + col] = f2bf(dv[e][j]);
-          }
+      for (int e = 0; e < NE; e += 2) {
+        c_store_rows(scr, dk[e], dk[e + 1], rs, lane, dkg + e * 16, a.k_ts, k0, T);
+        c_store_rows(scr, dv[e], dv[e + 1], 1.f, lane, dvg + e * 16, a.v_ts, k0, T);
       }
     }
   }
@@ -681,6 +773,12 @@ static int check_desc(const lthm_attn_desc* d) {
   if (!d || d->B < 0 || d->T <= 0 || d->T > 256 || d->H <= 0) return 1;
   if (d->table && d->table_rows < 2 * d->T + 1) return 1;
   if ((d->q_tok_stride % 8) || (d->k_tok_stride % 8) || (d->v_tok_stride % 8) || (d->o_tok_stride % 8)) return 1;
+  // 16-B rows: LDS-DMA image staging and vector row stores
+  if ((d->q_head_stride % 8) || (d->k_head_stride % 8) || (d->v_head_stride % 8) || (d->o_head_stride % 8)) return 1;
+  if ((d->q_batch_stride % 8) || (d->k_batch_stride % 8) || (d->v_batch_stride % 8) || (d->o_batch_stride % 8)) return 1;
+  const void* ptrs[8] = {d->q, d->k, d->v, d->out, d->dout, d->dq, d->dk, d->dv};
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16) return 1;
   return 0;
 }
 
