@@ -16,6 +16,8 @@
 // Reference call sites served: every nn.Linear of commons/transformers/layers.py
 // (MultiHeadAttention.c_attn/c_proj :240-241, _MLP.c_fc/c_proj :274-276),
 // commons/layers.py:65-81 (MLP + QuickGELU), models/lthm/sequence/*.py Linears.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace lthm {
@@ -574,7 +576,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
 
   int kk = 0, ti = 0;
   for (int s = 0; s < S; ++s) {
-    asm volatile("" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the stage the loaders refill next are done
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const unsigned char* sa = sh.ring[s % PS_NST];
@@ -664,6 +666,100 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
   }
 }
 
+// ---------------------------------------------------------------- weight-gradient GEMM
+// dW = dY^T X over M = B*T' = 528k token rows (both operands K-strided), N_out x
+// N_in <= 1024 x 1024.  The one-tile kernel re-reads each operand slice from L2
+// once per 128-wide output tile; this kernel gives a workgroup a 256 x 256 output
+// tile (8 compute waves as 4 x 2, 64 x 128 each: 128 accumulator registers per
+// lane) and a split of the M range, halving the LDS fill traffic per flop.  The
+// waves themselves stream 32-k stages (A 256 + B 256 columns, 2 x 16 KiB) into a
+// 4-deep LDS ring by LDS-DMA, retired by counted vmcnt waits + s_barrier; nothing
+// else in the loop touches vmcnt.  XCD-aware: the logical order split-major /
+// tile-minor keeps the output tiles of one split on one XCD, so each k-slice of
+// the operands is fetched from HBM once and re-read from that XCD's L2.  Each
+// workgroup writes its raw f32 partial tile to the split-K slab; splitk_reduce_k
+// applies alpha's epilogue (accumulate / output dtype).
+// Requires: A and B K-strided, batch 1, K % 32 == 0, 16-B aligned operands and
+// leading dims % 8 == 0.
+constexpr int WG_NST = 4;
+constexpr int WG_BK = 32;
+constexpr int WG_SUB = 32 * 256;  // one [32 k][128 cols] sub-image (8 KiB)
+struct WgSmem {
+  unsigned char ring[WG_NST][4][WG_SUB];  // per stage: A cols 0-127, A 128-255, B 0-127, B 128-255
+};
+
+__global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int tiles_n, int splits, int64_t kps) {
+  __shared__ __attribute__((aligned(16))) WgSmem sh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nblk = tiles_m * tiles_n * splits;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int split = lid / (tiles_m * tiles_n), tile = lid - split * (tiles_m * tiles_n);
+  const int64_t m0 = (int64_t)(tile / tiles_n) * 256, n0 = (int64_t)(tile % tiles_n) * 256;
+  const int64_t kb = (int64_t)split * kps, ke = min(g.K, kb + kps);
+  const int S = ke > kb ? (int)((ke - kb) / WG_BK) : 0;
+  // stage s: pieces 0..31 (1 KiB each, 4 k-rows x 256 B of one sub-image); wave w issues w, w+8, w+16, w+24
+  auto issue = [&](int st) {
+    const int64_t k = kb + (int64_t)st * WG_BK;
+    unsigned char* base = sh.ring[st % WG_NST][0];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int piece = wave + 8 * u;  // u = sub-image: 0,1 -> A halves, 2,3 -> B halves
+      const int sub = piece >> 3, d = piece & 7;
+      const bool isA = sub < 2;
+      const bf16_t* P = isA ? g.A : g.B;
+      const int64_t ld = isA ? g.lda : g.ldb, cols = isA ? g.M : g.N;
+      const int64_t c0 = (isA ? m0 : n0) + (sub & 1) * 128;
+      const int kr = 4 * d + (lane >> 4);
+      const int ch = (lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+      const int64_t gc = c0 + ch * 8;
+      const void* src = gc < cols ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
+      glds16(src, base + sub * WG_SUB + d * 1024);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;  // rows wm*64.., cols wn*128..
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  retire_loads();
+  for (int st = 0; st < WG_NST - 1 && st < S; ++st) issue(st);
+  for (int s = 0; s < S; ++s) {
+    // issued: 0 .. min(S-1, s+NST-2); step s must have landed (4 DMAs per wave and stage)
+    const int behind = min(S - 1, s + WG_NST - 2) - s;
+    if (behind >= 2) wait_vm<8>();
+    else if (behind == 1) wait_vm<4>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the stage being freed are done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + WG_NST - 1 < S) issue(s + WG_NST - 1);  // into the stage step s-1 freed
+    const unsigned char* sa = sh.ring[s % WG_NST][wm >> 1];  // A rows wm*64: sub-image wm/2, cols (wm&1)*64
+    const unsigned char* sb = sh.ring[s % WG_NST][2 + wn];  // B cols wn*128..: sub-image 2 + wn
+    bf16x8v af[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<false>(sa, (wm & 1) * 64 + i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8v bfr = read_frag<false>(sb, j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+    }
+  }
+  // raw alpha * partial tile -> split-K slab [split][M][N] (16 lanes = 64 contiguous bytes)
+  float* ws = g.ws + (int64_t)split * g.M * g.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t col = n0 + wn * 128 + j * 16 + (lane & 15);
+        if (row < g.M && col < g.N) ws[row * g.N + col] = g.alpha * acc[i][j][r];
+      }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -726,6 +822,31 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   }
   const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
   hipStream_t s = (hipStream_t)stream;
+  // weight gradients: 256 x 256 split-K tiles (splits bounded by the caller's workspace)
+  if (lthm_gemm_ps_mode() && !ka && !kb && d->batch == 1 && d->workspace && d->K % WG_BK == 0 && g.fast_ok &&
+      d->M % 8 == 0 && d->N % 8 == 0 && d->act == LTHM_ACT_NONE && !d->bias && d->M * d->N > 0) {
+    const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
+    const int64_t cap = (int64_t)(d->workspace_bytes / ((size_t)d->M * d->N * 4));
+    int64_t sp = std::min<int64_t>(std::max(1, lthm_cu_count() / (tm * tn)), cap);
+    sp = std::min<int64_t>(sp, d->K / (WG_BK * 8));  // >= 8 stages per split
+    if (sp >= 2 && tm * tn <= lthm_cu_count()) {
+      int64_t kpw = (d->K + sp - 1) / sp;
+      kpw = (kpw + WG_BK - 1) / WG_BK * WG_BK;
+      const int spl = (int)((d->K + kpw - 1) / kpw);
+      GemmArgs gw = g;
+      gw.ws = d->workspace;
+      gw.res1 = nullptr; gw.res2 = nullptr;
+      hipLaunchKernelGGL(gemm_wg_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
+      LTHM_CHECK_LAUNCH();
+      GemmArgs gr = g;
+      gr.ws = d->workspace;
+      gr.alpha = 1.f;  // alpha already applied to the partials
+      const int64_t total = d->M * d->N;
+      hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, gr, spl, 1);
+      LTHM_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const int per_xcd = lthm_cu_count() / 8;
   int epi = -1;
   {

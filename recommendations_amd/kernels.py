@@ -202,12 +202,16 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
 
 
 def _splits_for(M: int, N: int, K: int) -> int:
-    """Split-K factor for tall reductions (weight gradients): fill ~2 waves of 256 CUs."""
+    """Split-K factor (and so the f32 partial-slab workspace) for tall reductions
+    (weight gradients): ~2 waves of 128 x 128 tiles on 256 CUs for the one-tile
+    kernel, or one 256 x 256 tile per CU for gemm_wg_k (csrc/gemm.hip), whichever
+    is larger; the library picks its kernel and uses at most this many splits."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     if tiles >= 256 or K < 4096:
         return 1
     s = max(1, min(512 // tiles, K // 2048))
-    return s
+    tiles256 = ((M + 255) // 256) * ((N + 255) // 256)
+    return max(s, min(256 // tiles256, K // 256))
 
 
 def linear_fwd(x2d, w_bf16, bias=None, act=ACT_NONE, aux_out=None, res1=None, res2=None, out_dtype=torch.bfloat16):

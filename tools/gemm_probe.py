@@ -38,6 +38,10 @@ def main():
         ("dh2", lambda: K.linear_dgrad(g, w1)),
         ("do", lambda: K.linear_dgrad(dy, wp)),
         ("dh1", lambda: K.linear_dgrad(dqkv, wqkv)),
+        ("dw2", lambda: K.linear_wgrad(dy, g)),
+        ("dw1", lambda: K.linear_wgrad(g, h)),
+        ("dwp", lambda: K.linear_wgrad(dy, h)),
+        ("dwqkv", lambda: K.linear_wgrad(dqkv, h)),
     ]
     out, tot = [], 0.0
     for name, fn in res:
