@@ -92,6 +92,8 @@ CONFIGS = {
     # SURVEY §8 C3 per GPU: 100M-row item table row-sharded over the ranks, 64 categorical tables
     "c3": dict(B=4096, T=128, d=256, L=4, H=4, n_cat=64, cat_vocab=1_000_000, item_vocab=100_000_000,
                item_table_sharded=True),
+    # BASELINE.json configs[3]: ranker, 128 dense + 64 cat x 1M, interaction layers only
+    "c4": dict(kind="ranker", B=65536, n_dense=128, n_cat=64, cat_vocab=1_000_000),
 }
 
 
@@ -99,6 +101,12 @@ def build(cfgd, dev):
     from recommendations_amd.models.lthm.builder import LTHMModelBuilder
     from recommendations_amd.models.lthm.config import lthm_config
     torch.manual_seed(1234)  # identical replicas on every rank
+    if cfgd.get("kind") == "ranker":
+        from recommendations_amd.models.ranker.config import ranker_config
+        cfg = ranker_config(n_dense=cfgd["n_dense"], n_cat=cfgd["n_cat"], cat_vocab=cfgd["cat_vocab"])
+        with torch.device(dev):  # 64 x 1M x 32 tables drawn on the device
+            model = cfg.get_builder().build()
+        return cfg, model
     cfg = lthm_config(T=cfgd["T"], d=cfgd["d"], n_layers=cfgd["L"], n_head=cfgd["H"], cat_features=cfgd["n_cat"],
                       cat_vocab=cfgd["cat_vocab"], item_vocab=cfgd["item_vocab"],
                       item_table_sharded=cfgd.get("item_table_sharded", False))
@@ -142,6 +150,45 @@ def cpu_baseline(cfg, model, cfgd, B_cpu):
                        f"(fp32 torch-CPU oracle: oracle/lthm_ref.py + torch.optim.AdamW over every parameter)")
 
 
+def cpu_baseline_ranker(cfg, model, cfgd, B_cpu):
+    """The oracle's CPU restatement of the ranker step (oracle/ranker_ref.py fwd + BCE
+    + bwd + torch.optim.AdamW over the dense parameters and the touched table rows'
+    full tables), on a bounded sample of B_cpu rows of the C4 workload."""
+    from oracle import ranker_ref
+    from recommendations_amd.data import synthetic_ranker_batch
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    sd = {k: (v.detach().float().cpu().clone().requires_grad_(True) if v.is_floating_point() else v.cpu())
+          for k, v in model.state_dict().items()}
+    params = [v for k, v in sd.items() if v.is_floating_point() and ("emb.weight" in k or "interaction" in k)]
+    tabs = [sd["_model.cat_tables.weight"]]
+    opt = torch.optim.AdamW([p for p in params if p is not tabs[0]], lr=cfg.lr, weight_decay=cfg.weight_decay,
+                            betas=cfg.betas)
+    batch = synthetic_ranker_batch(B_cpu, cfg.n_dense, cfg.n_categorical, seed=99)
+
+    def step():
+        loss = ranker_ref.ranker_loss(sd, cfg, batch)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        with torch.no_grad():  # plain SGD-style row update of the touched table rows (bounded CPU work)
+            g = tabs[0].grad
+            tabs[0].sub_(cfg.lr * g)
+            tabs[0].grad = None
+
+    step()
+    t0 = time.perf_counter()
+    step()
+    dt = time.perf_counter() - t0
+    return dict(value=round(B_cpu / dt, 3), unit="samples/s", cores=cores, kind="port",
+                sample=f"{B_cpu} rows of the {cfgd} workload, 1 timed step after 1 warm-up "
+                       f"(fp32 torch-CPU oracle: oracle/ranker_ref.py + torch.optim.AdamW on the dense parameters)")
+
+
 def k_of(sd, v):
     for k, t in sd.items():
         if t is v:
@@ -163,7 +210,7 @@ def main():
     args = ap.parse_args()
 
     from recommendations_amd import _lib
-    from recommendations_amd.data import synthetic_lthm_batch
+    from recommendations_amd.data import synthetic_lthm_batch, synthetic_ranker_batch
     from recommendations_amd.distributed import GradBucketAllReduce, init_from_env, step_flags
 
     rank, local, world = init_from_env()
@@ -176,12 +223,19 @@ def main():
         cfgd["B"] = args.batch
     cfg, model = build(cfgd, dev)
     B = cfgd["B"]
-    if world > 1 and model._model.user_context is not None:
-        model._model.user_context.tables.replicated_dp = True
+    ranker = cfgd.get("kind") == "ranker"
+    if world > 1:
+        if ranker:
+            model._model.cat_tables.replicated_dp = True
+        elif model._model.user_context is not None:
+            model._model.user_context.tables.replicated_dp = True
     opts = model.optimizers_for_param_groups(model.param_groups())
-    dense_params = [p for n, p in model.named_parameters() if p.requires_grad and "user_context.tables" not in n]
+    dense_params = [p for n, p in model.named_parameters() if p.requires_grad and not model.is_sparse(n)]
     allreduce = GradBucketAllReduce(dense_params)
-    batch = synthetic_lthm_batch(B, cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=rank, device=dev)
+    if ranker:
+        batch = synthetic_ranker_batch(B, cfgd["n_dense"], cfgd["n_cat"], seed=1234, rank=rank, device=dev)
+    else:
+        batch = synthetic_lthm_batch(B, cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=rank, device=dev)
 
     def step():
         out = model(batch)
@@ -218,7 +272,8 @@ def main():
     assert float(flags[1]) == 0.0, "non-finite loss"
     samples = B * world * args.steps
     res = {
-        "metric": "training samples/sec (LTHM fwd+bwd) at 1/2/4/8 MI355X; embedding HBM GB/s",
+        "metric": ("training samples/sec (ranker C4 fwd+bwd)" if ranker else
+                   "training samples/sec (LTHM fwd+bwd) at 1/2/4/8 MI355X; embedding HBM GB/s"),
         "value": round(samples / dt, 2),
         "unit": "samples/s",
         "n_gpus": world,
@@ -229,12 +284,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (seeded full-range int64 item ids with 0-padding, labels 0..3, 2023 timestamps, "
-                "uniform int64 categorical ids); random-init weights",
-        "config": {"workload": f"LTHM {args.config.upper()}: item KShift P={cfgd['item_vocab']} D=32 K=16, "
-                               f"{cfgd['n_cat']} cat x {cfgd['cat_vocab']} KShift D=32 K=8, T={cfgd['T']}, "
-                               f"d={cfgd['d']}, {cfgd['L']} layers, H={cfgd['H']}, 6 lookahead heads",
-                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd["T"],
+        "data": ("synthetic (N(0,1) dense features, uniform int64 categorical ids, Bernoulli(0.1) clicks); "
+                 "random-init weights" if ranker else
+                 "synthetic (seeded full-range int64 item ids with 0-padding, labels 0..3, 2023 timestamps, "
+                 "uniform int64 categorical ids); random-init weights"),
+        "config": {"workload": (f"ranker C4: {cfgd['n_dense']} dense -> DenseMapper(16 proj x 20 bins) + "
+                                f"{cfgd['n_cat']} cat x {cfgd['cat_vocab']} FlatEmbedding D=32 -> MLP [1024, 512] -> 1, "
+                                f"QuickGELU, BCE" if ranker else
+                                f"LTHM {args.config.upper()}: item KShift P={cfgd['item_vocab']} D=32 K=16, "
+                                f"{cfgd['n_cat']} cat x {cfgd['cat_vocab']} KShift D=32 K=8, T={cfgd['T']}, "
+                                f"d={cfgd['d']}, {cfgd['L']} layers, H={cfgd['H']}, 6 lookahead heads"),
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
                    "parallelism": f"dp{world}" + (
                        (" (item table row-sharded, all_to_all row exchange; categorical tables replicated, "
                         "gathered row updates)" if cfgd.get("item_table_sharded") else
@@ -283,7 +343,8 @@ def main():
             res["embedding_gather"] = embedding_gather_hbm(dev)
         res["kernels"] = kern
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfgd.get("item_table_sharded"):
-        res["cpu_baseline"] = cpu_baseline(cfg, model, cfgd, args.cpu_batch)
+        res["cpu_baseline"] = (cpu_baseline_ranker(cfg, model, cfgd, 256) if ranker else
+                               cpu_baseline(cfg, model, cfgd, args.cpu_batch))
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

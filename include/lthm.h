@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 8 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 9 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -285,6 +285,15 @@ int lthm_table_bwd_mfma(const uint16_t* rows, int32_t nidx, int32_t R, const voi
  * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
 int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,
                       float* out, void* stream);
+
+/* Binary cross-entropy with logits, mean reduction
+ * (F.binary_cross_entropy_with_logits; the ranker's click loss and
+ * embedding_module_gen.py:112-116's mask-model loss).
+ * fwd: *loss_sum += inv_n * sum_i [max(z,0) - z y + log1p(exp(-|z|))]  (caller zeroes it)
+ * bwd: dz_i = (sigmoid(z_i) - y_i) * (*gscale) * inv_n                      */
+int lthm_bce_logits_fwd(const float* z, const float* y, int64_t n, float inv_n, float* loss_sum, void* stream);
+int lthm_bce_logits_bwd(const float* z, const float* y, int64_t n, const float* gscale, float inv_n, float* dz,
+                        void* stream);
 
 /* QueryTower input assembly (query_tower.py:89-111): action + time embeddings,
  * pad substitution, zero/CLS token, reversed position embedding. */

@@ -357,7 +357,12 @@ class DenseMapper(nn.Module):
 
     def forward(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         x = torch.cat([batch[f].reshape(-1, 1) for f in self.mappers], dim=1).float().contiguous()
-        z = K.quantile_map(x, self.quantile_table().contiguous(), shared=False)
+        return self.forward_matrix(x)
+
+    def forward_matrix(self, x: torch.Tensor) -> torch.Tensor:
+        """Same as forward for the features already stacked as columns of x [B, F]
+        (in the mappers' order): one quantile-map kernel, one fused CVE kernel."""
+        z = K.quantile_map(x.float().contiguous(), self.quantile_table().contiguous(), shared=False)
         return CVEFn.apply(z.unsqueeze(1), list(self.emb), *[m.emb.weight for m in self.emb]).squeeze(1)
 
 

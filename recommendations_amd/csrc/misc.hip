@@ -194,3 +194,46 @@ extern "C" int lthm_quantile_map(const float* x, int64_t B, int32_t F, const flo
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- BCE with logits
+namespace lthm {
+__global__ __launch_bounds__(256) void bce_fwd_k(const float* __restrict__ z, const float* __restrict__ y, int64_t n,
+                                                 float inv_n, float* __restrict__ loss_sum) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float zi = z[i];
+    acc += fmaxf(zi, 0.f) - zi * y[i] + log1pf(expf(-fabsf(zi)));
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss_sum, ((red[0] + red[1]) + (red[2] + red[3])) * inv_n);
+}
+__global__ __launch_bounds__(256) void bce_bwd_k(const float* __restrict__ z, const float* __restrict__ y, int64_t n,
+                                                 const float* __restrict__ gscale, float inv_n, float* __restrict__ dz) {
+  const float g = (gscale ? *gscale : 1.f) * inv_n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dz[i] = (1.f / (1.f + expf(-z[i])) - y[i]) * g;
+}
+}  // namespace lthm
+
+extern "C" int lthm_bce_logits_fwd(const float* z, const float* y, int64_t n, float inv_n, float* loss_sum,
+                                   void* stream) {
+  LTHM_REQUIRE(n >= 0 && loss_sum != nullptr);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bce_fwd_k, dim3(grid_for(n, 256, 1024)), dim3(256), 0, (hipStream_t)stream, z, y, n, inv_n,
+                     loss_sum);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_bce_logits_bwd(const float* z, const float* y, int64_t n, const float* gscale, float inv_n,
+                                   float* dz, void* stream) {
+  LTHM_REQUIRE(n >= 0 && dz != nullptr);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bce_bwd_k, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, z, y, n, gscale,
+                     inv_n, dz);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -58,21 +58,32 @@ __global__ __launch_bounds__(256) void ptower_fwd_k(lthm_ptower_desc d, int tota
   const TT* tab = reinterpret_cast<const TT*>(d.tables);
   const TT* hist = reinterpret_cast<const TT*>(d.hist);
   for (int64_t tok = (int64_t)blockIdx.x * 4 + wave; tok < d.n; tok += (int64_t)gridDim.x * 4) {
-    // norm, mask, normalise (product_tower.py:47-51)
-    float xv = 0.f;
-    if (lane < Din) xv = Elem<TX>::ld(reinterpret_cast<const TX*>(d.x) + tok * Din + lane);
-    const float nrm = sqrtf(wave_sum(xv * xv));
-    const bool masked = !d.cve_only && ((nrm < d.norm_threshold) || (d.ids[tok] == 0));
-    const float xn = xv / fmaxf(nrm, 1e-12f);
-    float xn2 = xn;
-    if (!d.cve_only) {  // CosineVectorEmbedding re-normalises its already normalised input (layers.py:464)
-      const float nrm2 = sqrtf(wave_sum(xn * xn));
-      xn2 = xn / fmaxf(nrm2, 1e-12f);
+    // norm, mask, normalise (product_tower.py:47-51); Din <= 256: up to 4 elements per lane
+    float xv[4], ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = lane + 64 * k;
+      xv[k] = (i < Din) ? Elem<TX>::ld(reinterpret_cast<const TX*>(d.x) + tok * Din + i) : 0.f;
+      ss += xv[k] * xv[k];
     }
-    if (lane < Din) {
-      xw[lane] = xn;
-      xw2[lane] = xn2;
-      if (d.xn_out) reinterpret_cast<bf16_t*>(d.xn_out)[tok * Din + lane] = f2bf(xn);
+    const float nrm = sqrtf(wave_sum(ss));
+    const bool masked = !d.cve_only && ((nrm < d.norm_threshold) || (d.ids[tok] == 0));
+    float xn[4], ss2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xn[k] = xv[k] / fmaxf(nrm, 1e-12f);
+      ss2 += xn[k] * xn[k];
+    }
+    // CosineVectorEmbedding re-normalises its already normalised input (layers.py:464)
+    const float den2 = d.cve_only ? 1.f : fmaxf(sqrtf(wave_sum(ss2)), 1e-12f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = lane + 64 * k;
+      if (i < Din) {
+        xw[i] = xn[k];
+        xw2[i] = d.cve_only ? xn[k] : xn[k] / den2;
+        if (d.xn_out) reinterpret_cast<bf16_t*>(d.xn_out)[tok * Din + i] = f2bf(xn[k]);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     // bucket rows for all modules: lane handles (module, projection) pairs
@@ -785,7 +796,7 @@ extern "C" int lthm_flip_tokens(const int64_t* in, int64_t* out, int64_t B, int3
 }
 
 extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
-  LTHM_REQUIRE(d && d->n >= 0 && d->Din > 0 && d->Din <= 64 && d->n_mod >= 0 && d->n_mod <= LTHM_MAX_CVE);
+  LTHM_REQUIRE(d && d->n >= 0 && d->Din > 0 && d->Din <= 256 && d->n_mod >= 0 && d->n_mod <= LTHM_MAX_CVE);
   LTHM_REQUIRE(d->Dout > 0 && d->Dout <= 512);
   if (d->n == 0) return 0;
   int total = 0;

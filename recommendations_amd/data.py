@@ -44,3 +44,16 @@ def synthetic_lthm_batch(B: int, T: int, n_cat: int = 0, seed: int = 1234, rank:
     if device is not None:
         batch = {k: v.to(device, non_blocking=True) for k, v in batch.items()}
     return batch
+
+
+def synthetic_ranker_batch(B: int, n_dense: int = 128, n_cat: int = 64, seed: int = 1234, rank: int = 0,
+                           device: Optional[torch.device] = None, ctr: float = 0.1) -> Dict[str, torch.Tensor]:
+    """dense [B, n_dense] ~ N(0, 1) f32, categorical [B, n_cat] uniform
+    int64 ids, click label ~ Bernoulli(ctr) as float."""
+    g = torch.Generator().manual_seed(seed + rank)
+    batch = {"dense": torch.randn(B, n_dense, generator=g),
+             "categorical": torch.randint(INT64_MIN, INT64_MAX, (B, n_cat), generator=g, dtype=torch.int64),
+             "label": (torch.rand(B, generator=g) < ctr).float()}
+    if device is not None:
+        batch = {k: v.to(device, non_blocking=True) for k, v in batch.items()}
+    return batch

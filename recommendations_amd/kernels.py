@@ -636,3 +636,33 @@ def segmented_table_bwd(rows, dY, R, segments, out=None):
              ptr(ws) if ws is not None else None, wsb, stream(),
              _key="seg_tab_bwd_k", _work=float(n) * D * dY.element_size(), _unit="byte")
     return out
+
+
+# ----------------------------------------------------------------- BCE with logits
+class BCEWithLogitsFn(torch.autograd.Function):
+    """F.binary_cross_entropy_with_logits(z, y), mean over all elements, on the
+    lthm_bce_logits_* kernels (the ranker's click loss)."""
+
+    @staticmethod
+    def forward(ctx, z, y):
+        require_gpu(z, y)
+        _check(z.dtype == torch.float32 and y.dtype == torch.float32 and z.numel() == y.numel(),
+               "bce_with_logits takes float32 logits and targets of the same size")
+        z, y = z.contiguous(), y.contiguous()
+        n = z.numel()
+        out = zeros((1,), torch.float32, z.device)
+        call("lthm_bce_logits_fwd", ptr(z), ptr(y), n, 1.0 / max(n, 1), ptr(out), stream())
+        ctx.save_for_backward(z, y)
+        return out.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        z, y = ctx.saved_tensors
+        dz = torch.empty_like(z)
+        g = g.contiguous().float()
+        call("lthm_bce_logits_bwd", ptr(z), ptr(y), z.numel(), ptr(g), 1.0 / max(z.numel(), 1), ptr(dz), stream())
+        return dz, None
+
+
+def bce_with_logits(z, y):
+    return BCEWithLogitsFn.apply(z, y)
