@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 9 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 10 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -192,12 +192,18 @@ typedef struct lthm_attn_desc {
   void* dk;
   void* dv;
   float* dtable_part;
+  float* delta;
 } lthm_attn_desc;
 
-/* bf16 q/k/v/out, f32 table [table_rows, H] (row q-k+T), lse f32 [B, H, T]. T <= 256. */
+/* bf16 q/k/v/out, f32 table [table_rows, H] (row q-k+T), lse f32 [B, H, T].
+ * T <= 256: one workgroup per (batch, head) holds K and V whole in LDS.
+ * 256 < T <= 4096 (E = 32/64/128): 64-row workgroups stream K/V windows. */
 int lthm_attn_fwd(const lthm_attn_desc* desc, void* stream);
-/* dq/dk/dv bf16 (same strides as q/k/v); dtable_part f32 [B, 2T+1, H] (reduce over B). */
+/* dq/dk/dv bf16 (same strides as q/k/v); dtable_part f32 [parts, 2T+1, H] with
+ * parts = lthm_attn_bwd_parts(B, T) (reduce over the first dim; = B for T <= 256);
+ * delta: f32 [B, H, T] workspace, required when T > 256. */
 int lthm_attn_bwd(const lthm_attn_desc* desc, void* stream);
+int64_t lthm_attn_bwd_parts(int32_t B, int32_t T);
 
 /* ------------------------------------------------------------------------- */
 /* LTHM towers (models/lthm/sequence/ encoder, product and query towers)     */

@@ -28,7 +28,9 @@ struct AttnArgs {
   // backward
   const bf16_t* dout;
   bf16_t *dq, *dk, *dv;      // same strides as q, k, v
-  float* dtable_part;        // [B, 2T+1, H]
+  float* dtable_part;        // [B, 2T+1, H] (T' <= 256) / [parts, 2T+1, H] (windowed)
+  float* delta;              // [B, H, T] workspace of the windowed backward
+  int B;
 };
 
 constexpr int ROWPAD = 2;  // bf16 elements of row padding (bank spread)
@@ -697,7 +699,382 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
     }
   }
 }
+// ===========================================================================
+// Long sequences (T' > 256, e.g. the C5 config's T' = 513): the head no longer
+// fits LDS whole.  A workgroup owns 64 rows (one 16-row tile per wave) and
+// streams the other side through LDS in windows of AW_W rows by LDS-DMA (K/V
+// for the forward and the dQ pass, Q/dO for the dK/dV pass); the online softmax
+// (forward) and the register accumulators (backward) carry across windows.
+// Same per-element math, bias and causal mask as the whole-head kernels above.
+// delta = rowsum(dO * O) comes from attn_delta_k; the dQ pass also produces the
+// bias gradient, accumulated in LDS over AW_BG batch entries per workgroup and
+// written as one partial per (batch group, row block): no atomics to HBM.
+// ===========================================================================
+constexpr int AW_W = 128;  // window rows
+constexpr int AW_R = 64;   // rows owned by a workgroup
+constexpr int AW_BG = 16;  // batch entries per dQ / bias-gradient workgroup
+
+template <int E>
+__device__ __forceinline__ void fwd_kblock(const unsigned char* Ki, const unsigned char* Vi, int k0, int kimg, int q0,
+                                           const bf16x8v (&qf)[E / 32], f32x4 (&o)[E / 16], float (&m)[4],
+                                           float (&l)[4], const float* bias, float rs, int T, bool causal, float* scr,
+                                           int lane) {
+  constexpr int NS = E / 32, NE = E / 16;
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    s0 = MFMA(qf[s], img_row_frag<E>(Ki, kimg, s, lane), s0);
+    s1 = MFMA(qf[s], img_row_frag<E>(Ki, kimg + 16, s, lane), s1);
+  }
+  float bm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = q0 + rg + j;
+    const int ka = k0 + col, kb = k0 + 16 + col;
+    const bool va = q < T && ka < T && (!causal || ka <= q);
+    const bool vb = q < T && kb < T && (!causal || kb <= q);
+    s0[j] = va ? s0[j] * rs + bias[q - ka + T] : -INFINITY;
+    s1[j] = vb ? s1[j] * rs + bias[q - kb + T] : -INFINITY;
+    bm[j] = row16_max(fmaxf(s0[j], s1[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float mn = fmaxf(m[j], bm[j]);
+    const float alpha = (mn == -INFINITY) ? 1.f : __expf(m[j] - mn);
+    m[j] = mn;
+    const float pa = (s0[j] == -INFINITY) ? 0.f : __expf(s0[j] - mn);
+    const float pb = (s1[j] == -INFINITY) ? 0.f : __expf(s1[j] - mn);
+    s0[j] = pa;
+    s1[j] = pb;
+    l[j] = l[j] * alpha + pa + pb;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) o[e][j] *= alpha;
+  }
+  bf16x8v ph, pl;
+  c_to_a_split(scr, s0, s1, lane, ph, pl);
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const bf16x8v vf = img_tr_frag<E>(Vi, kimg, e * 16, lane);
+    o[e] = MFMA(ph, vf, o[e]);
+    o[e] = MFMA(pl, vf, o[e]);
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void attn_fwd_win_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NS = E / 32, NE = E / 16;
+  const int T = a.T, Tk = (T + 31) & ~31;
+  unsigned char* Ki = smem;
+  unsigned char* Vi = Ki + AW_W * E * 2;
+  float* bias = reinterpret_cast<float*>(Vi + AW_W * E * 2);  // [2T+1], region padded to 16 B
+  float* scr_all = bias + ((2 * T + 4) & ~3);
+  const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.y * AW_R, q0 = r0 + wave * 16;
+  const bool valid = q0 < T;
+  for (int i = tid; i <= 2 * T; i += 256) bias[i] = a.table ? a.table[(int64_t)i * a.H + h] : 0.f;
+  float* scr = scr_all + wave * 16 * SCR_LD;
+  const float rs = rsqrtf((float)E);
+  const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+  const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+  bf16x8v qf[NS];
+  glob_row_frags<E>(qf, a.q + b * a.q_bs + h * a.q_hs, a.q_ts, q0, T, lane);
+  f32x4 o[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) o[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
+  const int kend_blk = a.causal ? min(Tk, (r0 + AW_R + 31) & ~31) : Tk;
+  const int kend = a.causal ? min(Tk, (q0 + 16 + 31) & ~31) : Tk;
+  for (int w0 = 0; w0 < kend_blk; w0 += AW_W) {
+    const int wr = min(AW_W, kend_blk - w0);
+    __syncthreads();  // the previous window is consumed (first pass: the bias fill is done)
+    stage_img_dma<E>(Ki, kg + (int64_t)w0 * a.k_ts, a.k_ts, T - w0, wr, wave, lane);
+    stage_img_dma<E>(Vi, vg + (int64_t)w0 * a.v_ts, a.v_ts, T - w0, wr, wave, lane);
+    wait_vm<0>();
+    __syncthreads();
+    if (valid)
+      for (int k0 = w0; k0 < min(w0 + wr, kend); k0 += 32)
+        fwd_kblock<E>(Ki, Vi, k0, k0 - w0, q0, qf, o, m, l, bias, rs, T, a.causal != 0, scr, lane);
+  }
+  if (!valid) return;
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = q0 + rg + j;
+    const float lt = row16_sum(l[j]);
+    const float inv = 1.f / lt;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) o[e][j] *= inv;
+    if (q < T && col == 0) a.lse[((int64_t)b * a.H + h) * T + q] = m[j] + __logf(lt);
+  }
+#pragma unroll
+  for (int e = 0; e < NE; e += 2) c_store_rows(scr, o[e], o[e + 1], 1.f, lane, og + e * 16, a.o_ts, q0, T);
+}
+
+// delta[b, h, q] = dO[q] . O[q] (f32 over the bf16 operands), one thread per row
+template <int E>
+__global__ __launch_bounds__(256) void attn_delta_k(AttnArgs a) {
+  const int64_t n = (int64_t)a.B * a.H * a.T;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(i % a.T);
+    const int64_t bh = i / a.T;
+    const int h = (int)(bh % a.H);
+    const int64_t b = bh / a.H;
+    const bf16_t* dp = a.dout + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ts;
+    const bf16_t* op = a.o + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ts;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < E / 8; ++c) {
+      const u32x4 u = *reinterpret_cast<const u32x4*>(dp + c * 8);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(op + c * 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        d += __uint_as_float(u[k] << 16) * __uint_as_float(v[k] << 16) +
+             __uint_as_float(u[k] & 0xffff0000u) * __uint_as_float(v[k] & 0xffff0000u);
+    }
+    a.delta[i] = d;
+  }
+}
+
+// dQ (+ bias gradient) of 64 query rows, K / V streamed in windows
+template <int E>
+__global__ __launch_bounds__(256, 2) void attn_bwd_rows_win_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NS = E / 32, NE = E / 16;
+  const int T = a.T, Tk = (T + 31) & ~31;
+  unsigned char* I0 = smem;                 // K window
+  unsigned char* I1 = I0 + AW_W * E * 2;    // V window
+  float* bias = reinterpret_cast<float*>(I1 + AW_W * E * 2);  // [2T+2]
+  float* dbias = bias + 2 * T + 2;                            // [2T+2]
+  float* scr_all = dbias + 2 * T + 2;
+  const int h = blockIdx.x % a.H, bg = blockIdx.x / a.H, rc = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = rc * AW_R, q0 = r0 + wave * 16;
+  const bool valid = q0 < T;
+  for (int i = tid; i < 2 * T + 2; i += 256) bias[i] = (a.table && i <= 2 * T) ? a.table[(int64_t)i * a.H + h] : 0.f;
+  for (int i = tid; i < 2 * T + 2; i += 256) dbias[i] = 0.f;
+  float* scr = scr_all + wave * 16 * SCR_LD;
+  const float rs = rsqrtf((float)E);
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  const int kend_blk = a.causal ? min(Tk, (r0 + AW_R + 31) & ~31) : Tk;
+  const int kend = a.causal ? min(Tk, (q0 + 16 + 31) & ~31) : Tk;
+  const int b1 = min(a.B, (bg + 1) * AW_BG);
+  for (int b = bg * AW_BG; b < b1; ++b) {
+    const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+    const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+    bf16x8v qf[NS], df[NS];
+    glob_row_frags<E>(qf, a.q + b * a.q_bs + h * a.q_hs, a.q_ts, q0, T, lane);
+    glob_row_frags<E>(df, a.dout + b * a.o_bs + h * a.o_hs, a.o_ts, q0, T, lane);
+    float lq[4], dl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t qi = ((int64_t)b * a.H + h) * T + min(q0 + rg + j, T - 1);
+      lq[j] = a.lse[qi];
+      dl[j] = a.delta[qi];
+    }
+    f32x4 dq[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dq[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int w0 = 0; w0 < kend_blk; w0 += AW_W) {
+      const int wr = min(AW_W, kend_blk - w0);
+      __syncthreads();
+      stage_img_dma<E>(I0, kg + (int64_t)w0 * a.k_ts, a.k_ts, T - w0, wr, wave, lane);
+      stage_img_dma<E>(I1, vg + (int64_t)w0 * a.v_ts, a.v_ts, T - w0, wr, wave, lane);
+      wait_vm<0>();
+      __syncthreads();
+      if (!valid) continue;
+      for (int k0 = w0; k0 < min(w0 + wr, kend); k0 += 32) {
+        const int ki = k0 - w0;
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, p0 = s0, p1 = s0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          s0 = MFMA(qf[s], img_row_frag<E>(I0, ki, s, lane), s0);
+          s1 = MFMA(qf[s], img_row_frag<E>(I0, ki + 16, s, lane), s1);
+          p0 = MFMA(df[s], img_row_frag<E>(I1, ki, s, lane), p0);
+          p1 = MFMA(df[s], img_row_frag<E>(I1, ki + 16, s, lane), p1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = q0 + rg + j;
+          const int ka = k0 + col, kb = k0 + 16 + col;
+          const bool va = q < T && ka < T && (!a.causal || ka <= q);
+          const bool vb = q < T && kb < T && (!a.causal || kb <= q);
+          s0[j] = va ? __expf(s0[j] * rs + bias[q - ka + T] - lq[j]) * (p0[j] - dl[j]) : 0.f;
+          s1[j] = vb ? __expf(s1[j] * rs + bias[q - kb + T] - lq[j]) * (p1[j] - dl[j]) : 0.f;
+        }
+        bf16x8v gh, gl;
+        c_to_a_split(scr, s0, s1, lane, gh, gl);
+        if (a.dtable_part) {  // diagonal sums of the 16 x 32 dS tile, one LDS atomic per lane
+          const int dd = lane - 31;
+          const int idx = q0 - k0 + T + dd;
+          if (lane < 47 && idx >= 0 && idx <= 2 * T) {
+            float sum = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int c = r - dd;
+              if (c >= 0 && c < 32) sum += scr[r * SCR_LD + c];
+            }
+            atomicAdd(&dbias[idx], sum);
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const bf16x8v kf = img_tr_frag<E>(I0, ki, e * 16, lane);
+          dq[e] = MFMA(gh, kf, dq[e]);
+          dq[e] = MFMA(gl, kf, dq[e]);
+        }
+      }
+    }
+    if (valid) {
+      bf16_t* dqg = a.dq + b * a.q_bs + h * a.q_hs;
+#pragma unroll
+      for (int e = 0; e < NE; e += 2) c_store_rows(scr, dq[e], dq[e + 1], rs, lane, dqg + e * 16, a.q_ts, q0, T);
+    }
+  }
+  __syncthreads();
+  if (a.dtable_part)
+    for (int i = tid; i <= 2 * T; i += 256)
+      a.dtable_part[(((int64_t)bg * gridDim.y + rc) * (2 * T + 1) + i) * a.H + h] = dbias[i];
+}
+
+// dK and dV of 64 key rows, Q / dO (+ their lse, delta) streamed in windows
+template <int E>
+__global__ __launch_bounds__(256, 2) void attn_bwd_cols_win_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NS = E / 32, NE = E / 16;
+  const int T = a.T, Tk = (T + 31) & ~31;
+  unsigned char* I0 = smem;                 // Q window
+  unsigned char* I1 = I0 + AW_W * E * 2;    // dO window
+  float* bias = reinterpret_cast<float*>(I1 + AW_W * E * 2);  // [2T+2]
+  float* wl = bias + 2 * T + 2;                               // [AW_W] lse of the window rows
+  float* wd = wl + AW_W;                                      // [AW_W] delta of the window rows
+  float* scr_all = wd + AW_W;
+  const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c0 = blockIdx.y * AW_R, k0 = c0 + wave * 16;
+  const bool valid = k0 < T;
+  for (int i = tid; i < 2 * T + 2; i += 256) bias[i] = (a.table && i <= 2 * T) ? a.table[(int64_t)i * a.H + h] : 0.f;
+  float* scr = scr_all + wave * 16 * SCR_LD;
+  const float rs = rsqrtf((float)E);
+  const int col = lane & 15, rg = (lane >> 4) * 4;
+  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+  const bf16_t* dog = a.dout + b * a.o_bs + h * a.o_hs;
+  const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  const float* del_g = a.delta + ((int64_t)b * a.H + h) * T;
+  bf16x8v kf[NS], vf[NS];
+  glob_row_frags<E>(kf, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, k0, T, lane);
+  glob_row_frags<E>(vf, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, k0, T, lane);
+  f32x4 dk[NE], dv[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) { dk[e] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[e] = dk[e]; }
+  const int qbeg_blk = a.causal ? (c0 & ~31) : 0;
+  const int qbeg = a.causal ? (k0 & ~31) : 0;
+  for (int w0 = qbeg_blk; w0 < Tk; w0 += AW_W) {
+    const int wr = min(AW_W, Tk - w0);
+    __syncthreads();
+    stage_img_dma<E>(I0, qg + (int64_t)w0 * a.q_ts, a.q_ts, T - w0, wr, wave, lane);
+    stage_img_dma<E>(I1, dog + (int64_t)w0 * a.o_ts, a.o_ts, T - w0, wr, wave, lane);
+    for (int i = tid; i < wr; i += 256) {
+      wl[i] = w0 + i < T ? lse_g[w0 + i] : 0.f;
+      wd[i] = w0 + i < T ? del_g[w0 + i] : 0.f;
+    }
+    wait_vm<0>();
+    __syncthreads();
+    if (!valid) continue;
+    for (int q0 = max(w0, qbeg); q0 < w0 + wr; q0 += 32) {
+      const int qi = q0 - w0;
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, p0 = s0, p1 = s0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s0 = MFMA(kf[s], img_row_frag<E>(I0, qi, s, lane), s0);
+        s1 = MFMA(kf[s], img_row_frag<E>(I0, qi + 16, s, lane), s1);
+        p0 = MFMA(vf[s], img_row_frag<E>(I1, qi, s, lane), p0);
+        p1 = MFMA(vf[s], img_row_frag<E>(I1, qi + 16, s, lane), p1);
+      }
+      const int qa = q0 + col, qb = q0 + 16 + col;
+      const float la = wl[qi + col], lb = wl[qi + 16 + col], da_ = wd[qi + col], db_ = wd[qi + 16 + col];
+      f32x4 g0, g1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + rg + j;
+        const bool va = k < T && qa < T && (!a.causal || k <= qa);
+        const bool vb = k < T && qb < T && (!a.causal || k <= qb);
+        const float pa = va ? __expf(s0[j] * rs + bias[qa - k + T] - la) : 0.f;
+        const float pb = vb ? __expf(s1[j] * rs + bias[qb - k + T] - lb) : 0.f;
+        g0[j] = pa * (p0[j] - da_);
+        g1[j] = pb * (p1[j] - db_);
+        s0[j] = pa;
+        s1[j] = pb;
+      }
+      bf16x8v ph, pl, gh, gl;
+      c_to_a_split(scr, s0, s1, lane, ph, pl);
+      c_to_a_split(scr, g0, g1, lane, gh, gl);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const bf16x8v dof = img_tr_frag<E>(I1, qi, e * 16, lane);
+        dv[e] = MFMA(ph, dof, dv[e]);
+        dv[e] = MFMA(pl, dof, dv[e]);
+        const bf16x8v qf = img_tr_frag<E>(I0, qi, e * 16, lane);
+        dk[e] = MFMA(gh, qf, dk[e]);
+        dk[e] = MFMA(gl, qf, dk[e]);
+      }
+    }
+  }
+  if (!valid) return;
+  bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
+  bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
+#pragma unroll
+  for (int e = 0; e < NE; e += 2) {
+    c_store_rows(scr, dk[e], dk[e + 1], rs, lane, dkg + e * 16, a.k_ts, k0, T);
+    c_store_rows(scr, dv[e], dv[e + 1], 1.f, lane, dvg + e * 16, a.v_ts, k0, T);
+  }
+}
 #undef MFMA
+
+static size_t fwd_win_lds(int T, int E) {
+  return (size_t)2 * AW_W * E * 2 + (size_t)((2 * T + 4) & ~3) * 4 + (size_t)4 * 16 * SCR_LD * 4;
+}
+static size_t rows_win_lds(int T, int E) {
+  return (size_t)2 * AW_W * E * 2 + (size_t)(2 * T + 2) * 8 + (size_t)4 * 16 * SCR_LD * 4;
+}
+static size_t cols_win_lds(int T, int E) {
+  return (size_t)2 * AW_W * E * 2 + (size_t)(2 * T + 2) * 4 + (size_t)2 * AW_W * 4 + (size_t)4 * 16 * SCR_LD * 4;
+}
+// windowed path: T' beyond what one workgroup keeps in LDS whole
+static bool attn_windowed(int T) { return T > 256; }
+static int attn_row_blocks(int T) { return (T + AW_R - 1) / AW_R; }
+static int64_t attn_parts(int B, int T) {
+  return attn_windowed(T) ? (int64_t)((B + AW_BG - 1) / AW_BG) * attn_row_blocks(T) : (int64_t)B;
+}
+
+template <int E>
+static int attn_launch_win(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
+  const unsigned nrb = (unsigned)attn_row_blocks(a.T);
+  if (!bwd) {
+    const size_t sh = fwd_win_lds(a.T, E);
+    if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((attn_fwd_win_k<E>), dim3(B * a.H, nrb), dim3(256), sh, s, a);
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
+  const size_t sr = rows_win_lds(a.T, E), sc = cols_win_lds(a.T, E);
+  if (sr > 160 * 1024 || sc > 160 * 1024 || !a.delta) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((attn_delta_k<E>), dim3(grid_for((int64_t)B * a.H * a.T, 256, 256 * 16)), dim3(256), 0, s, a);
+  LTHM_CHECK_LAUNCH();
+  const unsigned nbg = (unsigned)((B + AW_BG - 1) / AW_BG);
+  hipLaunchKernelGGL((attn_bwd_rows_win_k<E>), dim3(nbg * a.H, nrb), dim3(256), sr, s, a);
+  LTHM_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd_cols_win_k<E>), dim3(B * a.H, nrb), dim3(256), sc, s, a);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
 
 static size_t fwd_mfma_lds(int T, int E) {
   const int Tk = (T + 31) & ~31;
@@ -745,6 +1122,14 @@ static int attn_launch(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
 }
 
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
+  if (attn_windowed(a.T)) {
+    switch (E) {
+      case 32: return attn_launch_win<32>(a, B, bwd, s);
+      case 64: return attn_launch_win<64>(a, B, bwd, s);
+      case 128: return attn_launch_win<128>(a, B, bwd, s);
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   switch (E) {
     case 16: return attn_launch<16>(a, B, bwd, s);
     case 32: return attn_launch_mfma<32>(a, B, bwd, s);
@@ -767,10 +1152,13 @@ static void fill_common(AttnArgs& a, const lthm_attn_desc* d) {
   a.table = d->table; a.lse = d->lse; a.T = d->T; a.H = d->H; a.causal = d->causal;
   a.dout = (const bf16_t*)d->dout; a.dq = (bf16_t*)d->dq; a.dk = (bf16_t*)d->dk; a.dv = (bf16_t*)d->dv;
   a.dtable_part = d->dtable_part;
+  a.delta = d->delta;
+  a.B = d->B;
 }
 
 static int check_desc(const lthm_attn_desc* d) {
-  if (!d || d->B < 0 || d->T <= 0 || d->T > 256 || d->H <= 0) return 1;
+  if (!d || d->B < 0 || d->T <= 0 || d->T > 4096 || d->H <= 0) return 1;
+  if (d->T > 256 && d->E == 16) return 1;  // the windowed path is MFMA-only (E = 32, 64, 128)
   if (d->table && d->table_rows < 2 * d->T + 1) return 1;
   if ((d->q_tok_stride % 8) || (d->k_tok_stride % 8) || (d->v_tok_stride % 8) || (d->o_tok_stride % 8)) return 1;
   // 16-B rows: LDS-DMA image staging and vector row stores
@@ -781,6 +1169,8 @@ static int check_desc(const lthm_attn_desc* d) {
     if ((uintptr_t)p % 16) return 1;
   return 0;
 }
+
+extern "C" int64_t lthm_attn_bwd_parts(int32_t B, int32_t T) { return attn_parts(B, T); }
 
 extern "C" int lthm_attn_fwd(const lthm_attn_desc* d, void* stream) {
   LTHM_REQUIRE(check_desc(d) == 0 && d->lse != nullptr && d->out != nullptr);

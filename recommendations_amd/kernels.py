@@ -275,7 +275,8 @@ def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True
 # ----------------------------------------------------------------- attention
 def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs):
     from ._lib import STRUCTS
-    _check(min(B, T, H, E) >= 1 and T <= 256, f"attention takes 1 <= T <= 256 (got B={B} T={T} H={H} E={E})")
+    _check(min(B, T, H, E) >= 1 and T <= 4096 and (T <= 256 or E in (32, 64, 128)),
+           f"attention takes 1 <= T <= 4096 (E in 32/64/128 beyond T = 256; got B={B} T={T} H={H} E={E})")
     _need(q, (B - 1) * T * q_ts + (T - 1) * q_ts + (H - 1) * E + E, "q")
     _need(k, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "k")
     _need(v, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "v")
@@ -314,15 +315,18 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
     import ctypes
     C = H * E
     dqkv = torch.empty_like(qkv)
-    part = torch.empty((B, 2 * T + 1, H), dtype=torch.float32, device=qkv.device) if table is not None else None
+    from ._lib import load
+    parts = int(load().lthm_attn_bwd_parts(B, T))
+    part = torch.empty((parts, 2 * T + 1, H), dtype=torch.float32, device=qkv.device) if table is not None else None
+    delta = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device) if T > 256 else None
     d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
     d.dout, d.dq, d.dk, d.dv = ptr(dout), ptr(dqkv), ptr(dqkv[:, C:]), ptr(dqkv[:, 2 * C:])
-    d.dtable_part = ptr(part)
+    d.dtable_part, d.delta = ptr(part), ptr(delta)
     call("lthm_attn_bwd", ctypes.addressof(d), stream(), _key="attn_bwd_k", _work=10.0 * B * H * T * T * E,
          _unit="flop")
     dtab = None
     if part is not None:
-        dtab = colsum(part.view(B, (2 * T + 1) * H)).view(2 * T + 1, H)
+        dtab = colsum(part.view(parts, (2 * T + 1) * H)).view(2 * T + 1, H)
     return dqkv, dtab
 
 
