@@ -92,6 +92,9 @@ CONFIGS = {
     # SURVEY §8 C3 per GPU: 100M-row item table row-sharded over the ranks, 64 categorical tables
     "c3": dict(B=4096, T=128, d=256, L=4, H=4, n_cat=64, cat_vocab=1_000_000, item_vocab=100_000_000,
                item_table_sharded=True),
+    # BASELINE.json configs[4]: long history, fp8 encoder GEMMs; 8-sequence loss
+    # mini-batches keep the in-batch logits at 8 x 512 = 4096 rows (C2's size)
+    "c5": dict(B=1024, T=512, d=512, L=6, H=8, n_cat=0, cat_vocab=1_000_000, item_vocab=1_000_000, fp8=True, mbs=8),
     # BASELINE.json configs[3]: ranker, 128 dense + 64 cat x 1M, interaction layers only
     "c4": dict(kind="ranker", B=65536, n_dense=128, n_cat=64, cat_vocab=1_000_000),
 }
@@ -109,7 +112,8 @@ def build(cfgd, dev):
         return cfg, model
     cfg = lthm_config(T=cfgd["T"], d=cfgd["d"], n_layers=cfgd["L"], n_head=cfgd["H"], cat_features=cfgd["n_cat"],
                       cat_vocab=cfgd["cat_vocab"], item_vocab=cfgd["item_vocab"],
-                      item_table_sharded=cfgd.get("item_table_sharded", False))
+                      item_table_sharded=cfgd.get("item_table_sharded", False), fp8=cfgd.get("fp8", False),
+                      train_mini_batch_size=cfgd.get("mbs", 32))
     model = LTHMModelBuilder(None, cfg).build().to(dev)
     return cfg, model
 
@@ -283,7 +287,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8-e4m3 fwd GEMMs / bf16" if cfgd.get("fp8") else "bf16",
         "data": ("synthetic (N(0,1) dense features, uniform int64 categorical ids, Bernoulli(0.1) clicks); "
                  "random-init weights" if ranker else
                  "synthetic (seeded full-range int64 item ids with 0-padding, labels 0..3, 2023 timestamps, "
@@ -293,7 +297,9 @@ def main():
                                 f"QuickGELU, BCE" if ranker else
                                 f"LTHM {args.config.upper()}: item KShift P={cfgd['item_vocab']} D=32 K=16, "
                                 f"{cfgd['n_cat']} cat x {cfgd['cat_vocab']} KShift D=32 K=8, T={cfgd['T']}, "
-                                f"d={cfgd['d']}, {cfgd['L']} layers, H={cfgd['H']}, 6 lookahead heads"),
+                                f"d={cfgd['d']}, {cfgd['L']} layers, H={cfgd['H']}, 6 lookahead heads"
+                                + (", fp8 e4m3 forward encoder GEMMs" if cfgd.get("fp8") else "")
+                                + (f", {cfgd['mbs']}-sequence loss mini-batches" if cfgd.get("mbs") else "")),
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
                    "parallelism": f"dp{world}" + (
                        (" (item table row-sharded, all_to_all row exchange; categorical tables replicated, "

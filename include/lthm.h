@@ -23,10 +23,11 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 10 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 11 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
+#define LTHM_FP8_E4M3 2 /* OCP e4m3fn (gfx950), GEMM operands only */
 
 /* KShift finalisation modes */
 #define LTHM_KSHIFT_SCALE 0      /* x / sqrt(K)               commons/layers.py:170 */
@@ -139,9 +140,24 @@ typedef struct lthm_gemm_desc {
   int32_t pad0;
   float* workspace;
   size_t workspace_bytes;
+  int32_t ab_dtype;
+  int32_t pad1;
+  const float* a_scale;
+  const float* b_scale;
 } lthm_gemm_desc;
 
+/* ab_dtype LTHM_BF16 (0 is read as bf16 too) or LTHM_FP8_E4M3: A [M, K] and B [N, K]
+ * both K-contiguous e4m3 bytes (lda / ldb in bytes), per-tensor device scales
+ * a_scale / b_scale (C = epi(alpha * a_scale * b_scale * A.B)); batch 1, no split-K,
+ * K % 128 == 0 -- the fp8 encoder GEMMs of the C5 config, on
+ * v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales. */
 int lthm_gemm(const lthm_gemm_desc* desc, void* stream);
+
+/* Per-tensor fp8 quantisation: scale = amax(|x|) / 448 (1 if x == 0),
+ * q = e4m3(clamp(x / scale, -448, 448)) round-to-nearest-even.  x: n f32 / bf16
+ * (n % 8 == 0, 16-B aligned); q: n bytes; scale: device f32; work: 4-byte scratch. */
+int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_t* q, float* scale, int32_t* work,
+                      void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm (commons/transformers/layers.py:142-149, eps 1e-5)               */

@@ -45,3 +45,5 @@ class TransformerConfig(BaseModel):
     sparsity_factor: float = 0.5
     enable_gradient_checkpointing: bool = False
     attn_config: SelfAttentionConfig
+    # build-defined (BASELINE configs[4], C5): forward encoder GEMMs on the fp8 MFMA
+    fp8_gemm: bool = False

@@ -36,22 +36,33 @@ class TransformerBlockFn(torch.autograd.Function):
     """x -> x + attn(ln_1 x) -> + mlp(ln_2 .)  [+ x again when double_residual]."""
 
     @staticmethod
-    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal, double_residual):
+    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal, double_residual,
+                fp8=False):
         require_gpu(x)
         B, T, d = x.shape
         E = d // H
         M = B * T
         x2 = x.contiguous().view(M, d)
         wqkv_b, wp_b, w1_b, w2_b = _bf(wqkv), _bf(wp), _bf(w1), _bf(w2)
+        if fp8:
+            # build-defined C5 mode: the four forward GEMMs take per-tensor-scaled e4m3
+            # operands on the fp8 MFMA; the backward runs bf16 on the saved activations
+            def lin(xb, wb, b, **kw):
+                xq, xs = K.quantize_fp8(xb)
+                wq, ws = K.quantize_fp8(wb)
+                return K.linear_fwd_fp8(xq, xs, wq, ws, b, **kw)
+        else:
+            def lin(xb, wb, b, **kw):
+                return K.linear_fwd(xb, wb, b, **kw)
         h1, mu1, rs1 = K.layernorm_fwd(x2, ln1w.detach(), _f(ln1b))
-        qkv = K.linear_fwd(h1, wqkv_b, _f(bqkv))
+        qkv = lin(h1, wqkv_b, _f(bqkv))
         tab = None if table is None else table.detach().contiguous()
         o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
-        x1 = K.linear_fwd(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
+        x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
-        g = K.linear_fwd(h2, w1_b, _f(b1), act=K.ACT_GELU, aux_out=pre)
-        out = K.linear_fwd(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
+        g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU, aux_out=pre)
+        out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
         ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
@@ -91,7 +102,7 @@ class TransformerBlockFn(torch.autograd.Function):
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
         return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
-                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None)
+                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None)
 
 
 # ------------------------------------------------------------------ modules
@@ -220,6 +231,7 @@ class TransformerBlock(nn.Module):
         if self.is_sparse:
             raise NotImplementedError("is_sparse_attn is disabled in every north-star config")
         self.enable_gradient_checkpointing = getattr(config, "enable_gradient_checkpointing", False)
+        self.fp8_gemm = bool(getattr(config, "fp8_gemm", False))  # build-defined (C5)
         self.null_connector = nn.Identity()
         self.register_buffer("input_mask_idx", torch.empty(0, dtype=torch.long), persistent=True)
         self.register_buffer("input_mask_not_idx", torch.empty(0, dtype=torch.long), persistent=True)
@@ -235,7 +247,8 @@ class TransformerBlock(nn.Module):
             raise ValueError("TransformerBlock expects [B, T, d]")
         if self.attn.attn.table is not None:
             self.attn.attn.pos_bias.check(x.shape[1], x.shape[1])
-        return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal, double_residual)
+        return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal, double_residual,
+                                        self.fp8_gemm)
 
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if attn_mask is not None:

@@ -43,6 +43,8 @@ struct GemmArgs {
   int out_dt;
   float* ws;           // split-K slabs [splits][M][N] f32 (when splits > 1)
   bool fast_ok;        // 16-B aligned operands and leading dims (interior-tile fast path)
+  const float* sa;     // fp8 per-tensor scales (device scalars), or null
+  const float* sb;
 };
 
 // tanh-GELU through r = 1 / (e^(2u) + 1), u = sqrt(2/pi) (x + 0.044715 x^3):
@@ -502,7 +504,21 @@ __device__ __forceinline__ void ps_epi_load(const GemmArgs& g, PsIn<EPI>& in, in
   }
 }
 
-template <bool KB, bool BRES, int EPI>
+typedef int i32x8v __attribute__((ext_vector_type(8)));
+// fp8 A/B fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row rbase + (l & 15),
+// k bytes 32 (l >> 4) .. + 31 = the two 16-B chunks 2 (l >> 4), 2 (l >> 4) + 1 of a 128-B row
+__device__ __forceinline__ i32x8v read_frag8(const unsigned char* lds, int rbase, int lane) {
+  const int r = rbase + (lane & 15), c = 2 * (lane >> 4);
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(lds + kc_off(r, c));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(lds + kc_off(r, c + 1));
+  return i32x8v{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
+// F8: A and B are e4m3 bytes; the host passes K and the leading dims in 2-byte units so
+// that the 16-KiB stage / B-slab / DMA geometry is byte-identical to the bf16 kernel (a
+// stage holds 128 k of fp8 instead of 64 k of bf16) and one 16x16x128 MFMA (unit block
+// scales) replaces the two 16x16x32 steps; the per-tensor scales fold into alpha.
+template <bool KB, bool BRES, int EPI, bool F8 = false>
 __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles_m, int tiles_n, int R) {
   __shared__ __attribute__((aligned(16))) PsSmem<BRES> sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -573,6 +589,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float* stg = sh.stg[wave];
+  const float alpha = F8 ? g.alpha * *g.sa * *g.sb : g.alpha;
 
   int kk = 0, ti = 0;
   for (int s = 0; s < S; ++s) {
@@ -581,17 +598,31 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
     asm volatile("" ::: "memory");
     const unsigned char* sa = sh.ring[s % PS_NST];
     const unsigned char* sb = BRES ? sh.bslab[kk] : sa + TILE_BYTES;
+    if constexpr (F8) {
+      i32x8v af[4], bfr[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8v af[4], bfr[4];
+      for (int i = 0; i < 4; ++i) af[i] = read_frag8(sa, wm * 64 + i * 16, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<true>(sa, wm * 64 + i * 16, s2, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<KB>(sb, wn * 64 + j * 16, s2, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag8(sb, wn * 64 + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8v af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = read_frag<true>(sa, wm * 64 + i * 16, s2, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = read_frag<KB>(sb, wn * 64 + j * 16, s2, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
     if (++kk < NK) continue;
     // ---- tile done: per-wave epilogue, 16 rows at a time through the wave's strip
@@ -621,7 +652,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
         const PsIn<EPI>& q = in[i & 1];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = g.alpha * v[e] + bias[e];
+        for (int e = 0; e < 8; ++e) v[e] = alpha * v[e] + bias[e];
         const bool ok = row < g.M && col0 < g.N;
         if constexpr (EPI == EPI_ACT) {
           if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, v);
@@ -815,6 +846,8 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   g.res1 = d->res1; g.res2 = d->res2; g.ldr1 = d->ldr1 > 0 ? d->ldr1 : d->N; g.ldr2 = d->ldr2 > 0 ? d->ldr2 : d->N;
   g.res1_dt = d->res1_dtype; g.res2_dt = d->res2_dtype; g.out_dt = d->out_dtype;
   g.ws = (splits > 1) ? d->workspace : nullptr;
+  g.sa = nullptr;
+  g.sb = nullptr;
   g.fast_ok = ((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0 && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
               d->sA % 8 == 0 && d->sB % 8 == 0;
   if (splits > 1) {
@@ -861,6 +894,34 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     else if ((act == LTHM_ACT_GELU_GRAD || act == LTHM_ACT_QGELU_GRAD) && !d->bias && !d->res1 && !d->res2) epi = EPI_GRAD;
     else if (act == LTHM_ACT_NONE && r1 && !d->res2) epi = EPI_RES1;
     else if (act == LTHM_ACT_NONE && r1 && r2) epi = EPI_RES2;
+  }
+  if (d->ab_dtype == LTHM_FP8_E4M3) {
+    // fp8 encoder GEMMs: persistent kernel only, geometry in 2-byte units
+    LTHM_REQUIRE(epi >= 0 && ka && kb && splits == 1 && d->batch == 1 && d->K % 128 == 0 && d->K > 0);
+    LTHM_REQUIRE(d->a_scale && d->b_scale && d->lda % 16 == 0 && d->ldb % 16 == 0 && d->N % 8 == 0);
+    LTHM_REQUIRE(((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0 && tiles_n <= per_xcd);
+    GemmArgs g8 = g;
+    g8.K = d->K / 2; g8.lda = d->lda / 2; g8.ldb = d->ldb / 2;
+    g8.sa = d->a_scale; g8.sb = d->b_scale;
+    const int R = per_xcd / tiles_n;
+    dim3 grid(8 * R * tiles_n);
+    const bool bres = g8.K <= 4 * BK;
+#define LTHM_PS8(BRES_, EPI_) \
+  hipLaunchKernelGGL((gemm_ps_k<true, BRES_, EPI_, true>), grid, dim3(PS_THREADS), 0, s, g8, tiles_m, tiles_n, R)
+#define LTHM_PS8_EPI(BRES_)                              \
+  switch (epi) {                                         \
+    case EPI_PLAIN: LTHM_PS8(BRES_, EPI_PLAIN); break;   \
+    case EPI_ACT: LTHM_PS8(BRES_, EPI_ACT); break;       \
+    case EPI_GRAD: LTHM_PS8(BRES_, EPI_GRAD); break;     \
+    case EPI_RES1: LTHM_PS8(BRES_, EPI_RES1); break;     \
+    default: LTHM_PS8(BRES_, EPI_RES2); break;           \
+  }
+    if (bres) { LTHM_PS8_EPI(true) }
+    else { LTHM_PS8_EPI(false) }
+#undef LTHM_PS8_EPI
+#undef LTHM_PS8
+    LTHM_CHECK_LAUNCH();
+    return 0;
   }
   if (lthm_gemm_ps_mode() && epi >= 0 && ka && splits == 1 && d->batch == 1 && g.fast_ok && d->K % BK == 0 &&
       d->K > 0 && d->N % 8 == 0 && tiles_n <= per_xcd && (int64_t)tiles_m * tiles_n >= 4 * 8 * per_xcd) {

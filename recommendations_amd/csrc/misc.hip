@@ -237,3 +237,73 @@ extern "C" int lthm_bce_logits_bwd(const float* z, const float* y, int64_t n, co
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- fp8 quantisation
+namespace lthm {
+template <typename T>
+__global__ __launch_bounds__(256) void amax_k(const T* __restrict__ x, int64_t n8, unsigned* __restrict__ amax) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      load_vec<T, 16>(x + i * 8, v);
+    } else {
+      load_vec<T, 16>(x + i * 8, v);
+      load_vec<T, 16>(x + i * 8 + 4, v + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+template <typename T>
+__global__ __launch_bounds__(256) void quant_fp8_k(const T* __restrict__ x, int64_t n8, const unsigned* __restrict__ amax,
+                                                   uint8_t* __restrict__ q, float* __restrict__ scale) {
+  const float am = __uint_as_float(*amax);
+  const float s = am > 0.f ? am / 448.f : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale = s;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      load_vec<T, 16>(x + i * 8, v);
+    } else {
+      load_vec<T, 16>(x + i * 8, v);
+      load_vec<T, 16>(x + i * 8 + 4, v + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e] / s, -448.f), 448.f);
+    u32x2 w;
+    w[0] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    w[0] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], (int)w[0], true);
+    w[1] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+    w[1] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], (int)w[1], true);
+    *reinterpret_cast<u32x2*>(q + i * 8) = w;
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_t* q, float* scale, int32_t* work,
+                                 void* stream) {
+  LTHM_REQUIRE(n >= 0 && n % 8 == 0 && q && scale && work);
+  LTHM_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
+  LTHM_REQUIRE(dtype == LTHM_F32 || dtype == LTHM_BF16);
+  hipStream_t s = (hipStream_t)stream;
+  LTHM_REQUIRE(hipMemsetAsync(work, 0, 4, s) == hipSuccess);
+  const int64_t n8 = n / 8;
+  const int grid = grid_for(n8 > 0 ? n8 : 1, 256, 256 * 8);
+  if (dtype == LTHM_BF16) {
+    if (n8) hipLaunchKernelGGL((amax_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, n8, (unsigned*)work);
+    hipLaunchKernelGGL((quant_fp8_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, n8, (const unsigned*)work,
+                       q, scale);
+  } else {
+    if (n8) hipLaunchKernelGGL((amax_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, n8, (unsigned*)work);
+    hipLaunchKernelGGL((quant_fp8_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, n8, (const unsigned*)work,
+                       q, scale);
+  }
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -154,8 +154,9 @@ def _workspace(dev, nbytes: int) -> torch.Tensor:
 
 def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, out=None,
          out_dtype=torch.bfloat16, ldc=None, alpha=1.0, bias=None, act=ACT_NONE, aux=None, aux_out=None,
-         res1=None, res2=None, batch=1, sA=0, sB=0, sC=0, splits=1):
-    """C = epi(alpha * A.B) on the MFMA GEMM kernel (include/lthm.h lthm_gemm)."""
+         res1=None, res2=None, batch=1, sA=0, sB=0, sC=0, splits=1, a_scale=None, b_scale=None):
+    """C = epi(alpha * A.B) on the MFMA GEMM kernel (include/lthm.h lthm_gemm).  uint8
+    A / B are fp8 e4m3 bytes with per-tensor device scales a_scale / b_scale."""
     from ._lib import STRUCTS
     require_gpu(A, B)
     dev = A.device
@@ -195,10 +196,42 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
         ws = _workspace(dev, splits * batch * M * N * 4)
         d.workspace, d.workspace_bytes = ptr(ws), ws.numel() * 4
     d.splits = splits
+    fp8 = A.dtype == torch.uint8
+    if fp8:
+        _check(B.dtype == torch.uint8 and a_scale is not None and b_scale is not None,
+               "fp8 GEMM takes uint8 (e4m3) A and B with device scales")
+        d.ab_dtype, d.a_scale, d.b_scale = FP8_E4M3, ptr(a_scale), ptr(b_scale)
     import ctypes
-    call("lthm_gemm", ctypes.addressof(d), stream(), _key=f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>",
+    call("lthm_gemm", ctypes.addressof(d), stream(),
+         _key="gemm_fp8" if fp8 else f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>",
          _work=2.0 * M * N * K * batch, _unit="flop")
     return out
+
+
+FP8_E4M3 = 2
+
+
+def quantize_fp8(x):
+    """Per-tensor e4m3 quantisation (include/lthm.h lthm_quantize_fp8): -> (q uint8 of
+    x's shape, scale f32 [1] on the device) with x = q * scale up to e4m3 rounding."""
+    require_gpu(x)
+    n = x.numel()
+    _check(n % 8 == 0, "quantize_fp8 takes n % 8 == 0")
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    scale = torch.empty(1, dtype=torch.float32, device=x.device)
+    work = torch.empty(1, dtype=torch.int32, device=x.device)
+    call("lthm_quantize_fp8", ptr(x), dcode(x), n, ptr(q), ptr(scale), ptr(work), stream(), _key="quantize_fp8",
+         _work=n * (x.element_size() * 2 + 1), _unit="byte")
+    return q, scale
+
+
+def linear_fwd_fp8(xq, xs, wq, ws, bias=None, act=ACT_NONE, aux_out=None, res1=None, res2=None,
+                   out_dtype=torch.bfloat16):
+    """y = act(xs ws (xq wq^T) + b) (+ res1 + res2) on the fp8 MFMA: xq [M, K], wq [N, K] e4m3 bytes."""
+    M, K_ = xq.shape
+    N = wq.shape[0]
+    return gemm(xq, wq, M, N, K_, bias=bias, act=act, aux_out=aux_out, res1=res1, res2=res2, out_dtype=out_dtype,
+                a_scale=xs, b_scale=ws)
 
 
 def _splits_for(M: int, N: int, K: int) -> int:
@@ -435,10 +468,22 @@ def small_table_bwd(rows, dY, R, out=None):
     _check(rows.dtype == torch.int16 and dY.numel() == n * D, "rows must be int16 [n, nidx] and dY [n, D]")
     _check(0 < nidx <= 64 and 0 < R < 0xFFFF, f"small_table_bwd takes nidx <= 64 slots and R < 65535 rows")
     mfma = D in (16, 32, 64, 128, 256) and nidx <= 8 and R <= 8192
-    _check(mfma or R * 64 * 4 <= 160 * 1024, f"R={R} rows exceed the LDS slice; use segmented_table_bwd")
+    wide = D > 256 and D % 256 == 0 and nidx <= 8 and R <= 8192
+    _check(mfma or wide or R * 64 * 4 <= 160 * 1024, f"R={R} rows exceed the LDS slice; use segmented_table_bwd")
     if out is None:
         out = torch.zeros((R, D), dtype=torch.float32, device=dY.device)
     _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
+    if wide:
+        # d_model > 256 (C5: 512): the one-hot MFMA reduction over 256-column slices of dY
+        dYc = dY.contiguous()
+        for c0 in range(0, D, 256):
+            part = zeros((R, 256), torch.float32, dY.device)
+            ws, wsb = _table_ws(dY.device, n, R, 256)
+            call("lthm_table_bwd_mfma", ptr(rows), nidx, R, dYc.data_ptr() + c0 * dYc.element_size(), dcode(dYc), D,
+                 n, 256, ptr(part), ptr(ws) if ws is not None else None, wsb, stream(), _key="table_bwd_mfma_k",
+                 _work=2.0 * n * 256 * R * (2 if dY.dtype == torch.float32 else 1), _unit="flop")
+            out[:, c0:c0 + 256] += part
+        return out
     ws, wsb = _table_ws(dY.device, n, R, D)
     if mfma:
         # one-hot MFMA reduction (f32 dY split into bf16 hi + lo): no LDS atomics
@@ -594,7 +639,8 @@ def cve_table_bwd(rows, dY, R, modules, out=None):
     D = dY.shape[-1]
     _check(rows.dtype == torch.int16 and dY.dtype in (torch.bfloat16, torch.float32) and dY.numel() == n * D,
            "rows must be int16 [n, nidx] and dY bf16 / f32 [n, D]")
-    _check(D in (16, 32, 64, 128, 256), f"cve_table_bwd takes D in 16..256 (power of two), got {D}")
+    _check(D in (16, 32, 64, 128, 256) or D % 256 == 0,
+           f"cve_table_bwd takes D in 16..256 (power of two) or a multiple of 256, got {D}")
     _check(0 < len(modules) <= 16, "1..16 modules")
     for s0, ns, r0, rps in modules:
         _check(0 <= s0 and ns > 0 and s0 + ns <= nidx, f"module slots ({s0}, {ns}) outside [0, {nidx})")
@@ -602,8 +648,20 @@ def cve_table_bwd(rows, dY, R, modules, out=None):
     if out is None:
         out = zeros((R, D), torch.float32, dY.device)
     _check(out.dtype == torch.float32 and tuple(out.shape) == (R, D), "out must be float32 [R, D]")
-    ws, wsb = _table_ws(dY.device, n, R, D)
     m = _np.ascontiguousarray(_np.array(modules, dtype=_np.int32).T)
+    if D > 256:
+        # d_model > 256 (C5: 512): the one-hot MFMA reduction over 256-column slices of dY
+        dYc = dY.contiguous()
+        ws, wsb = _table_ws(dY.device, n, R, 256)
+        for c0 in range(0, D, 256):
+            part = zeros((R, 256), torch.float32, dY.device)
+            call("lthm_cve_table_bwd", ptr(rows), nidx, m.shape[1], m[0].ctypes.data, m[1].ctypes.data,
+                 m[2].ctypes.data, m[3].ctypes.data, dYc.data_ptr() + c0 * dYc.element_size(), dcode(dYc), D, n, 256,
+                 ptr(part), ptr(ws) if ws is not None else None, wsb, stream(), _key="cve_tab_bwd_k",
+                 _work=2.0 * n * 256 * sum(ns * rps for _, ns, _, rps in modules), _unit="flop")
+            out[:, c0:c0 + 256] += part
+        return out
+    ws, wsb = _table_ws(dY.device, n, R, D)
     call("lthm_cve_table_bwd", ptr(rows), nidx, m.shape[1], m[0].ctypes.data, m[1].ctypes.data, m[2].ctypes.data,
          m[3].ctypes.data, ptr(dY), dcode(dY), D, n, D, ptr(out), ptr(ws) if ws is not None else None, wsb, stream(),
          _key="cve_tab_bwd_k", _work=2.0 * n * D * sum(ns * rps for _, ns, _, rps in modules), _unit="flop")

@@ -91,7 +91,7 @@ class ProductTowerFn(torch.autograd.Function):
         dw_map = K.linear_wgrad(de, xn)
         db_map = K.colsum(de) if has_b else None
         R = R_cve + max(nb, 1)
-        if Dout in (16, 32, 64, 128, 256) and len(ctx.modules) <= 16:
+        if (Dout in (16, 32, 64, 128, 256) or Dout % 256 == 0) and len(ctx.modules) <= 16:
             dtab = K.cve_table_bwd(rows, de, R, ctx.modules)
         else:
             segs = []
