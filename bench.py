@@ -30,30 +30,39 @@ BF16_PEAK_TFLOPS = 2500.0
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-PMC_KERNELS = {
-    "cl_bwd_k": ["cl_bwd_k<true>", "cl_bwd_k<false>"],
-    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<true>", "cl_stats_k"],
-    "attn_bwd_k": ["attn_bwd_mfma_k<64>"],
-    "attn_fwd_k": ["attn_fwd_mfma_k<64>"],
-    "gemm_k<1,1>": ["gemm_k<true, true>"],
-    "gemm_k<1,0>": ["gemm_k<true, false>"],
-    "gemm_k<0,0>": ["gemm_k<false, false>", "splitk_reduce_k"],
-    "cve_tab_bwd_k": ["cve_tab_bwd_k<256>", "seg_tab_reduce_k"],
-    "lthm_product_tower_fwd": ["ptower_fwd_k<float, unsigned short, 4>"],
+PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
+    "cl_bwd_k": ["cl_bwd_k<", "cl_shift_k"],
+    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_stats_k"],
+    "attn_bwd_k": ["attn_bwd_mfma_k<", "attn_bwd_rows_win_k<", "attn_bwd_cols_win_k<", "attn_delta_k<"],
+    "attn_fwd_k": ["attn_fwd_mfma_k<", "attn_fwd_win_k<"],
+    "gemm_k<1,1>": ["gemm_k<true, true>", "gemm_ps_k<true, "],
+    "gemm_k<1,0>": ["gemm_k<true, false>", "gemm_ps_k<false, "],
+    "gemm_k<0,0>": ["gemm_k<false, false>", "gemm_wg_k", "splitk_reduce_k"],
+    "cve_tab_bwd_k": ["cve_tab_bwd_k<", "seg_tab_reduce_k"],
+    "lthm_product_tower_fwd": ["ptower_"],
 }
+PMC_STEPS = 3  # tools/pmc_passes.sh profiles `bench.py --steps 2 --warmup 1`
 
 
-def pmc_traffic(key):
-    """HBM bytes per call of `key` from the committed PMC summary (FETCH_SIZE x 2 +
-    WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None if the kernel was not profiled."""
+def pmc_traffic(key, calls_per_step):
+    """HBM bytes per call of `key` from the committed PMC summary: FETCH_SIZE x 2 +
+    WRITE_SIZE (MI355X_MICROARCH.md §HBM) of every dispatch of the kernels the call
+    launches, over the calls the profiled run made; None if not profiled."""
     try:
         with open(PMC_SUMMARY) as f:
             pmc = json.load(f)
     except OSError:
         return None
-    names = PMC_KERNELS.get(key, [key])
-    vals = [pmc[n]["hbm_bytes"] for n in names if n in pmc and "hbm_bytes" in pmc[n]]
-    return float(sum(vals)) if vals else None
+    prefixes = PMC_KERNELS.get(key, [key])
+    tot = 0.0
+    hit = False
+    for name, v in pmc.items():
+        if any(name.startswith(pf) for pf in prefixes) and "hbm_bytes" in v:
+            tot += v["hbm_bytes"] * v.get("dispatches", 1)
+            hit = True
+    if not hit or calls_per_step <= 0:
+        return None
+    return tot / (calls_per_step * PMC_STEPS)
 
 
 def embedding_gather_hbm(dev, P=4_000_000, D=128, K=16, n=524_288, iters=10):
@@ -331,7 +340,7 @@ def main():
             ach, peak, unit, bound = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
         else:
             ach, peak, unit, bound = per_launch / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s", "mfma"
-        traffic = pmc_traffic(dom)
+        traffic = pmc_traffic(dom, s["calls"] / args.steps)
         res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                            "frac": round(ach / peak, 4),
                            "traffic": round(traffic) if traffic is not None else None,
