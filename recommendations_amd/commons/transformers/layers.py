@@ -189,6 +189,93 @@ class SelfAttention(nn.Module):
         return MultiHeadAttention(config)
 
 
+def _mask_is_causal(mask: Optional[torch.Tensor], T: int) -> bool:
+    """True for the reference's causal additive mask (commons/transformers/layers.py:
+    397-402: -inf above the diagonal and the constant 1.0 elsewhere, a softmax-invariant
+    shift); other additive masks are not fused in the kernel."""
+    if mask is None:
+        return False
+    m = mask.reshape(-1, T, T)
+    tri = torch.ones((T, T), dtype=torch.bool, device=mask.device).triu(1)
+    kept = m[:, ~tri]
+    if not (bool(torch.isneginf(m[:, tri]).all()) and bool((kept == kept.reshape(-1)[0]).all())):
+        raise NotImplementedError("additive attention masks other than the causal mask are not fused in the kernel")
+    return True
+
+
+class _SelfAttnFn(torch.autograd.Function):
+    """Standalone attention module forward/backward on the HIP kernels:
+    MHA (commons/transformers/layers.py:247-265: c_attn -> SDPA -> c_proj) when
+    ``shared_kv`` is False, MQA (:214-234: q_proj, kv_proj with one K/V head,
+    out_proj) when True.  The MQA backward runs the multi-head kernel on K/V
+    expanded per head and sums their gradients over the heads."""
+
+    @staticmethod
+    def forward(ctx, x, w_in, b_in, w_kv, b_kv, w_out, b_out, table, H, causal, shared_kv):
+        require_gpu(x)
+        B, T, C = x.shape
+        E = C // H
+        M = B * T
+        xb = K.cast(x.contiguous().view(M, C), torch.bfloat16)
+        w_in_b, w_out_b = _bf(w_in), _bf(w_out)
+        tab = None if table is None else table.detach().contiguous()
+        if shared_kv:
+            w_kv_b = _bf(w_kv)
+            q = K.linear_fwd(xb, w_in_b, _f(b_in))
+            kv = K.linear_fwd(xb, w_kv_b, _f(b_kv))
+            o, lse = K.attn_fwd_mqa(q, kv, B, T, H, E, tab, causal)
+            saved = (xb, q, kv, o, lse, w_in_b, w_kv_b, w_out_b)
+        else:
+            qkv = K.linear_fwd(xb, w_in_b, _f(b_in))
+            o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
+            saved = (xb, qkv, o, lse, w_in_b, w_out_b)
+        y = K.linear_fwd(o, w_out_b, _f(b_out), out_dtype=torch.float32)
+        ctx.save_for_backward(*saved, tab)
+        ctx.cfg = (B, T, C, H, E, causal, shared_kv, b_in is not None, b_kv is not None, b_out is not None,
+                   None if table is None else table.shape)
+        return y.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, T, C, H, E, causal, shared_kv, has_bin, has_bkv, has_bout, tshape = ctx.cfg
+        M = B * T
+        saved = ctx.saved_tensors
+        tab = saved[-1]
+        dy = dy.contiguous().view(M, C).float()
+        dyb = K.cast(dy, torch.bfloat16)
+        if shared_kv:
+            xb, q, kv, o, lse, w_in_b, w_kv_b, w_out_b = saved[:-1]
+        else:
+            xb, qkv, o, lse, w_in_b, w_out_b = saved[:-1]
+        dw_out = K.linear_wgrad(dyb, o)
+        db_out = K.colsum(dy) if has_bout else None
+        do = K.linear_dgrad(dyb, w_out_b)
+        dw_kv = db_kv = None
+        if shared_kv:
+            qkv_e = torch.cat([q, kv[:, :E].repeat(1, H), kv[:, E:].repeat(1, H)], dim=1).contiguous()
+            dqkv, dtab = K.attn_bwd_qkv(qkv_e, o, do, lse, B, T, H, E, tab, causal)
+            dq = dqkv[:, :C].contiguous()
+            dkv = torch.cat([dqkv[:, C:2 * C].float().view(M, H, E).sum(1),
+                             dqkv[:, 2 * C:].float().view(M, H, E).sum(1)], dim=1).contiguous()
+            dkvb = K.cast(dkv, torch.bfloat16)
+            dw_in = K.linear_wgrad(dq, xb)
+            db_in = K.colsum(dq) if has_bin else None
+            dw_kv = K.linear_wgrad(dkvb, xb)
+            db_kv = K.colsum(dkv) if has_bkv else None
+            dx = K.linear_dgrad(dq, w_in_b, out_dtype=torch.float32)
+            dx = K.linear_dgrad(dkvb, w_kv_b, out_dtype=torch.float32, res1=dx)
+        else:
+            dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+            dw_in = K.linear_wgrad(dqkv, xb)
+            db_in = K.colsum(dqkv) if has_bin else None
+            dx = K.linear_dgrad(dqkv, w_in_b, out_dtype=torch.float32)
+        dtable = None
+        if tshape is not None:
+            dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
+            dtable[: dtab.shape[0]] = dtab
+        return dx.view(B, T, C), dw_in, db_in, dw_kv, db_kv, dw_out, db_out, dtable, None, None, None
+
+
 class MultiHeadAttention(SelfAttention):
     """commons/transformers/layers.py:237-265."""
 
@@ -200,6 +287,37 @@ class MultiHeadAttention(SelfAttention):
         self.resid_dropout = nn.Dropout(config.dropout)
         self.n_head = config.n_head
         self.n_embd = config.n_embd
+
+    def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        T = x.shape[1]
+        if self.attn.table is not None:
+            self.attn.pos_bias.check(T, T)
+        causal = _mask_is_causal(mask, T)
+        return _SelfAttnFn.apply(x.float(), self.c_attn.weight, self.c_attn.bias, None, None, self.c_proj.weight,
+                                 self.c_proj.bias, self.attn.table, self.n_head, causal, False)
+
+
+class MultiQueryAttention(SelfAttention):
+    """commons/transformers/layers.py:202-234: query heads share one K/V head."""
+
+    def __init__(self, config):
+        super().__init__(config)
+        self.q_proj = nn.Linear(config.n_embd, config.n_embd, bias=config.bias)
+        self.kv_proj = nn.Linear(config.n_embd, 2 * (config.n_embd // config.n_head), bias=config.bias)
+        self.out_proj = nn.Linear(config.n_embd, config.n_embd, bias=config.bias)
+        self.attn_dropout = nn.Dropout(config.attn_dropout)
+        self.resid_dropout = nn.Dropout(config.dropout)
+        self.n_head = config.n_head
+        self.n_embd = config.n_embd
+
+    def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        T = x.shape[1]
+        if self.attn.table is not None:
+            self.attn.pos_bias.check(T, T)
+        causal = _mask_is_causal(mask, T)
+        return _SelfAttnFn.apply(x.float(), self.q_proj.weight, self.q_proj.bias, self.kv_proj.weight,
+                                 self.kv_proj.bias, self.out_proj.weight, self.out_proj.bias, self.attn.table,
+                                 self.n_head, causal, True)
 
 
 class _MLP(nn.Module):
@@ -228,13 +346,27 @@ class TransformerBlock(nn.Module):
         hidden_mult = config.rotator_config if isinstance(config.rotator_config, (int, float)) else 4
         self.mlp = _MLP(attn_cfg.n_embd, attn_cfg.bias, attn_cfg.dropout, hidden_mult)
         self.is_sparse = getattr(config, "is_sparse_attn", False)
-        if self.is_sparse:
-            raise NotImplementedError("is_sparse_attn is disabled in every north-star config")
         self.enable_gradient_checkpointing = getattr(config, "enable_gradient_checkpointing", False)
         self.fp8_gemm = bool(getattr(config, "fp8_gemm", False))  # build-defined (C5)
-        self.null_connector = nn.Identity()
-        self.register_buffer("input_mask_idx", torch.empty(0, dtype=torch.long), persistent=True)
-        self.register_buffer("input_mask_not_idx", torch.empty(0, dtype=torch.long), persistent=True)
+        if self.is_sparse:
+            # :352-368: a seeded permutation keeps n_cls + sparsity_factor * max_block_size
+            # tokens for the block; the rest go through the null connector Linear
+            max_block_size = config.max_block_size
+            n_non_zeros = int(config.sparsity_factor * max_block_size)
+            g = torch.Generator()
+            if seed is not None:
+                g.manual_seed(seed)
+            perm = torch.randperm(max_block_size, generator=g)
+            full_mask = torch.cat((torch.arange(0, n_cls, dtype=torch.long), perm[n_cls:]), dim=0)
+            idx_sorted, _ = full_mask[:n_non_zeros].sort()
+            not_idx_sorted, _ = full_mask[n_non_zeros:].sort()
+            self.register_buffer("input_mask_idx", idx_sorted, persistent=True)
+            self.register_buffer("input_mask_not_idx", not_idx_sorted, persistent=True)
+            self.null_connector = nn.Linear(attn_cfg.n_embd, attn_cfg.n_embd, bias=attn_cfg.bias)
+        else:
+            self.null_connector = nn.Identity()
+            self.register_buffer("input_mask_idx", torch.empty(0, dtype=torch.long), persistent=True)
+            self.register_buffer("input_mask_not_idx", torch.empty(0, dtype=torch.long), persistent=True)
 
     def _args(self):
         a, m = self.attn, self.mlp
@@ -253,9 +385,34 @@ class TransformerBlock(nn.Module):
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if attn_mask is not None:
             raise NotImplementedError("additive attn_mask: only the causal mask is fused in the kernel")
-        # Activation checkpointing is unnecessary at 288 GB HBM: the fused op keeps
-        # its bf16 activations, and recompute would give the same numbers.
-        return self._fused(x, False)
+        # Activation checkpointing (:375-380) changes memory, not numbers: at 288 GB HBM
+        # the fused op keeps its bf16 activations instead of recomputing them.
+        if not self.is_sparse:
+            return self._fused(x, False)
+        return self._sparse_forward(x)
+
+    def _null(self, x):
+        from ...models.lthm.sequence.query_tower import LinearFn
+        shp = x.shape
+        y = LinearFn.apply(x.reshape(-1, shp[-1]).float().contiguous(), self.null_connector.weight,
+                           self.null_connector.bias)
+        return y.float().view(shp)
+
+    def _sparse_forward(self, x_orig: torch.Tensor) -> torch.Tensor:
+        """:383-420: the dense block on the kept tokens (gather), the null connector on the
+        others, scattered back into place."""
+        T = x_orig.size(1)
+        idx = self.input_mask_idx[self.input_mask_idx < T]
+        if idx.numel() <= 1:
+            return x_orig + self._null(x_orig)
+        not_idx = self.input_mask_not_idx[self.input_mask_not_idx < T]
+        x = self._fused(x_orig[:, idx].contiguous(), False)
+        x_final = torch.zeros_like(x_orig)
+        x_final[:, idx] = x
+        if not_idx.numel():
+            rest = x_orig[:, not_idx]
+            x_final[:, not_idx] = rest + self._null(rest)
+        return x_final
 
     def forward_double_residual(self, x: torch.Tensor) -> torch.Tensor:
         """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137)."""

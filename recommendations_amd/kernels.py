@@ -343,6 +343,21 @@ def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True):
     return out, lse
 
 
+def attn_fwd_mqa(q, kv, B, T, H, E, table=None, causal=True):
+    """Multi-query attention forward: q bf16 [B*T, H*E], kv bf16 [B*T, 2E] (one K/V head
+    shared by all query heads: head stride 0) -> out bf16 [B*T, H*E], lse f32 [B, H, T]."""
+    import ctypes
+    require_gpu(q, kv)
+    C = H * E
+    _check(q.shape[-1] == C and kv.shape[-1] == 2 * E, "attn_fwd_mqa takes q [M, H*E] and kv [M, 2E]")
+    out = torch.empty((B * T, C), dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty((B, H, T), dtype=torch.float32, device=q.device)
+    d = _attn_desc(q, kv, kv[:, E:], B, T, H, E, out, lse, table, causal, C, 2 * E, 0)
+    call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
+         _unit="flop")
+    return out, lse
+
+
 def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
     """-> dqkv bf16 [B*T, 3C], dtable f32 [2T+1, H] (or None)."""
     import ctypes
