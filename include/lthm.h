@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 11 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 12 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -307,6 +307,20 @@ int lthm_table_bwd_mfma(const uint16_t* rows, int32_t nidx, int32_t R, const voi
  * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
 int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,
                       float* out, void* stream);
+
+/* MoELinear (commons/transformers/layers.py:101-136), the parts around its GEMMs.
+ * gate: probs[m, :] = softmax(g) with g = scale * logits[m, :] and, when top_k > 0,
+ * g[e] -> -inf where g[e] is below the top_k-th largest (:123-127); E <= 64.
+ * gate_bwd: dlogits = scale * p (dp - sum_j p_j dp_j).
+ * scale: GH[m, e P + p] = probs[m, e] * H[m, e P + p]   (bf16 in / out).
+ * hidden_bwd: dg[m, e] = sum_p dGH H;  dpre = probs[m, e] dGH gelu_tanh'(pre)  (bf16 out). */
+int lthm_moe_gate_fwd(const float* logits, int64_t M, int32_t E, float scale, int32_t top_k, float* probs,
+                      void* stream);
+int lthm_moe_gate_bwd(const float* probs, const float* dprobs, int64_t M, int32_t E, float scale, float* dlogits,
+                      void* stream);
+int lthm_moe_scale(const void* H, const float* probs, int64_t M, int32_t E, int32_t P, void* GH, void* stream);
+int lthm_moe_hidden_bwd(const float* dGH, const void* H, const void* pre, const float* probs, int64_t M, int32_t E,
+                        int32_t P, void* dpre, float* dg, void* stream);
 
 /* Binary cross-entropy with logits, mean reduction
  * (F.binary_cross_entropy_with_logits; the ranker's click loss and

@@ -341,10 +341,16 @@ class TransformerBlock(nn.Module):
         self.ln_1 = LayerNorm(attn_cfg.n_embd, bias=attn_cfg.bias)
         self.attn = SelfAttention.from_config(attn_cfg)
         self.ln_2 = LayerNorm(attn_cfg.n_embd, bias=attn_cfg.bias)
-        if isinstance(config.rotator_config, dict) and "moe" in config.rotator_config:
-            raise NotImplementedError("MoE feed-forward: use MoELinear directly (SURVEY a14)")
-        hidden_mult = config.rotator_config if isinstance(config.rotator_config, (int, float)) else 4
-        self.mlp = _MLP(attn_cfg.n_embd, attn_cfg.bias, attn_cfg.dropout, hidden_mult)
+        rc = config.rotator_config
+        if not isinstance(rc, dict) and hasattr(rc, "model_dump"):
+            rc = rc.model_dump()
+        self.is_moe = isinstance(rc, dict) and rc.get("moe") is not None
+        if self.is_moe:
+            # :340-343: MoE feed-forward (composed path: attention module + MoE MLP)
+            self.mlp = _MoEMLP(attn_cfg.n_embd, attn_cfg.bias, attn_cfg.dropout, rc["moe"])
+        else:
+            hidden_mult = config.rotator_config if isinstance(config.rotator_config, (int, float)) else 4
+            self.mlp = _MLP(attn_cfg.n_embd, attn_cfg.bias, attn_cfg.dropout, hidden_mult)
         self.is_sparse = getattr(config, "is_sparse_attn", False)
         self.enable_gradient_checkpointing = getattr(config, "enable_gradient_checkpointing", False)
         self.fp8_gemm = bool(getattr(config, "fp8_gemm", False))  # build-defined (C5)
@@ -377,6 +383,15 @@ class TransformerBlock(nn.Module):
     def _fused(self, x, double_residual: bool):
         if x.dim() != 3:
             raise ValueError("TransformerBlock expects [B, T, d]")
+        if self.is_moe:
+            T = x.shape[1]
+            mask = None
+            if self.is_causal:
+                tri = torch.ones((T, T), dtype=torch.bool, device=x.device).tril(0)
+                mask = tri.float().masked_fill(~tri, -float("inf"))[None, None]
+            y = x + self.attn(self.ln_1(x), mask)
+            y = y + self.mlp(self.ln_2(y))
+            return y + x if double_residual else y
         if self.attn.attn.table is not None:
             self.attn.attn.pos_bias.check(x.shape[1], x.shape[1])
         return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal, double_residual,
@@ -554,3 +569,137 @@ class MLP(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         lins = [m for m in self.model if isinstance(m, nn.Linear)]
         return K.mlp_chain(x, lins, [K.ACT_GELU] * (len(lins) - 1) + [K.ACT_NONE], out_f32=True)
+
+
+# ------------------------------------------------------------------ mixture of experts
+class _MoEGateFn(torch.autograd.Function):
+    """softmax(top-k-masked logits / sqrt(in_features)), commons/transformers/layers.py:122-128."""
+
+    @staticmethod
+    def forward(ctx, logits, scale, top_k):
+        from ..._lib import call, ptr, stream
+        require_gpu(logits)
+        lg = logits.contiguous()
+        M, E = lg.shape
+        probs = torch.empty_like(lg)
+        call("lthm_moe_gate_fwd", ptr(lg), M, E, scale, top_k, ptr(probs), stream())
+        ctx.save_for_backward(probs)
+        ctx.scale = scale
+        return probs
+
+    @staticmethod
+    def backward(ctx, dp):
+        from ..._lib import call, ptr, stream
+        (probs,) = ctx.saved_tensors
+        dp = dp.contiguous().float()
+        dl = torch.empty_like(probs)
+        call("lthm_moe_gate_bwd", ptr(probs), ptr(dp), probs.shape[0], probs.shape[1], ctx.scale, ptr(dl), stream())
+        return dl, None, None
+
+
+class _MoEExpertsFn(torch.autograd.Function):
+    """sum_e g_e (l2_e(gelu(l1_e(x)))) (:130-136) as two GEMMs over the stacked experts:
+    H = gelu(x W1^T + b1) with W1 = [l1_0; ...; l1_{E-1}] (one GEMM, GELU epilogue),
+    GH = g (x) H per expert block (kernel), out = GH W2^T + g B2 with W2 = [l2_0 | ... ]
+    along K and B2 the stacked l2 biases (the bias mix is one more GEMM, fed in as the
+    residual of the second)."""
+
+    @staticmethod
+    def forward(ctx, x2, g, E, P, *params):
+        from ..._lib import call, ptr, stream
+        require_gpu(x2, g)
+        M = x2.shape[0]
+        w1s, b1s, w2s, b2s = params[:E], params[E:2 * E], params[2 * E:3 * E], params[3 * E:]
+        W1b = K.cast(torch.cat([w.detach() for w in w1s], 0).contiguous(), torch.bfloat16)   # [E*P, in]
+        b1 = torch.cat([b.detach() for b in b1s], 0).contiguous()                            # [E*P]
+        W2b = K.cast(torch.cat([w.detach() for w in w2s], 1).contiguous(), torch.bfloat16)   # [out, E*P]
+        B2 = torch.stack([b.detach() for b in b2s], 0).contiguous()                          # [E, out]
+        xb = K.cast(x2, torch.bfloat16)
+        pre = torch.empty((M, E * P), dtype=torch.bfloat16, device=x2.device)
+        H = K.linear_fwd(xb, W1b, b1, act=K.ACT_GELU, aux_out=pre)
+        GH = torch.empty_like(H)
+        gc = g.contiguous()
+        call("lthm_moe_scale", ptr(H), ptr(gc), M, E, P, ptr(GH), stream())
+        gb = K.cast(gc, torch.bfloat16)
+        B2tb = K.cast(B2.t().contiguous(), torch.bfloat16)                                   # [out, E]
+        mix = K.linear_fwd(gb, B2tb, out_dtype=torch.float32)                                # g B2
+        out = K.linear_fwd(GH, W2b, res1=mix, out_dtype=torch.float32)
+        ctx.save_for_backward(xb, H, pre, GH, gc, gb, W1b, W2b, B2)
+        ctx.dims = (E, P)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..._lib import call, ptr, stream
+        xb, H, pre, GH, g, gb, W1b, W2b, B2 = ctx.saved_tensors
+        E, P = ctx.dims
+        M = xb.shape[0]
+        dO = dout.contiguous().float()
+        dOb = K.cast(dO, torch.bfloat16)
+        dW2 = K.linear_wgrad(dOb, GH)                       # [out, E*P]
+        dB2 = K.linear_wgrad(dOb, gb).t().contiguous()      # [E, out]
+        dGH = K.linear_dgrad(dOb, W2b, out_dtype=torch.float32)
+        dpre = torch.empty_like(pre)
+        dg = torch.empty((M, E), dtype=torch.float32, device=xb.device)
+        call("lthm_moe_hidden_bwd", ptr(dGH), ptr(H), ptr(pre), ptr(g), M, E, P, ptr(dpre), ptr(dg), stream())
+        dg = dg + K.linear_fwd(dOb, K.cast(B2, torch.bfloat16), out_dtype=torch.float32)
+        dW1 = K.linear_wgrad(dpre, xb)                      # [E*P, in]
+        db1 = K.colsum(dpre)
+        dx = K.linear_dgrad(dpre, W1b, out_dtype=torch.float32)
+        return (dx, dg, None, None, *dW1.split(P, 0), *db1.split(P, 0), *dW2.split(P, 1),
+                *[dB2[e] for e in range(E)])
+
+
+class _MoEUnit(nn.Module):
+    """commons/transformers/layers.py:87-95."""
+
+    def __init__(self, in_features: int, out_features: int, proj_features: int):
+        super().__init__()
+        self.l1 = nn.Linear(in_features, proj_features)
+        self.activation = nn.GELU(approximate="tanh")
+        self.l2 = nn.Linear(proj_features, out_features)
+
+
+class MoELinear(nn.Module):
+    """commons/transformers/layers.py:101-136 (softmax-gated dense mixture of experts,
+    optional top-k threshold), on the HIP GEMMs + gate kernels."""
+
+    def __init__(self, in_features: int, out_features: int, proj_features: int, num_experts: int, bias: bool = True,
+                 top_k: Optional[int] = None, gate_sizes: Optional[Tuple[int, ...]] = None):
+        super().__init__()
+        self._in_features = in_features
+        self._out_features = out_features
+        self.expert_gates = MLP(in_features, num_experts, gate_sizes=gate_sizes, bias=bias)
+        self.experts = nn.ModuleList([_MoEUnit(in_features, out_features, proj_features) for _ in range(num_experts)])
+        self.top_k = top_k
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        x2 = x.reshape(-1, self._in_features).float().contiguous()
+        logits = self.expert_gates(x2)
+        E = len(self.experts)
+        g = _MoEGateFn.apply(logits, 1.0 / math.sqrt(float(self._in_features)),
+                             0 if self.top_k is None else min(self.top_k, E))
+        P = self.experts[0].l1.out_features
+        params = ([m.l1.weight for m in self.experts] + [m.l1.bias for m in self.experts] +
+                  [m.l2.weight for m in self.experts] + [m.l2.bias for m in self.experts])
+        out = _MoEExpertsFn.apply(x2, g, E, P, *params)
+        return out.view(*shp[:-1], self._out_features)
+
+
+class _MoEMLP(nn.Module):
+    """commons/transformers/layers.py:287-317."""
+
+    def __init__(self, n_embd: int, bias: bool, dropout: float, moe_config: Dict[str, Any]):
+        super().__init__()
+        kw = dict(proj_features=moe_config["proj_features"], num_experts=moe_config["num_experts"], bias=bias,
+                  top_k=moe_config.get("top_k", None), gate_sizes=tuple(moe_config.get("gate_sizes", [])))
+        self.c_fc = MoELinear(n_embd, int(moe_config["ff_mult_factor"] * n_embd), **kw)
+        self.gelu = nn.GELU(approximate="tanh")
+        self.c_proj = MoELinear(int(moe_config["ff_mult_factor"] * n_embd), n_embd, **kw)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = self.c_fc(x)
+        h = K.ActivationFn.apply(h.contiguous(), K.ACT_GELU)
+        return self.c_proj(h)

@@ -307,3 +307,113 @@ extern "C" int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- MoELinear gates / expert scaling
+namespace lthm {
+__global__ __launch_bounds__(256) void moe_gate_fwd_k(const float* __restrict__ logits, int64_t M, int E, float scale,
+                                                      int top_k, float* __restrict__ probs) {
+  for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+    const float* lg = logits + m * E;
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) {
+      const float ge = lg[e] * scale;
+      bool keep = true;
+      if (top_k > 0) {  // kept iff fewer than top_k entries are strictly larger (ties stay, as torch.where(g < thr))
+        int greater = 0;
+        for (int j = 0; j < E; ++j) greater += (lg[j] * scale > ge) ? 1 : 0;
+        keep = greater < top_k;
+      }
+      if (keep) mx = fmaxf(mx, ge);
+      probs[m * E + e] = keep ? ge : -INFINITY;
+    }
+    float sum = 0.f;
+    for (int e = 0; e < E; ++e) {
+      const float v = probs[m * E + e];
+      const float p = v == -INFINITY ? 0.f : expf(v - mx);
+      probs[m * E + e] = p;
+      sum += p;
+    }
+    const float inv = 1.f / sum;
+    for (int e = 0; e < E; ++e) probs[m * E + e] *= inv;
+  }
+}
+__global__ __launch_bounds__(256) void moe_gate_bwd_k(const float* __restrict__ probs, const float* __restrict__ dp,
+                                                      int64_t M, int E, float scale, float* __restrict__ dl) {
+  for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+    float dot = 0.f;
+    for (int e = 0; e < E; ++e) dot += probs[m * E + e] * dp[m * E + e];
+    for (int e = 0; e < E; ++e) dl[m * E + e] = scale * probs[m * E + e] * (dp[m * E + e] - dot);
+  }
+}
+__global__ __launch_bounds__(256) void moe_scale_k(const bf16_t* __restrict__ H, const float* __restrict__ probs,
+                                                   int64_t M, int E, int P, bf16_t* __restrict__ GH) {
+  const int64_t n = M * E * P;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / ((int64_t)E * P);
+    const int e = (int)((i / P) % E);
+    GH[i] = f2bf(probs[m * E + e] * bf2f(H[i]));
+  }
+}
+__device__ __forceinline__ float moe_gelu_grad(float x) {
+  const float kb = 0.7978845608028654f, kk = 0.044715f;
+  const float x2 = x * x, t = tanhf(kb * (x + kk * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kb * (1.f + 3.f * kk * x2);
+}
+// one wave per (m, e): lanes stride the P hidden units, wave-reduced dg
+__global__ __launch_bounds__(256) void moe_hidden_bwd_k(const float* __restrict__ dGH, const bf16_t* __restrict__ H,
+                                                        const bf16_t* __restrict__ pre, const float* __restrict__ probs,
+                                                        int64_t M, int E, int P, bf16_t* __restrict__ dpre,
+                                                        float* __restrict__ dg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t w = blockIdx.x * 4 + (threadIdx.x >> 6); w < M * E; w += nw) {
+    const int64_t base = w * P;  // (m, e) row segment: m * E * P + e * P
+    const float pr = probs[w];
+    float acc = 0.f;
+    for (int p = lane; p < P; p += 64) {
+      const float d = dGH[base + p];
+      acc += d * bf2f(H[base + p]);
+      dpre[base + p] = f2bf(pr * d * moe_gelu_grad(bf2f(pre[base + p])));
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) dg[w] = acc;
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_moe_gate_fwd(const float* logits, int64_t M, int32_t E, float scale, int32_t top_k, float* probs,
+                                 void* stream) {
+  LTHM_REQUIRE(M >= 0 && E > 0 && E <= 64 && top_k >= 0);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(moe_gate_fwd_k, dim3(grid_for(M, 256, 2048)), dim3(256), 0, (hipStream_t)stream, logits, M, E,
+                     scale, top_k, probs);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+extern "C" int lthm_moe_gate_bwd(const float* probs, const float* dprobs, int64_t M, int32_t E, float scale,
+                                 float* dlogits, void* stream) {
+  LTHM_REQUIRE(M >= 0 && E > 0 && E <= 64);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(moe_gate_bwd_k, dim3(grid_for(M, 256, 2048)), dim3(256), 0, (hipStream_t)stream, probs, dprobs,
+                     M, E, scale, dlogits);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+extern "C" int lthm_moe_scale(const void* H, const float* probs, int64_t M, int32_t E, int32_t P, void* GH,
+                              void* stream) {
+  LTHM_REQUIRE(M >= 0 && E > 0 && P > 0);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(moe_scale_k, dim3(grid_for(M * E * P, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)H, probs, M, E, P, (bf16_t*)GH);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+extern "C" int lthm_moe_hidden_bwd(const float* dGH, const void* H, const void* pre, const float* probs, int64_t M,
+                                   int32_t E, int32_t P, void* dpre, float* dg, void* stream) {
+  LTHM_REQUIRE(M >= 0 && E > 0 && P > 0);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(moe_hidden_bwd_k, dim3(grid_for(M * E, 4, 4096)), dim3(256), 0, (hipStream_t)stream, dGH,
+                     (const bf16_t*)H, (const bf16_t*)pre, probs, M, E, P, (bf16_t*)dpre, dg);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
