@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 12 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 13 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -65,6 +65,17 @@ int lthm_kshift_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtyp
 int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* W,
                           int32_t w_dtype, int64_t P, int32_t D, int32_t K, int32_t mode,
                           void* out, int32_t out_dtype, float* norms, void* stream);
+
+/* Item-embedding artifact forward (embedding_module_gen.py:32-41 ModelWrapper, consumed
+ * at encoder.py:25-29 via torch.jit.load): out[i] = KShift_K(ids[i]; W [P, D], mode)
+ * * sigmoid(w2 . QuickGELU(W1 m + b1) + b2) with m = KShift_Km(ids[i]; Wm [Pm, Dm]) / sqrt(Km)
+ * (the mask model: KShiftEmbedding(normalize_output=False) -> commons MLP with one
+ * hidden layer, W1 [H1, Dm], b1 [H1], w2 [H1], b2 [1]; all f32).  Dm % 4 == 0, Dm <= 16,
+ * H1 <= 256, Wm 16-B aligned; W f32 or bf16, out f32 or bf16 [n, D].  Forward only. */
+int lthm_item_artifact_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtype, int64_t P, int32_t D,
+                           int32_t K, int32_t mode, const float* Wm, int64_t Pm, int32_t Dm, int32_t Km,
+                           const float* W1, const float* b1, int32_t H1, const float* w2, const float* b2, void* out,
+                           int32_t out_dtype, void* stream);
 
 /* Pool K rows of a gathered buffer W [R, D] given explicit row indices
  * rows [n, K] (< R): same in-order f32 sum and finalisation as lthm_kshift_fwd.

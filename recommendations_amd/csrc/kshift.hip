@@ -263,6 +263,152 @@ static int pick_vb(int D, int esz, int* lpr_log2) {
   return vb;
 }
 
+// ---------------------------------------------------------------------------
+// Item-embedding artifact (embedding_module_gen.py:32-41, consumed at
+// encoder.py:25-29): out = KShift_K(id; W) * sigmoid(MLP(KShift_Km(id; Wm))),
+// MLP = Linear(Dm, H1) -> QuickGELU -> Linear(H1, 1) (commons/layers.py:65-81,
+// the mask model of embedding_module_gen.py:79-87).  One pass: the group of LPR
+// lanes that pools the item's D-wide row sum also pools its Dm-wide mask rows
+// (every lane of the group reads the same 16-B mask vectors: one coalesced
+// request), evaluates the H1 hidden units strided over the group, reduces the
+// logit by shuffles and scales its own slice of the pooled row.  The MLP
+// weights sit in LDS.  Main-table pooling keeps the in-order c = 0..K-1 sum.
+// ---------------------------------------------------------------------------
+constexpr int IA_MAX_DM = 16;
+constexpr int IA_MAX_H1 = 256;
+
+template <typename TW, typename TO, int VB>
+__global__ __launch_bounds__(KS_BLOCK) void item_artifact_fwd_k(
+    const int64_t* __restrict__ ids, int64_t n, const TW* __restrict__ W, int64_t P, int D, int K, int mode,
+    float scale, const float* __restrict__ Wm, int64_t Pm, int Dm, int Km, float mscale,
+    const float* __restrict__ W1, const float* __restrict__ b1, int H1, const float* __restrict__ w2,
+    const float* __restrict__ b2, TO* __restrict__ out, int LPR_LOG2) {
+  constexpr int NE = VB / (int)sizeof(TW);
+  __shared__ int64_t rows_lds[KS_BLOCK / 64][KS_ROWS_LDS / 2];
+  __shared__ int64_t mrows_lds[KS_BLOCK / 64][KS_ROWS_LDS / 2];
+  __shared__ float w1_lds[IA_MAX_H1 * IA_MAX_DM];
+  __shared__ float b1_lds[IA_MAX_H1], w2_lds[IA_MAX_H1];
+  for (int i = threadIdx.x; i < H1 * Dm; i += KS_BLOCK) w1_lds[i] = W1[i];
+  for (int i = threadIdx.x; i < H1; i += KS_BLOCK) {
+    b1_lds[i] = b1[i];
+    w2_lds[i] = w2[i];
+  }
+  const float bias2 = b2[0];
+  const int LPR = 1 << LPR_LOG2;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gl = lane & (LPR - 1);
+  const int gi = lane >> LPR_LOG2;
+  const int IPW = 64 >> LPR_LOG2;
+  const int IPB = IPW * (KS_BLOCK / 64);
+  __syncthreads();
+
+  for (int64_t base = (int64_t)blockIdx.x * IPB; base < n; base += (int64_t)gridDim.x * IPB) {
+    const int64_t item = base + wave * IPW + gi;
+    const bool valid = item < n;
+    const int64_t id = valid ? ids[item] : 0;
+    for (int c = gl; c < K; c += LPR) rows_lds[wave][gi * K + c] = valid ? kshift_row(id, c, P) : 0;
+    for (int c = gl; c < Km; c += LPR) mrows_lds[wave][gi * Km + c] = valid ? kshift_row(id, c, Pm) : 0;
+    __syncthreads();
+    float acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.f;
+    float logit = 0.f;
+    if (valid) {
+      const TW* colp = W + (size_t)gl * NE;
+      for (int c = 0; c < K; c += 2) {
+        float v0[NE], v1[NE];
+        load_vec<TW, VB>(colp + rows_lds[wave][gi * K + c] * D, v0);
+        if (c + 1 < K) load_vec<TW, VB>(colp + rows_lds[wave][gi * K + c + 1] * D, v1);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] = (c == 0) ? v0[e] : acc[e] + v0[e];
+        if (c + 1 < K) {
+#pragma unroll
+          for (int e = 0; e < NE; ++e) acc[e] += v1[e];
+        }
+      }
+      // mask vector m [Dm] (every lane of the group, same addresses), in-order sum
+      float m[IA_MAX_DM];
+#pragma unroll
+      for (int d = 0; d < IA_MAX_DM; ++d) m[d] = 0.f;
+      for (int c = 0; c < Km; ++c) {
+        const float* mr = Wm + mrows_lds[wave][gi * Km + c] * Dm;
+#pragma unroll
+        for (int d4 = 0; d4 < IA_MAX_DM / 4; ++d4)
+          if (d4 * 4 < Dm) {
+            const float4 v = *(const float4*)(mr + d4 * 4);
+            if (c == 0) {
+              m[d4 * 4] = v.x; m[d4 * 4 + 1] = v.y; m[d4 * 4 + 2] = v.z; m[d4 * 4 + 3] = v.w;
+            } else {
+              m[d4 * 4] += v.x; m[d4 * 4 + 1] += v.y; m[d4 * 4 + 2] += v.z; m[d4 * 4 + 3] += v.w;
+            }
+          }
+      }
+#pragma unroll
+      for (int d = 0; d < IA_MAX_DM; ++d) m[d] = m[d] / mscale;
+      // hidden units strided over the group: QuickGELU(W1 m + b1) . w2
+      float part = 0.f;
+      for (int j = gl; j < H1; j += LPR) {
+        float h = b1_lds[j];
+        const float* wr = w1_lds + j * Dm;
+#pragma unroll
+        for (int d = 0; d < IA_MAX_DM; ++d)
+          if (d < Dm) h = fmaf(wr[d], m[d], h);
+        const float qg = h / (1.f + __expf(-1.702f * h));
+        part = fmaf(w2_lds[j], qg, part);
+      }
+      for (int o = LPR >> 1; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      logit = part + bias2;
+    }
+    if (mode == LTHM_KSHIFT_NORMALIZE) {
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) ss += acc[e] * acc[e];
+      for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float den = fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / den;
+    } else if (mode == LTHM_KSHIFT_SCALE) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / scale;
+    }
+    const float gate = 1.f / (1.f + __expf(-logit));
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = gate * acc[e];
+    if (valid) store_vec<TO, NE>(out + item * D + (size_t)gl * NE, acc);
+    __syncthreads();
+  }
+}
+
+template <typename TW, typename TO>
+static int launch_item_artifact(const int64_t* ids, int64_t n, const void* W, int64_t P, int D, int K, int mode,
+                                const float* Wm, int64_t Pm, int Dm, int Km, const float* W1, const float* b1,
+                                int H1, const float* w2, const float* b2, void* out, hipStream_t s) {
+  int l2 = 0;
+  const int vb = pick_vb(D, (int)sizeof(TW), &l2);
+  LTHM_REQUIRE(vb > 0);
+  const int ipw = 64 >> l2;
+  LTHM_REQUIRE(ipw * K <= KS_ROWS_LDS / 2 && ipw * Km <= KS_ROWS_LDS / 2);
+  const int ipb = ipw * (KS_BLOCK / 64);
+  const int grid = grid_for(n, ipb, 256 * 16);
+  const float scale = (float)__builtin_sqrt((double)K);
+  const float mscale = (float)__builtin_sqrt((double)Km);
+#define IA_LAUNCH(V)                                                                                         \
+  hipLaunchKernelGGL((item_artifact_fwd_k<TW, TO, V>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n, (const TW*)W, \
+                     P, D, K, mode, scale, Wm, Pm, Dm, Km, mscale, W1, b1, H1, w2, b2, (TO*)out, l2)
+  if (vb == 16)
+    IA_LAUNCH(16);
+  else if (vb == 8)
+    IA_LAUNCH(8);
+  else if (vb == 4)
+    IA_LAUNCH(4);
+  else
+    return (int)hipErrorInvalidValue;
+#undef IA_LAUNCH
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename TW, typename TO>
 static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W, int64_t P, int D, int K,
                       int mode, void* out, float* norms, hipStream_t s, const int64_t* xrows = nullptr) {
@@ -396,6 +542,27 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
     return launch_bwd<float, bf16_t>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
   if (dy_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
     return launch_bwd<bf16_t, float>(ids, items, F, dY, out, norms, P, D, K, mode, dW, flags, list, (unsigned long long*)count, s);
+  return (int)hipErrorInvalidValue;
+}
+
+int lthm_item_artifact_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtype, int64_t P, int32_t D,
+                           int32_t K, int32_t mode, const float* Wm, int64_t Pm, int32_t Dm, int32_t Km,
+                           const float* W1, const float* b1, int32_t H1, const float* w2, const float* b2, void* out,
+                           int32_t out_dtype, void* stream) {
+  LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n >= 0 && mode >= 0 && mode <= 2);
+  LTHM_REQUIRE(Pm > 0 && Km > 0 && Km <= 64 && Dm > 0 && Dm <= IA_MAX_DM && Dm % 4 == 0);
+  LTHM_REQUIRE(H1 > 0 && H1 <= IA_MAX_H1 && W1 && b1 && w2 && b2 && Wm);
+  LTHM_REQUIRE(((uintptr_t)Wm % 16) == 0);
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (w_dtype == LTHM_F32 && out_dtype == LTHM_F32)
+    return launch_item_artifact<float, float>(ids, n, W, P, D, K, mode, Wm, Pm, Dm, Km, W1, b1, H1, w2, b2, out, s);
+  if (w_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
+    return launch_item_artifact<bf16_t, float>(ids, n, W, P, D, K, mode, Wm, Pm, Dm, Km, W1, b1, H1, w2, b2, out, s);
+  if (w_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
+    return launch_item_artifact<float, bf16_t>(ids, n, W, P, D, K, mode, Wm, Pm, Dm, Km, W1, b1, H1, w2, b2, out, s);
+  if (w_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
+    return launch_item_artifact<bf16_t, bf16_t>(ids, n, W, P, D, K, mode, Wm, Pm, Dm, Km, W1, b1, H1, w2, b2, out, s);
   return (int)hipErrorInvalidValue;
 }
 

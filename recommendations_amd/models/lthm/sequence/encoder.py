@@ -17,6 +17,7 @@ import torch.nn as nn
 from .... import kernels as K
 from ....commons.functional import cap_gradients
 from ....commons.layers import KShiftEmbedding, MLP, RowShardedKShiftEmbedding, TableBatchedKShiftEmbedding
+from .item_artifact import load_item_artifact
 from .product_tower import ProductTower
 from .query_tower import QueryTower
 
@@ -43,12 +44,17 @@ class Encoder(nn.Module):
     def __init__(self, model_config):
         super().__init__()
         pt = model_config.product_tower
-        if pt.model_init_metadata is not None:
-            raise NotImplementedError("TorchScript item-embedding artifacts are loaded via load_item_artifact()")
         lm = pt.latent_model_config
         # fp32 output: the CVE bucketize downstream is discontinuous, a bf16-rounded
         # input would flip ~1% of the bucket decisions relative to the reference
-        if model_config.item_table_sharded:
+        if pt.model_init_metadata is not None:
+            # encoder.py:25-29: a pre-trained item-embedding artifact replaces the KShift
+            # table (local safetensors file; the S3 fetch is out of scope)
+            md = pt.model_init_metadata
+            path = md["embedding_module_path"] if isinstance(md, dict) else md.embedding_module_path
+            self.product_emb_module = load_item_artifact(
+                path, table_dtype=torch.bfloat16 if model_config.item_table_bf16 else None)
+        elif model_config.item_table_sharded:
             self.product_emb_module = RowShardedKShiftEmbedding(
                 lm.vocab_size_latent, pt.inp_emb_dim, num_shifts=lm.num_shifts_latent,
                 normalize_output=lm.normalize_embedding,

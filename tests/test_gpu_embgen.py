@@ -115,3 +115,72 @@ def test_model_wrapper_forward(dev):
                            [l.weight.detach().cpu() for l in lins], [l.bias.detach().cpu() for l in lins])
     exp = mk.sigmoid() * e
     assert relerr(got, exp) < 2e-2  # the mask MLP runs on bf16 MFMA operands
+
+
+def _artifact_ref(ids, sd, K, normalize, Km):
+    e = ref.kshift_fwd_torch(ids, sd["model.emb.weight"].float(), K, normalize)
+    m = ref.kshift_fwd_torch(ids, sd["mask_model.0.emb.weight"], Km, False)
+    lg = ref.mlp_quickgelu(m, [sd["mask_model.1.model.0.weight"], sd["mask_model.1.model.2.weight"]],
+                           [sd["mask_model.1.model.0.bias"], sd["mask_model.1.model.2.bias"]])
+    return lg.sigmoid() * e
+
+
+@pytest.mark.parametrize("D,K,Km,Dm,H1,norm,tdt", [(32, 16, 16, 4, 64, True, torch.float32),
+                                                  (128, 8, 16, 8, 128, True, torch.bfloat16),
+                                                  (64, 16, 4, 16, 256, False, torch.float32),
+                                                  (32, 3, 5, 4, 64, True, torch.bfloat16)])
+def test_item_artifact_fused_vs_oracle(dev, D, K, Km, Dm, H1, norm, tdt):
+    """the fused artifact kernel (KShift pool + mask KShift pool +
+    QuickGELU MLP + sigmoid gate, one launch) vs the oracle composition of the
+    reference's ModelWrapper (embedding_module_gen.py:32-41).  All-f32 arithmetic
+    (the table is read as stored; bf16 tables are compared on the same bf16 values):
+    1e-5 relative Frobenius (exp / summation-order rounding only)."""
+    from recommendations_amd.models.lthm.sequence.item_artifact import ItemEmbeddingArtifact
+    torch.manual_seed(D + K)
+    m = ItemEmbeddingArtifact(7001, D, K, norm, 3001, Dm, Km, H1, table_dtype=tdt)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape).to(p.dtype))
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (3, 333), dtype=torch.int64)
+    ids[0, :5] = torch.tensor([0, 1, -1, 2 ** 63 - 1, -2 ** 63])
+    got = m(ids.to(dev)).cpu()
+    assert got.shape == (3, 333, D)
+    assert relerr(got, _artifact_ref(ids.view(-1), sd, K, norm, Km).view(3, 333, D)) < 1e-5
+    assert m(torch.empty(0, dtype=torch.int64, device=dev)).shape == (0, D)
+
+
+def test_item_artifact_round_trip_and_encoder(dev, tmp_path):
+    """embedding_module_gen ModelWrapper -> save_item_artifact (safetensors) ->
+    load_item_artifact -> fused forward == the unfused ModelWrapper forward; the LTHM
+    encoder built with product_tower.model_init_metadata uses it (encoder.py:25-29)."""
+    from recommendations_amd.commons.layers import MLP, KShiftEmbedding
+    from recommendations_amd.embedding_module_gen import ModelWrapper
+    from recommendations_amd.models.lthm.sequence.item_artifact import (ItemEmbeddingArtifact, load_item_artifact,
+                                                                      save_item_artifact)
+    torch.manual_seed(1)
+    w = ModelWrapper(KShiftEmbedding(5000, 32, num_shifts=16, normalize_output=True),
+                     torch.nn.Sequential(KShiftEmbedding(5750, 4, num_shifts=16), MLP(4, 1, [64])))
+    path = str(tmp_path / "item.safetensors")
+    save_item_artifact(w, path)
+    a = load_item_artifact(path, device=dev)
+    w = w.to(dev)
+    ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (4096,), dtype=torch.int64, device=dev)
+    with torch.no_grad():
+        assert relerr(a(ids), w(ids)) < 2e-2       # the unfused mask MLP uses bf16 MFMA operands
+    sd = {k: v.detach().cpu() for k, v in w.state_dict().items()}
+    assert relerr(a(ids).cpu(), _artifact_ref(ids.cpu(), sd, 16, True, 16)) < 1e-5
+
+    from recommendations_amd.models.lthm.builder import LTHMModelBuilder
+    from recommendations_amd.models.lthm.config import lthm_config
+    from recommendations_amd.data import synthetic_lthm_batch
+    cfg = lthm_config(T=32, d=64, n_layers=2, n_head=1, item_vocab=5000)
+    cfg.product_tower.model_init_metadata = {"embedding_module_path": path}
+    model = LTHMModelBuilder(None, cfg).build().to(dev)
+    arts = [mod for mod in model.modules() if isinstance(mod, ItemEmbeddingArtifact)]
+    assert len(arts) == 1
+    batch = synthetic_lthm_batch(64, 32, seed=3, device=dev)
+    out = model(batch)
+    loss, _ = model.train_step(batch, out)
+    assert torch.isfinite(loss).all()
