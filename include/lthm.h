@@ -421,7 +421,7 @@ typedef struct lthm_contrastive_desc {
                              backward: scratch for the per-row exp2 shift */
   float* w;               /* row weights, written by the forward, read by the backward */
   const float* gscale;    /* device scalar: upstream gradient of the loss (backward) */
-  float* d_out;           /* f32 [B, T+1, n_heads, De] (rows of this head written) */
+  float* d_out;           /* f32 [B, T+1, n_heads, De]: every row of this head is written (no pre-zeroing) */
   float* d_in;            /* f32 [B, T, De] (accumulated over heads) */
 } lthm_contrastive_desc;
 

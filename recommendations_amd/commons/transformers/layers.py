@@ -32,6 +32,27 @@ def _f(b):
     return None if b is None else b.detach().contiguous()
 
 
+# bf16 copy of the input gradient a block's backward produces (its final LayerNorm
+# backward writes it for free), handed to the backward of the block below, which
+# would otherwise cast the same f32 gradient again.  One slot; it holds the f32
+# tensor itself, so a match on (data_ptr, shape, version) is that very tensor.
+_GRAD_BF16: Dict[str, Any] = {}
+
+
+def _stash_grad_bf16(g32: torch.Tensor, gbf: torch.Tensor) -> None:
+    _GRAD_BF16["src"], _GRAD_BF16["bf"], _GRAD_BF16["ver"] = g32, gbf, g32._version
+
+
+def _grad_bf16(g32: torch.Tensor) -> torch.Tensor:
+    src = _GRAD_BF16.pop("src", None)
+    bf = _GRAD_BF16.pop("bf", None)
+    ver = _GRAD_BF16.pop("ver", None)
+    if (src is not None and src.data_ptr() == g32.data_ptr() and src.numel() == g32.numel()
+            and src.dtype == g32.dtype and ver == src._version and g32.is_contiguous()):
+        return bf.view(g32.shape)
+    return K.cast(g32, torch.bfloat16)
+
+
 class TransformerBlockFn(torch.autograd.Function):
     """x -> x + attn(ln_1 x) -> + mlp(ln_2 .)  [+ x again when double_residual]."""
 
@@ -78,7 +99,7 @@ class TransformerBlockFn(torch.autograd.Function):
         dy = dout.contiguous().view(M, d)
         if dy.dtype != torch.float32:
             dy = dy.float()
-        dyb = K.cast(dy, torch.bfloat16)
+        dyb = _grad_bf16(dy)
         # MLP half
         dw2 = K.linear_wgrad(dyb, g)
         db2 = K.colsum(dy) if has_b2 else None
@@ -95,8 +116,9 @@ class TransformerBlockFn(torch.autograd.Function):
         dwqkv = K.linear_wgrad(dqkv, h1)
         dbqkv = K.colsum(dqkv) if has_bqkv else None
         dh1 = K.linear_dgrad(dqkv, wqkv_b)
-        dx, _, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1, res2=dy if dbl else None,
-                                              want_bf16=False)
+        dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1,
+                                                res2=dy if dbl else None)
+        _stash_grad_bf16(dx, dxb)
         dtable = None
         if tshape is not None:
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)

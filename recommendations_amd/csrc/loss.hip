@@ -296,6 +296,17 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
     const float wv = r < g.n ? a.w[base + r] : 0.f;
     shift[base + r] = wv != 0.f ? __log2f(wv) - a.lse[base + r] * 1.4426950408889634f : -INFINITY;
   }
+  // d_out rows of this head that the ROWS kernel never writes (t >= L of each of the
+  // mini-batch's sequences) are zeroed here, so d_out needs no whole-tensor fill
+  const int tl0 = max(g.L, 0), ntail = a.T + 1 - tl0;
+  const int per_seq = ntail * (DE / 4);
+  const int64_t cnt = (int64_t)g.Bm * per_seq;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+    const int b = (int)(i / per_seq), rem = (int)(i - (int64_t)b * per_seq);
+    const int t = tl0 + rem / (DE / 4), c4 = rem % (DE / 4);
+    float* dst = a.d_out + (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
+    *reinterpret_cast<float4*>(dst) = float4{0.f, 0.f, 0.f, 0.f};
+  }
 }
 
 // ---------------------------------------------------------------- stats (one block per mini-batch)
@@ -303,7 +314,8 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
 // stats[mb][*] = {loss, used, sum_negatives, min_negatives, sum_rank, median_rank, hits@k...}
 __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a, float* __restrict__ stats, int nstat, const int* __restrict__ ks,
                                                   int nk, float loss_scale, float* __restrict__ wout) {
-  __shared__ int srank[4096];
+  constexpr int RPT = 4096 / 256;  // rows per thread (n <= 4096)
+  __shared__ int hist[4096];       // histogram of the used rows' ranks (rank < n <= 4096)
   __shared__ float red[256];
   __shared__ int ired[256];
   const int mb = blockIdx.x;
@@ -312,17 +324,33 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a, float* __restrict__ 
   float ls = 0.f, neg = 0.f, rks = 0.f;
   int used = 0, mneg = 0x7fffffff;
   const int64_t base = (int64_t)mb * a.n_max;
-  for (int r = tid; r < g.n; r += 256) {
-    const int nn = a.cnt[base + r] - 1;
-    const bool u = !pad_of(a, g, r) && nn > 0;
-    if (u) {
-      ls += a.lse[base + r] - a.pos[base + r];
-      neg += (float)nn;
-      rks += (float)a.rank[base + r];
-      used += 1;
-      mneg = min(mneg, nn);
+  for (int i = tid; i < 4096; i += 256) hist[i] = 0;
+  // one pass over the rows, all loads of a thread's rows in flight together;
+  // the used flags and ranks stay in registers for the later passes
+  int rkv[RPT];
+  unsigned umask = 0u;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = tid + 256 * i;
+    rkv[i] = 0x7fffffff;
+    if (r < g.n) {
+      const int nn = a.cnt[base + r] - 1;
+      const bool u = !pad_of(a, g, r) && nn > 0;
+      if (u) {
+        umask |= 1u << i;
+        rkv[i] = a.rank[base + r];
+        ls += a.lse[base + r] - a.pos[base + r];
+        neg += (float)nn;
+        rks += (float)rkv[i];
+        used += 1;
+        mneg = min(mneg, nn);
+      }
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i)
+    if (umask & (1u << i)) atomicAdd(&hist[rkv[i]], 1);
   // block reductions
   auto fsum = [&](float v) {
     red[tid] = v; __syncthreads();
@@ -342,61 +370,61 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a, float* __restrict__ 
   const float Ls = fsum(ls), Ns = fsum(neg), Rs = fsum(rks);
   const int U = isum(used), Mn = imin(mneg);
   const float wr = U > 0 ? loss_scale / (float)U : 0.f;
-  for (int r = tid; r < a.n_max; r += 256) {
-    float wv = 0.f;
-    if (r < g.n) {
-      const int nn = a.cnt[base + r] - 1;
-      if (!pad_of(a, g, r) && nn > 0) wv = wr;
-    }
-    wout[base + r] = wv;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = tid + 256 * i;
+    if (r < a.n_max) wout[base + r] = (umask & (1u << i)) ? wr : 0.f;
   }
-  // median of the used ranks: bitonic sort in LDS (n <= 4096)
-  int n2 = 1;
-  while (n2 < g.n) n2 <<= 1;
-  for (int i = tid; i < n2; i += 256) {
-    int v = 0x7fffffff;
-    if (i < g.n) {
-      const int nn = a.cnt[base + i] - 1;
-      if (!pad_of(a, g, i) && nn > 0) v = a.rank[base + i];
-    }
-    srank[i] = v;
-  }
-  __syncthreads();
-  for (int k = 2; k <= n2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = tid; t < n2 / 2; t += 256) {
-        const int i0 = 2 * t - (t & (j - 1)), i1 = i0 + j;
-        const bool up = (i0 & k) == 0;
-        const int x = srank[i0], y = srank[i1];
-        if ((x > y) == up) { srank[i0] = y; srank[i1] = x; }
-      }
-      __syncthreads();
-    }
   // hits@k: rank < min(k, min negatives)
   float* st = stats + (int64_t)mb * nstat;
   for (int q = 0; q < nk; ++q) {
     const int kq = min(ks[q], Mn);
     int h = 0;
-    for (int r = tid; r < g.n; r += 256) {
-      const int nn = a.cnt[base + r] - 1;
-      if (!pad_of(a, g, r) && nn > 0 && a.rank[base + r] < kq) h += 1;
-    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) h += (rkv[i] < kq) ? 1 : 0;  // unused rows hold INT_MAX
     h = isum(h);
     if (tid == 0) st[7 + q] = U > 0 ? (float)h / (float)U : 0.f;
   }
+  // median of the used ranks (torch.quantile(0.5): linear interpolation between the
+  // order statistics lo and hi) from the rank histogram: this thread's 16 bins,
+  // an exclusive scan of the 256 bin-group totals, then the owner of each
+  // order statistic reports its value
+  const int p_lo = U > 0 ? (int)floorf(0.5f * (float)(U - 1)) : 0;
+  const int p_hi = U > 0 ? min(p_lo + 1, U - 1) : 0;
+  int cnt16 = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) cnt16 += hist[tid * 16 + i];
+  ired[tid] = cnt16;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = tid >= o ? ired[tid - o] : 0;
+    __syncthreads();
+    ired[tid] += v;
+    __syncthreads();
+  }
+  int run = ired[tid] - cnt16;  // order statistics before this thread's bins
+  __syncthreads();
+  float* sel = red;  // red[0] = value at p_lo, red[1] = value at p_hi
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = hist[tid * 16 + i];
+    if (c > 0) {
+      if (p_lo >= run && p_lo < run + c) sel[0] = (float)(tid * 16 + i);
+      if (p_hi >= run && p_hi < run + c) sel[1] = (float)(tid * 16 + i);
+    }
+    run += c;
+  }
+  __syncthreads();
   if (tid == 0) {
     st[0] = U > 0 ? Ls / (float)U : 0.f;
     st[1] = (float)U;
     st[2] = U > 0 ? Ns / (float)U : 0.f;
     st[3] = (float)(U > 0 ? Mn : 0);
     st[4] = U > 0 ? Rs / (float)U : 0.f;
-    // torch.quantile(0.5): linear interpolation between the two middle order statistics
     float med = 0.f;
     if (U > 0) {
       const float p = 0.5f * (float)(U - 1);
-      const int lo = (int)floorf(p);
-      const int hi = min(lo + 1, U - 1);
-      med = (float)srank[lo] + (p - (float)lo) * (float)(srank[hi] - srank[lo]);
+      med = sel[0] + (p - (float)p_lo) * (sel[1] - sel[0]);
     }
     st[5] = med;
     st[6] = (float)g.off;

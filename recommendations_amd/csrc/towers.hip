@@ -292,48 +292,58 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
 // ------------------------------------------------------------------ product-tower embedding on MFMA
 // emb[t, :] = b + W xn[t] + sum_s Tab[rows[t, s], :]   (rows from the FULL = false pass)
 // The bag sums are a one-hot GEMM  onehot[t, k] . Tab[k, :]  over all R table
-// rows k: A fragments are built from the LDS-staged bucket ids (k belongs to
-// slot sOf[k]; A = [rows[t, sOf[k]] == k], exactly 0/1 in bf16, Tab bf16, f32
-// accumulation), Tab streams through LDS in 32-row slabs read with
-// ds_read_tr16_b64.  The mapper Linear (Din <= 64) runs in f32 on the VALU in the
-// epilogue.  Block = 8 waves = 128 tokens x D columns (D = 16 NF <= 256).
+// rows k (exactly 0/1 in bf16, Tab bf16, f32 accumulation).  The block first
+// turns its tokens' bucket rows into a per-token bitmask over the R rows (one
+// LDS OR per (token, slot)); an A fragment (8 consecutive k of one token) is
+// then one byte of that mask expanded through a 256-entry LDS table of bf16
+// 0/1 octets.  Tab streams through LDS in 32-row slabs read with
+// ds_read_tr16_b64.  Block = 8 waves = 128 tokens x D columns (D = 16 NF <= 256);
+// for even NF a wave owns 32 tokens x D/2 columns, so every B fragment read
+// from LDS feeds two MFMAs (LDS traffic per MFMA halved).  The mapper Linear
+// (Din <= 64) runs on the MFMA as bf16 hi/lo splits.
 constexpr int PE_TOK = 128;
 constexpr int PE_MAXR = 4096;  // table rows
+
+__host__ __device__ constexpr int pe_rbw(int R32) { return R32 / 32 + 1; }  // odd dword stride: no bank repeats
 
 template <typename TX, int NF>
 __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int total, int R) {
   constexpr int D = 16 * NF;
-  constexpr int SLAB = 32 * D * 2;  // one 32-row bf16 slab
+  constexpr int CH = (NF % 2 == 0) ? 2 : 1;  // column halves
+  constexpr int MT = CH;                     // 16-token tiles per wave
+  constexpr int NFW = NF / CH;               // 16-column fragments per wave
+  constexpr int TG = 8 / CH;                 // token groups
+  constexpr int SLAB = 32 * D * 2;           // one 32-row bf16 slab
   constexpr int PD = (32 * D / 8 + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* slab = smem;                                        // [2][SLAB]
-  float* wN = reinterpret_cast<float*>(smem + 2 * SLAB);            // [D][Din] (nn.Linear layout)
-  float* xs = wN + d.Din * D;                                       // [PE_TOK][Din]
-  uint16_t* rs = reinterpret_cast<uint16_t*>(xs + PE_TOK * d.Din);  // [PE_TOK][total]
-  uint16_t* sOf = rs + PE_TOK * total;                              // [R32]
+  unsigned char* slab = smem;                                            // [2][SLAB]
+  float* wN = reinterpret_cast<float*>(smem + 2 * SLAB);                // [D][Din] (nn.Linear layout)
+  float* xs = wN + d.Din * D;                                           // [PE_TOK][Din]
+  u32x4* lut = reinterpret_cast<u32x4*>(xs + PE_TOK * d.Din);           // [256] bf16 0/1 octets
+  uint32_t* bits = reinterpret_cast<uint32_t*>(lut + 256);              // [PE_TOK][RBW]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int Din = d.Din;
   const int R32 = (R + 31) & ~31;
+  const int RBW = pe_rbw(R32);
   const int64_t t0 = (int64_t)blockIdx.x * PE_TOK;
   const bf16_t* tab = reinterpret_cast<const bf16_t*>(d.tables);
-  // ---- per-block staging: mapper weights, slot-of-row map, bucket rows, normalised x
+  // ---- per-block staging: mapper weights, 0/1 octet table, row bitmask, normalised x
   for (int i = tid; i < Din * D; i += 512) wN[i] = d.w_map[i];
-  for (int k = tid; k < R32; k += 512) {
-    int sl = 0, so = 0;
-    if (k < d.cve_rows) {
-      for (int j = 0; j < d.n_mod; ++j) {
-        const int rps = d.mod_nbins[j] + 1, r0 = d.mod_row_off[j], np = d.mod_nproj[j];
-        if (k >= r0 && k < r0 + np * rps) sl = so + (k - r0) / rps;
-        so += np;
-      }
-    } else {
-      sl = total - 1;  // histogram slot
-    }
-    sOf[k] = (uint16_t)sl;
+  if (tid < 256) {
+    u32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = (((tid >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((tid >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[tid] = v;
   }
+  for (int i = tid; i < PE_TOK * RBW; i += 512) bits[i] = 0u;
+  __syncthreads();
   for (int i = tid; i < PE_TOK * total; i += 512) {
     const int tt = i / total;
-    rs[i] = (t0 + tt < d.n) ? d.rows_out[t0 * total + i] : (uint16_t)0xffff;
+    if (t0 + tt < d.n) {
+      const int k = d.rows_out[t0 * total + i];
+      if (k < R) atomicOr(bits + tt * RBW + (k >> 5), 1u << (k & 31));
+    }
   }
   {
     // xn = x / max(|x|, 1e-12): 8 lanes per token
@@ -380,10 +390,13 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   fetch(0);
   store(0);
   __syncthreads();
-  f32x4 acc[NF];
+  const int tg = w % TG, chh = w / TG;
+  const int nb0 = chh * NFW * 16;  // first column of this wave
+  f32x4 acc[MT][NFW];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int tl = w * 16 + (lane & 15);  // this lane's A row (token)
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int f = 0; f < NFW; ++f) acc[mt][f] = f32x4{0.f, 0.f, 0.f, 0.f};
   // mapper xn . W^T on MFMA: f32 operands split into bf16 hi + lo, three products
   // (hi.hi + hi.lo + lo.hi) keep ~16 mantissa bits
   auto split8 = [](const float* p, int valid, bf16x8v& hi, bf16x8v& lo) {
@@ -401,51 +414,62 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   for (int k0 = 0; k0 < Din; k0 += 32) {
     const int kb = k0 + 8 * (lane >> 4);
     const int valid = max(0, min(8, Din - kb));
-    bf16x8v xh, xl;
-    split8(xs + tl * Din + kb, valid, xh, xl);
+    bf16x8v xh[MT], xl[MT];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) {
+    for (int mt = 0; mt < MT; ++mt) split8(xs + (tg * 16 * MT + mt * 16 + (lane & 15)) * Din + kb, valid, xh[mt], xl[mt]);
+#pragma unroll
+    for (int f = 0; f < NFW; ++f) {
       bf16x8v wh, wl;
-      split8(wN + (f * 16 + (lane & 15)) * Din + kb, valid, wh, wl);
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, wh, acc[f], 0, 0, 0);
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, wl, acc[f], 0, 0, 0);
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, wh, acc[f], 0, 0, 0);
+      split8(wN + (nb0 + f * 16 + (lane & 15)) * Din + kb, valid, wh, wl);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[mt], wh, acc[mt][f], 0, 0, 0);
+        acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[mt], wl, acc[mt][f], 0, 0, 0);
+        acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl[mt], wh, acc[mt][f], 0, 0, 0);
+      }
     }
   }
-  const uint16_t* myrows = rs + tl * total;
+  // this lane's mask bytes: token row tl(mt), byte (k0 >> 3) + (lane >> 4)
+  const unsigned char* mb[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+    mb[mt] = reinterpret_cast<const unsigned char*>(bits + (tg * 16 * MT + mt * 16 + (lane & 15)) * RBW) + (lane >> 4);
   const int nslab = R32 / 32;
   for (int sI = 0; sI < nslab; ++sI) {
     const int cur = sI & 1, k0 = sI * 32;
     const bool more = sI + 1 < nslab;
     if (more) fetch(k0 + 32);
-    s16x8 a;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k = k0 + 8 * (lane >> 4) + i;
-      a[i] = ((int)myrows[sOf[k]] == k) ? (short)0x3F80 : (short)0;
-    }
-    const bf16x8v af = __builtin_bit_cast(bf16x8v, a);
     const unsigned char* img = slab + cur * SLAB;
+    bf16x8v af[MT];
 #pragma unroll
-    for (int f = 0; f < NF; ++f)
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img, f * 16, lane), acc[f], 0, 0, 0);
+    for (int mt = 0; mt < MT; ++mt) af[mt] = __builtin_bit_cast(bf16x8v, lut[mb[mt][k0 >> 3]]);
+#pragma unroll
+    for (int f = 0; f < NFW; ++f) {
+      const bf16x8v bf = ct_tr_frag<D>(img, nb0 + f * 16, lane);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bf, acc[mt][f], 0, 0, 0);
+    }
     if (more) store(cur ^ 1);
     __syncthreads();
   }
   // ---- epilogue: + bias, mask fill, bf16 store
   bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out);
-  float bias[NF];
+  float bias[NFW];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) bias[f] = d.b_map ? d.b_map[f * 16 + (lane & 15)] : 0.f;
+  for (int f = 0; f < NFW; ++f) bias[f] = d.b_map ? d.b_map[nb0 + f * 16 + (lane & 15)] : 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tb = w * 16 + 4 * (lane >> 4) + j;
-    const int64_t t = t0 + tb;
-    if (t >= d.n) continue;
-    const bool masked = d.mask_out[t] != 0;
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int f = 0; f < NF; ++f) eo[t * D + f * 16 + (lane & 15)] = f2bf(masked ? 0.f : acc[f][j] + bias[f]);
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int tb = tg * 16 * MT + mt * 16 + 4 * (lane >> 4) + j;
+      const int64_t t = t0 + tb;
+      if (t >= d.n) continue;
+      const bool masked = d.mask_out[t] != 0;
+#pragma unroll
+      for (int f = 0; f < NFW; ++f)
+        eo[t * D + nb0 + f * 16 + (lane & 15)] = f2bf(masked ? 0.f : acc[mt][f][j] + bias[f]);
+    }
 }
 
 // ------------------------------------------------------------------ small-table gradient
@@ -570,10 +594,16 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
   constexpr int PD = (CT_KT * NCH + 511) / 512;
   constexpr int PR = (CT_KT * CT_MAXSL + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tile = blockIdx.x;
+  // XCD-aware order: the row tiles of one token chunk get consecutive logical ids,
+  // i.e. land on the same XCD, so the chunk's dY streams from HBM once and the
+  // other tiles read it from that XCD's L2 (not once per tile)
+  const int nbl = (int)(gridDim.x * gridDim.z);
+  const int lid = xcd_remap((int)(blockIdx.x + gridDim.x * blockIdx.z), nbl);
+  const int tile = lid % (int)gridDim.x;
+  const int zc = lid / (int)gridDim.x;
   const int row0 = ct.row0[tile], nrow = ct.nrow[tile], sfirst = ct.sfirst[tile], nsl = ct.nsl[tile];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t t0 = (int64_t)blockIdx.z * tok_per_block;
+  const int64_t t0 = (int64_t)zc * tok_per_block;
   const int64_t t1 = min(n, t0 + tok_per_block);
   const int ml = wave * 16 + (lane & 15);
   const bool mvalid = ml < nrow;
@@ -680,7 +710,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
     if (st + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
   }
-  float* out = dst + (direct ? 0 : (int64_t)blockIdx.z * zstride);
+  float* out = dst + (direct ? 0 : (int64_t)zc * zstride);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int rl = wave * 16 + 4 * (lane >> 4) + j;
@@ -814,7 +844,7 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   const int R32 = (R + 31) & ~31;
   const int Dm = d->Dout;
   const size_t sh_mfma = (size_t)2 * 32 * Dm * 2 + (size_t)d->Din * Dm * 4 + (size_t)PE_TOK * d->Din * 4 +
-                         (size_t)PE_TOK * total * 2 + (size_t)R32 * 2;
+                         (size_t)256 * 16 + (size_t)PE_TOK * pe_rbw(R32) * 4;
   int maxnb = 0, nproj = 0;
   for (int j = 0; j < d->n_mod; ++j) {
     maxnb = std::max(maxnb, d->mod_nbins[j]);

@@ -93,7 +93,9 @@ class ContrastiveLossFn(torch.autograd.Function):
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         dev = yc.device
         g = dloss.contiguous().float()
-        d_out = K.zeros((B, T + 1, NH, De), torch.float32, dev)
+        # every element is written by lthm_contrastive_bwd (kept rows by the ROWS kernel,
+        # the t >= L tail of each head by its prologue), so no fill
+        d_out = torch.empty((B, T + 1, NH, De), dtype=torch.float32, device=dev)
         d_in = K.zeros((B, T, De), torch.float32, dev)
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,

@@ -36,7 +36,7 @@ def _run(rank, world, port, fn, q):
             dist.destroy_process_group()
 
 
-def spawn(fn, world=2):
+def _spawn_once(fn, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -46,10 +46,21 @@ def spawn(fn, world=2):
     res = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for r, v in res.items():
-        if isinstance(v, Exception):
-            raise v
-    return [res[r] for r in range(world)]
+    return res
+
+
+def spawn(fn, world=2):
+    # the free port is only probed, not held: another process can take it before the
+    # rendezvous binds it, so an address-in-use rendezvous failure is retried once
+    for attempt in range(2):
+        res = _spawn_once(fn, world)
+        errs = [v for v in res.values() if isinstance(v, Exception)]
+        if attempt == 0 and errs and any("address already in use" in str(e).lower() or "eaddrinuse" in str(e).lower()
+                                         for e in errs):
+            continue
+        for e in errs:
+            raise e
+        return [res[r] for r in range(world)]
 
 
 def _bucket_allreduce(rank, world):
