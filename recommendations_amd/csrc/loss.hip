@@ -222,6 +222,8 @@ struct ClArgs {
   const float* gscale;                             // device scalar dL (bwd)
   float* d_out;                                    // f32 [B, Tp, NH, DE]
   float* d_in;                                     // f32 [B, T, DE] (accumulated)
+  float* colb;  // forward only: per-column exp2 bias (-1/tau log2 e, -inf for pad / beyond n),
+                // kept in the row-weight buffer until cl_stats_k overwrites it
 };
 
 struct Geo {
@@ -282,7 +284,10 @@ __global__ __launch_bounds__(256) void cl_diag_k(ClArgs a) {
       s = bf2f(o[lane]) * bf2f(i[lane]) + bf2f(o[lane + 64]) * bf2f(i[lane + 64]);
       s = wave_sum(s) / a.tau;
     }
-    if (lane == 0) a.diag[(int64_t)mb * a.n_max + r] = s;
+    if (lane == 0) {
+      a.diag[(int64_t)mb * a.n_max + r] = s;
+      if (a.colb) a.colb[(int64_t)mb * a.n_max + r] = s == -INFINITY ? -INFINITY : -(1.f / a.tau) * 1.4426950408889634f;
+    }
   }
 }
 
@@ -466,6 +471,8 @@ struct ClTile {
 };
 
 __device__ __attribute__((aligned(16))) unsigned char cl_zero_row[256];
+__device__ float cl_ninf = -INFINITY;  // per-column values for the columns past n_max of a tile
+__device__ float cl_zero_f = 0.f;
 
 
 // Image-row staging.  Wave w stages rows 16w .. 16w + 15 of every tile with four
@@ -623,7 +630,7 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
   auto stage = [&](int t) {
     const int buf = t % CL_NBUF;
     cur_in.stage(sh.img[buf], g.n, w, lane);
-    glds4(a.diag + base + t * 64 + lane, sh.m0[buf][w]);
+    glds4(t * 64 + lane < a.n_max ? a.colb + base + t * 64 + lane : &cl_ninf, sh.m0[buf][w]);
   };
   retire_loads();
   stage(0);
@@ -636,15 +643,11 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
     if (tI + 2 < ntile) stage(tI + 2);
     f32x4 acc[2][4];
     st_tile(acc, qf, sh.img[cur], lane);
-    const float* cdg = sh.m0[cur][w];  // -inf: pad column or beyond n
+    const float* cdg = sh.m0[cur][w];  // column exp2 bias: cs, or -inf for a pad column / beyond n
     const bool special = !FIXED || (c0 < spec_hi && c0 + 64 > spec_lo);
     if (!special) {
       float cb[4][4];
       col_vals(cb, cdg, rg);
-#pragma unroll
-      for (int yb = 0; yb < 4; ++yb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cb[yb][j] = cb[yb][j] == -INFINITY ? -INFINITY : cs;
       const int np = __popcll(__ballot(cdg[lane] == -INFINITY));
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
@@ -802,8 +805,9 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     const int buf = t % CL_NBUF, y0 = t * 64;
     cur_img.stage(sh.img[buf], g.n, w, lane);
     if (!ROWS) {
-      glds4(shift + base + y0 + lane, sh.m0[buf][w]);
-      glds4(a.w + base + y0 + lane, sh.m1[buf][w]);
+      const bool inr = y0 + lane < a.n_max;  // past n_max: shift -inf, weight 0
+      glds4(inr ? shift + base + y0 + lane : &cl_ninf, sh.m0[buf][w]);
+      glds4(inr ? a.w + base + y0 + lane : &cl_zero_f, sh.m1[buf][w]);
     }
   };
   retire_loads();
@@ -928,6 +932,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.lse = d->lse; a.pos = d->pos; a.cnt = d->cnt; a.rank = d->rank; a.diag = d->diag; a.w = d->w;
   a.gscale = d->gscale;
   a.d_out = d->d_out; a.d_in = d->d_in;
+  a.colb = nullptr;
   return a;
 }
 
@@ -1001,6 +1006,7 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   LTHM_REQUIRE(cl_check(d) == 0 && stats && d->lse && d->pos && d->cnt && d->rank && d->diag && d->w);
   LTHM_REQUIRE(nstat >= 7 + nk);
   ClArgs a = cl_args(d);
+  a.colb = d->w;  // scratch until cl_stats_k writes the row weights
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();

@@ -605,13 +605,25 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t t0 = (int64_t)zc * tok_per_block;
   const int64_t t1 = min(n, t0 + tok_per_block);
-  const int ml = wave * 16 + (lane & 15);
-  const bool mvalid = ml < nrow;
-  const int m = row0 + ml;
-  const int ls = (!GEN && mvalid) ? ct.mslot0[tile] + (m - ct.mrow0[tile]) / ct.rps[tile] - sfirst : 0;
-  f32x4 acc[NF];
+  // for even NF a wave owns 32 table rows (two 16-row MFMA tiles) x D/2 columns, so
+  // every dY fragment read from LDS feeds two MFMAs
+  constexpr int CH = (NF % 2 == 0) ? 2 : 1;
+  constexpr int MT = CH, NFW = NF / CH, RG = 8 / CH;
+  const int rgp = wave % RG, nb0 = (wave / RG) * NFW * 16;
+  int mrow[MT], ls[MT];
+  bool mvalid[MT];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mt = 0; mt < MT; ++mt) {
+    const int ml = rgp * 16 * MT + mt * 16 + (lane & 15);
+    mvalid[mt] = ml < nrow;
+    mrow[mt] = row0 + ml;
+    ls[mt] = (!GEN && mvalid[mt]) ? ct.mslot0[tile] + (mrow[mt] - ct.mrow0[tile]) / ct.rps[tile] - sfirst : 0;
+  }
+  f32x4 acc[MT][NFW];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int f = 0; f < NFW; ++f) acc[mt][f] = f32x4{0.f, 0.f, 0.f, 0.f};
   u32x4 pd[PD];
   uint16_t pr[PR];
   auto fetch = [&](int64_t tb) {
@@ -676,53 +688,65 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
     if (st + 1 < nsteps) fetch(t0 + (st + 1) * CT_KT);  // global loads in flight during the MFMAs
     const unsigned char* img = smem + cur * BUF;
     const uint16_t* rt = reinterpret_cast<const uint16_t*>(img + (F32 ? 2 : 1) * IMG);
-    s16x8 a;
-    if constexpr (GEN) {
-      int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bf16x8v af[MT];
 #pragma unroll
-      for (int sl = 0; sl < CT_GENMAX; ++sl) {
-        if (sl < nsl) {
-          const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + sl * CT_KT + 8 * (lane >> 4));
+    for (int mt = 0; mt < MT; ++mt) {
+      s16x8 a;
+      if constexpr (GEN) {
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
-            cnt[i] += ((int)rr == m) ? 1 : 0;
+        for (int sl = 0; sl < CT_GENMAX; ++sl) {
+          if (sl < nsl) {
+            const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + sl * CT_KT + 8 * (lane >> 4));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
+              cnt[i] += ((int)rr == mrow[mt]) ? 1 : 0;
+            }
           }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = mvalid ? (short)f2bf((float)cnt[i]) : (short)0;
-    } else {
-      const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls * CT_KT + 8 * (lane >> 4));
+        for (int i = 0; i < 8; ++i) a[i] = mvalid[mt] ? (short)f2bf((float)cnt[i]) : (short)0;
+      } else {
+        const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls[mt] * CT_KT + 8 * (lane >> 4));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
-        a[i] = (mvalid && (int)rr == m) ? (short)0x3F80 : (short)0;
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
+          a[i] = (mvalid[mt] && (int)rr == mrow[mt]) ? (short)0x3F80 : (short)0;
+        }
       }
+      af[mt] = __builtin_bit_cast(bf16x8v, a);
     }
-    const bf16x8v af = __builtin_bit_cast(bf16x8v, a);
 #pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img, f * 16, lane), acc[f], 0, 0, 0);
-      if constexpr (F32)
-        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ct_tr_frag<D>(img + IMG, f * 16, lane), acc[f], 0, 0, 0);
+    for (int f = 0; f < NFW; ++f) {
+      const bf16x8v bh = ct_tr_frag<D>(img, nb0 + f * 16, lane);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bh, acc[mt][f], 0, 0, 0);
+      if constexpr (F32) {
+        const bf16x8v bl = ct_tr_frag<D>(img + IMG, nb0 + f * 16, lane);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bl, acc[mt][f], 0, 0, 0);
+      }
     }
     if (st + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
   }
   float* out = dst + (direct ? 0 : (int64_t)zc * zstride);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rl = wave * 16 + 4 * (lane >> 4) + j;
-    if (rl < nrow) {
-      float* p = out + (int64_t)(row0 + rl) * D + (lane & 15);
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        if (direct) p[f * 16] += acc[f][j];
-        else p[f * 16] = acc[f][j];
+    for (int j = 0; j < 4; ++j) {
+      const int rl = rgp * 16 * MT + mt * 16 + 4 * (lane >> 4) + j;
+      if (rl < nrow) {
+        float* p = out + (int64_t)(row0 + rl) * D + nb0 + (lane & 15);
+#pragma unroll
+        for (int f = 0; f < NFW; ++f) {
+          if (direct) p[f * 16] += acc[mt][f][j];
+          else p[f * 16] = acc[mt][f][j];
+        }
       }
     }
-  }
 }
 
 // ------------------------------------------------------------------ token assembly
