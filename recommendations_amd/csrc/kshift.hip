@@ -436,10 +436,59 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
   return 0;
 }
 
+// K = 1 (FlatEmbedding / table-batched flat lookups, e.g. the C4 ranker) with a
+// plain or /sqrt(K) output: every item touches one row, so the LDS dedup and
+// sort buy nothing for uniform ids.  A row's D columns map to D consecutive lanes
+// (64 / D items per wave instruction, each f32 atomic instruction covering
+// whole rows).  The first lane of an item marks the row touched; a block
+// collects its newly touched rows of a K1_CHUNK-item chunk in LDS and reserves
+// their list slots with ONE global atomic (a same-address atomic per wave
+// serialises at one L2 channel).
+constexpr int K1_CHUNK = 1024;
+template <typename TY>
+__global__ __launch_bounds__(256) void kshift_bwd_k1_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
+                                                       const TY* __restrict__ dY, int64_t P, int D,
+                                                       float* __restrict__ dW, int32_t* __restrict__ flags,
+                                                       int64_t* __restrict__ list,
+                                                       unsigned long long* __restrict__ count) {
+  __shared__ int64_t s_new[K1_CHUNK];
+  __shared__ int s_nnew;
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ipw = 64 / D;  // items per wave instruction
+  const int il = lane / D, d = lane - il * D;
+  for (int64_t c0 = (int64_t)blockIdx.x * K1_CHUNK; c0 < n_items; c0 += (int64_t)gridDim.x * K1_CHUNK) {
+    if (tid == 0) s_nnew = 0;
+    __syncthreads();
+    const int64_t c1 = min(n_items, c0 + K1_CHUNK);
+    for (int64_t b = c0 + (int64_t)wave * ipw; b < c1; b += 4 * ipw) {
+      const int64_t item = b + il;
+      if (item < c1) {
+        const int64_t row = ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], 0, P);
+        atomicAdd(dW + row * D + d, Elem<TY>::ld(dY + item * D + d));  // /sqrt(K) = 1 for the scale mode
+        if (flags != nullptr && d == 0 && atomicExch(flags + row, 1) == 0) s_new[atomicAdd(&s_nnew, 1)] = row;
+      }
+    }
+    __syncthreads();
+    if (flags != nullptr) {
+      if (tid == 0) s_base = s_nnew ? atomicAdd(count, (unsigned long long)s_nnew) : 0ull;
+      __syncthreads();
+      for (int i = tid; i < s_nnew; i += 256) list[s_base + i] = s_new[i];
+    }
+    __syncthreads();
+  }
+}
+
 template <typename TY, typename TO>
 static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY, const void* out,
                       const float* norms, int64_t P, int D, int K, int mode, float* dW, int32_t* flags,
                       int64_t* list, unsigned long long* count, hipStream_t s) {
+  if (K == 1 && mode != LTHM_KSHIFT_NORMALIZE && D <= 64 && 64 % D == 0) {
+    hipLaunchKernelGGL((kshift_bwd_k1_k<TY>), dim3(grid_for(n_items, K1_CHUNK, 256 * 8)), dim3(256), 0, s, ids,
+                       n_items, F, (const TY*)dY, P, D, dW, flags, list, count);
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   int ch = KB_NP / K;
   if (ch * D > KB_G_FLOATS) ch = KB_G_FLOATS / D;
   LTHM_REQUIRE(ch >= 1);

@@ -54,10 +54,14 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
                                                       float b2, float eps, float wd, float bc1, float bc2_sqrt,
                                                       bf16_t* __restrict__ shadow) {
   const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
+  // D <= 64 dividing 64: 64 / D rows per wave (all lanes busy); else one row per wave
   const int lane = threadIdx.x & 63;
-  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < cnt; k += (int64_t)gridDim.x * 4) {
+  const int rpw = (D <= 64 && 64 % D == 0) ? 64 / D : 1;
+  const int sub = rpw > 1 ? lane / D : 0, d0 = rpw > 1 ? lane - sub * D : lane;
+  for (int64_t k = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + sub; k < cnt;
+       k += (int64_t)gridDim.x * 4 * rpw) {
     const int64_t r = rows[k];
-    for (int d = lane; d < D; d += 64) {
+    for (int d = d0; d < D; d += 64) {
       const int64_t i = r * D + d;
       const float gi = g[i];
       float pi = p[i] * (1.f - lr * wd);
@@ -70,7 +74,7 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
     }
-    if (lane == 0) flags[r] = 0;
+    if (d0 == 0) flags[r] = 0;
   }
 }
 
@@ -80,9 +84,12 @@ __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restric
                                                         bf16_t* __restrict__ shadow) {
   const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
   const int lane = threadIdx.x & 63;
-  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < cnt; k += (int64_t)gridDim.x * 4) {
+  const int rpw = (D <= 64 && 64 % D == 0) ? 64 / D : 1;
+  const int sub = rpw > 1 ? lane / D : 0, d0 = rpw > 1 ? lane - sub * D : lane;
+  for (int64_t k = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + sub; k < cnt;
+       k += (int64_t)gridDim.x * 4 * rpw) {
     const int64_t r = rows[k];
-    for (int d = lane; d < D; d += 64) {
+    for (int d = d0; d < D; d += 64) {
       const int64_t i = r * D + d;
       const float gi = g[i];
       const float si = s[i] + gi * gi;
@@ -92,7 +99,7 @@ __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restric
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
     }
-    if (lane == 0) flags[r] = 0;
+    if (d0 == 0) flags[r] = 0;
   }
 }
 
