@@ -326,9 +326,11 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   const int R32 = (R + 31) & ~31;
   const int RBW = pe_rbw(R32);
   const int64_t t0 = (int64_t)blockIdx.x * PE_TOK;
-  const bf16_t* tab = reinterpret_cast<const bf16_t*>(d.tables);
+  // Dout > 256: blockIdx.y picks a 256-wide column slice of the ldt = Dout wide rows
+  const int ldt = D * (int)gridDim.y, col0 = D * (int)blockIdx.y;
+  const bf16_t* tab = reinterpret_cast<const bf16_t*>(d.tables) + col0;
   // ---- per-block staging: mapper weights, 0/1 octet table, row bitmask, normalised x
-  for (int i = tid; i < Din * D; i += 512) wN[i] = d.w_map[i];
+  for (int i = tid; i < Din * D; i += 512) wN[i] = d.w_map[(int64_t)col0 * Din + i];
   if (tid < 256) {
     u32x4 v;
 #pragma unroll
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
       const int idx = tid + 512 * q;
       const int r = idx / (D / 8), c = idx - r * (D / 8);
       pf[q] = u32x4{0u, 0u, 0u, 0u};
-      if (idx < 32 * D / 8 && k0 + r < R) pf[q] = *reinterpret_cast<const u32x4*>(tab + (int64_t)(k0 + r) * D + c * 8);
+      if (idx < 32 * D / 8 && k0 + r < R) pf[q] = *reinterpret_cast<const u32x4*>(tab + (int64_t)(k0 + r) * ldt + c * 8);
     }
   };
   auto store = [&](int buf) {
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out);
   float bias[NFW];
 #pragma unroll
-  for (int f = 0; f < NFW; ++f) bias[f] = d.b_map ? d.b_map[nb0 + f * 16 + (lane & 15)] : 0.f;
+  for (int f = 0; f < NFW; ++f) bias[f] = d.b_map ? d.b_map[col0 + nb0 + f * 16 + (lane & 15)] : 0.f;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -468,7 +470,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
       const bool masked = d.mask_out[t] != 0;
 #pragma unroll
       for (int f = 0; f < NFW; ++f)
-        eo[t * D + nb0 + f * 16 + (lane & 15)] = f2bf(masked ? 0.f : acc[mt][f][j] + bias[f]);
+        eo[t * ldt + col0 + nb0 + f * 16 + (lane & 15)] = f2bf(masked ? 0.f : acc[mt][f][j] + bias[f]);
     }
 }
 
@@ -867,7 +869,9 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   const int R = d->cve_rows + (d->norm_bins > 0 ? d->norm_bins : 0);
   const int R32 = (R + 31) & ~31;
   const int Dm = d->Dout;
-  const size_t sh_mfma = (size_t)2 * 32 * Dm * 2 + (size_t)d->Din * Dm * 4 + (size_t)PE_TOK * d->Din * 4 +
+  const int nsl = (Dm > 256 && Dm % 256 == 0) ? Dm / 256 : 1;  // 256-wide column slices (grid.y)
+  const int Ds = Dm / nsl;
+  const size_t sh_mfma = (size_t)2 * 32 * Ds * 2 + (size_t)d->Din * Ds * 4 + (size_t)PE_TOK * d->Din * 4 +
                          (size_t)256 * 16 + (size_t)PE_TOK * pe_rbw(R32) * 4;
   int maxnb = 0, nproj = 0;
   for (int j = 0; j < d->n_mod; ++j) {
@@ -875,7 +879,7 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
     nproj += d->mod_nproj[j];
   }
   const bool mfma = !d->cve_only && d->tab_dtype == LTHM_BF16 && d->emb_dtype == LTHM_BF16 && d->rows_out &&
-                    d->mask_out && d->ids && (Dm == 16 || Dm == 32 || Dm == 64 || Dm == 128 || Dm == 256) && R > 0 &&
+                    d->mask_out && d->ids && (Ds == 16 || Ds == 32 || Ds == 64 || Ds == 128 || Ds == 256) && nsl <= 4 && R > 0 &&
                     R <= PE_MAXR && sh_mfma <= 160 * 1024 && d->Din <= PR_DMAX && d->Din % 4 == 0 &&
                     maxnb <= PR_NBMAX && nproj <= 256;
   if (mfma) {
@@ -888,9 +892,9 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
       else hipLaunchKernelGGL((ptower_rows_k<float, 64>), g1, dim3(256), 0, s, *d, total);
     }
     LTHM_CHECK_LAUNCH();
-    const dim3 g2((unsigned)((d->n + PE_TOK - 1) / PE_TOK));
+    const dim3 g2((unsigned)((d->n + PE_TOK - 1) / PE_TOK), (unsigned)nsl);
 #define LTHM_PT_EMB(TX)                                                                                     \
-  switch (Dm) {                                                                                             \
+  switch (Ds) {                                                                                             \
     case 16: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 1>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
     case 32: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 2>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
     case 64: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 4>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \

@@ -10,9 +10,17 @@ import numpy as np
 import pytest
 import torch
 
+import torch.nn.functional as F
+
+from oracle import ref
 from recommendations_amd import kernels as K
 
 pytestmark = pytest.mark.gpu
+
+
+def relerr(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def table_ref(rows, dy, R, segments=None):
@@ -182,3 +190,45 @@ def test_kshift_sparse_touched_rows(dev, P, D, Kk, F, n):
     np.testing.assert_array_equal(got, want)
     fl = flags.cpu().numpy()
     assert fl[want].all() and fl.sum() == len(want)
+
+
+@pytest.mark.parametrize("Dout", [64, 256, 512])
+def test_product_tower_fwd_vs_oracle(dev, Dout):
+    """ProductTower.forward (product_tower.py:43-62): norm mask, normalise, emb_mapper,
+    6 CVE bag-sums, norm histogram, mask fill, product_mapper.  Dout = 512 (C5) runs
+    the MFMA one-hot kernel in two 256-column slices.  bf16 outputs: 2e-2 relative
+    Frobenius vs the fp32 oracle composition (a bucket id can flip where the f32
+    projection lands on a grid edge in a different summation order)."""
+    from types import SimpleNamespace
+    from recommendations_amd.models.lthm.config import lthm_config
+    from recommendations_amd.models.lthm.sequence.product_tower import ProductTower
+    torch.manual_seed(Dout)
+    cfg = lthm_config(T=16, d=64, n_layers=1, n_head=1, out_emb_dim=Dout, item_vocab=1000)
+    pt = cfg.product_tower
+    m = ProductTower(cfg)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.normal_(0.0, 0.5)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    B, T = 8, 150
+    ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (B, T), dtype=torch.int64)
+    ids[:, -20:] = 0
+    x = torch.randn(B, T, pt.inp_emb_dim)
+    x[0, :5] *= 1e-3  # below the norm threshold -> masked
+    emb, prod, mask = m(ids.to(dev), x.to(dev))
+    xn_ = x.norm(p=2.0, dim=-1)
+    mref = torch.logical_or(xn_ < pt.norm_threshold, ids == 0)
+    xn = F.normalize(x, p=2.0, dim=-1)
+    e = F.linear(xn, sd["emb_mapper.weight"], sd["emb_mapper.bias"])
+    for j in range(len(pt.cosine_lsh_config)):
+        pre = f"direction_emb.{j}."
+        e = e + ref.cve_fwd(xn, sd[pre + "projection_mat"], sd[pre + "grid"], sd[pre + "pos_offset"],
+                            sd[pre + "emb.weight"])
+    if pt.norm_bins > 1:
+        e = e + ref.histogram_embedding(xn_, 0.0, 1.0, pt.norm_bins, sd["norm_emb.emb.weight"])
+    e = e.masked_fill(mref.unsqueeze(-1), 0.0)
+    pr = F.linear(e, sd["product_mapper.weight"])
+    assert (mask.cpu().bool() == mref).all()
+    assert relerr(emb.float(), e) < 2e-2
+    assert relerr(prod.float(), pr) < 2e-2
