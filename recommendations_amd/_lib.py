@@ -33,6 +33,7 @@ _CTYPE = {
     "void*": ctypes.c_void_p,
     "char*": ctypes.c_char_p,
     "char**": ctypes.c_void_p,
+    "float**": ctypes.c_void_p,
     "int64_t": ctypes.c_int64,
     "uint64_t": ctypes.c_uint64,
     "int32_t": ctypes.c_int32,
@@ -128,8 +129,9 @@ class KernelTimer:
     stream every launch goes to).  bench.py enables it over the timed region;
     ``work`` is the algorithmic bytes / flops the wrapper declares per call."""
 
-    def __init__(self):
+    def __init__(self, only=None):
         self.records = []  # (key, ev0, ev1, work, unit)
+        self.only = None if only is None else set(only)  # time just these keys (others run untouched)
 
     def summary(self):
         torch.cuda.synchronize()
@@ -148,7 +150,7 @@ TIMER = None  # type: KernelTimer
 def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = None) -> None:
     lib = load()
     t = TIMER
-    if t is not None:
+    if t is not None and (t.only is None or (_key or name) in t.only):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()

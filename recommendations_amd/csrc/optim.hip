@@ -34,6 +34,42 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ p, float* __r
   }
 }
 
+// Multi-tensor AdamW: up to AW_MT tensors per launch (kernel-argument pointer
+// table), element i of the concatenation found by a binary search of the
+// prefix offsets.  Same update as adamw_k; one launch instead of one per tensor.
+constexpr int AW_MT = 48;
+struct AdamWList {
+  float* p[AW_MT];
+  float* g[AW_MT];
+  float* m[AW_MT];
+  float* v[AW_MT];
+  int64_t off[AW_MT + 1];
+  int nt;
+};
+__global__ __launch_bounds__(256) void adamw_multi_k(AdamWList L, float lr, float b1, float b2, float eps, float wd,
+                                                     float bc1, float bc2_sqrt, float gscale) {
+  const int64_t total = L.off[L.nt];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = L.nt - 1;
+    while (lo < hi) {  // largest t with off[t] <= i
+      const int mid = (lo + hi + 1) >> 1;
+      if (L.off[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t j = i - L.off[lo];
+    float* __restrict__ p = L.p[lo];
+    float* __restrict__ m = L.m[lo];
+    float* __restrict__ v = L.v[lo];
+    const float gi = L.g[lo][j] * gscale;
+    float pi = p[j] * (1.f - lr * wd);
+    const float mi = b1 * m[j] + (1.f - b1) * gi;
+    const float vi = b2 * v[j] + (1.f - b2) * gi * gi;
+    m[j] = mi;
+    v[j] = vi;
+    p[j] = pi - (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
+  }
+}
+
 __global__ __launch_bounds__(256) void adagrad_k(float* __restrict__ p, float* __restrict__ g, float* __restrict__ s,
                                                  int64_t n, float clr, float eps, float wd, int zero_grad) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -145,6 +181,31 @@ extern "C" int lthm_adamw(float* p, float* g, float* m, float* v, int64_t n, flo
   hipLaunchKernelGGL(adamw_k, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                      beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale, (bf16_t*)bf16_shadow, zero_grad);
   LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_adamw_multi(int32_t count, float** p, float** g, float** m, float** v,
+                                const int64_t* n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                                int64_t step, float grad_scale, void* stream) {
+  LTHM_REQUIRE(count >= 0 && step >= 1 && (count == 0 || (p && g && m && v && n)));
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2 = 1.f - powf(beta2, (float)step);
+  for (int t0 = 0; t0 < count; t0 += AW_MT) {
+    AdamWList L;
+    L.nt = 0;
+    L.off[0] = 0;
+    for (int t = t0; t < count && t < t0 + AW_MT; ++t) {
+      LTHM_REQUIRE(n[t] >= 0 && (n[t] == 0 || (p[t] && g[t] && m[t] && v[t])));
+      if (n[t] == 0) continue;
+      L.p[L.nt] = p[t]; L.g[L.nt] = g[t]; L.m[L.nt] = m[t]; L.v[L.nt] = v[t];
+      L.off[L.nt + 1] = L.off[L.nt] + n[t];
+      ++L.nt;
+    }
+    if (L.nt == 0) continue;
+    hipLaunchKernelGGL(adamw_multi_k, dim3(grid_for(L.off[L.nt], 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream,
+                       L, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale);
+    LTHM_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -405,6 +405,24 @@ def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, ze
          grad_scale, ptr(shadow), int(zero_grad), stream())
 
 
+def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0):
+    """lthm_adamw_multi: one launch per 48 fp32 tensors with identical hyper-parameters and step."""
+    import ctypes
+    n = len(ps)
+    for p, g, m, v in zip(ps, gs, ms, vs):
+        require_gpu(p)
+        for t, nm in ((g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+            _need(t, p.numel(), nm)
+        _check(all(t.dtype == torch.float32 and t.is_contiguous() for t in (p, g, m, v)),
+               "adamw_multi_ takes contiguous fp32 tensors")
+    arr = lambda ts: (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in ts])  # noqa: E731
+    cnt = (ctypes.c_int64 * max(n, 1))(*[p.numel() for p in ps])
+    call("lthm_adamw_multi", n, ctypes.cast(arr(ps), ctypes.c_void_p), ctypes.cast(arr(gs), ctypes.c_void_p),
+         ctypes.cast(arr(ms), ctypes.c_void_p), ctypes.cast(arr(vs), ctypes.c_void_p),
+         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, stream(),
+         _key="lthm_adamw", _work=28.0 * sum(p.numel() for p in ps), _unit="byte")
+
+
 def adagrad_(p, g, s, lr, lr_decay, eps, wd, step, zero_grad=False):
     _need(g, p.numel(), "grad")
     _need(s, p.numel(), "state_sum")

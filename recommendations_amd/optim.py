@@ -22,8 +22,11 @@ class FusedAdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
+        """One multi-tensor launch per (param group, step count) bucket of up to 48
+        tensors (lthm_adamw_multi) instead of one launch per parameter."""
         loss = closure() if closure is not None else None
         for g in self.param_groups:
+            buckets = {}
             for p in g["params"]:
                 if p.grad is None:
                     continue
@@ -36,8 +39,12 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = K.zeros(p.shape, torch.float32, p.device)
                 st["step"] += 1
                 grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                K.adamw_(p.data, grad, st["exp_avg"], st["exp_avg_sq"], g["lr"], g["betas"], g["eps"],
-                         g["weight_decay"], st["step"], grad_scale=grad_scale)
+                b = buckets.setdefault(st["step"], ([], [], [], []))
+                for lst, t in zip(b, (p.data, grad, st["exp_avg"], st["exp_avg_sq"])):
+                    lst.append(t)
+            for step, (ps, gs, ms, vs) in buckets.items():
+                K.adamw_multi_(ps, gs, ms, vs, g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
+                               grad_scale=grad_scale)
         return loss
 
 

@@ -1,0 +1,31 @@
+"""FusedAdamW (multi-tensor lthm_adamw_multi) vs torch.optim.AdamW
+(wrapper.py:263-275 hyper-parameters), fp32 elementwise: 1e-6 relative (torch
+uses lerp for the first moment, the kernel the b1 m + (1 - b1) g form)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fused_adamw_multi_matches_torch(dev):
+    from recommendations_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    shapes = [(0,)] + [(int(s),) for s in torch.randint(1, 5000, (55,))] + [(256, 768), (1024, 256), (3, 5, 7)]
+    ps = [torch.randn(s) for s in shapes]
+    mine = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    kw = dict(lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=1e-3)
+    o1, o2 = FusedAdamW(mine, **kw), torch.optim.AdamW(ref, **kw, foreach=False)
+    for it in range(3):
+        gs = [torch.randn(s) for s in shapes]
+        for a, b, gr in zip(mine, ref, gs):
+            a.grad, b.grad = gr.to(dev), gr.clone()
+        if it == 1:  # a parameter without a gradient is skipped
+            mine[5].grad = ref[5].grad = None
+        o1.step()
+        o2.step()
+    for a, b in zip(mine, ref):
+        d = (a.detach().cpu() - b.detach()).abs().max() if a.numel() else torch.tensor(0.0)
+        assert float(d) <= 1e-6 * max(1.0, float(b.detach().abs().max()) if b.numel() else 1.0)
+    st = o1.state[mine[5]]
+    assert st["step"] == 2 and o1.state[mine[6]]["step"] == 3
