@@ -111,6 +111,8 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
 #define LTHM_ACT_QGELU 2       /* QuickGELU x*sigmoid(1.702x)   commons/layers.py:9-11    */
 #define LTHM_ACT_GELU_GRAD 3   /* multiply by GELU'(aux)   (backward epilogue)            */
 #define LTHM_ACT_QGELU_GRAD 4  /* multiply by QuickGELU'(aux)                             */
+#define LTHM_ACT_GELU_D 5      /* GELU, but aux_out receives GELU'(x) (bf16), not x      */
+#define LTHM_ACT_MUL_AUX 6     /* multiply by aux (a derivative saved by LTHM_ACT_GELU_D) */
 
 /* C[b] = epi(alpha * A[b] . B[b]), bf16 operands, fp32 accumulation (MFMA).
  *   a_kcontig: A is [M][K] (row stride lda) else A is [K][M] (row stride lda)

@@ -81,8 +81,9 @@ class TransformerBlockFn(torch.autograd.Function):
         o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
         x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+        # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
-        g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU, aux_out=pre)
+        g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre)
         out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
         ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
@@ -103,7 +104,7 @@ class TransformerBlockFn(torch.autograd.Function):
         # MLP half
         dw2 = K.linear_wgrad(dyb, g)
         db2 = K.colsum(dy) if has_b2 else None
-        dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_GELU_GRAD, aux=pre)
+        dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_MUL_AUX, aux=pre)
         dw1 = K.linear_wgrad(dpre, h2)
         db1 = K.colsum(dpre) if has_b1 else None
         dh2 = K.linear_dgrad(dpre, w1_b)

@@ -63,6 +63,14 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float r = gelu_r(x);
   return (1.f - r) * __builtin_fmaf(2.f * kb * x * r, __builtin_fmaf(k3, x * x, 1.f), 1.f);
 }
+// gelu(x) and gelu'(x) from one v_exp + one v_rcp (the forward that saves the
+// derivative for the backward's plain multiply, LTHM_ACT_GELU_D)
+__device__ __forceinline__ float gelu_tanh_and_grad(float x, float& dg) {
+  constexpr float kb = 0.7978845608028654f, k3 = 3.f * 0.044715f;
+  const float r = gelu_r(x), q = 1.f - r;
+  dg = q * __builtin_fmaf(2.f * kb * x * r, __builtin_fmaf(k3, x * x, 1.f), 1.f);
+  return x * q;
+}
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 __device__ __forceinline__ float qgelu(float x) { return x * sigmoidf_(1.702f * x); }
 __device__ __forceinline__ float qgelu_grad(float x) {
@@ -83,6 +91,12 @@ __device__ __forceinline__ float epilogue(const GemmArgs g, float v, int64_t row
     v *= gelu_tanh_grad(bf2f(g.aux[b * g.M * g.ldaux + row * g.ldaux + col]));
   } else if (g.act == LTHM_ACT_QGELU_GRAD) {
     v *= qgelu_grad(bf2f(g.aux[b * g.M * g.ldaux + row * g.ldaux + col]));
+  } else if (g.act == LTHM_ACT_GELU_D) {
+    float dv;
+    v = gelu_tanh_and_grad(v, dv);
+    if (g.aux_out) g.aux_out[b * g.M * g.ldaux + row * g.ldaux + col] = f2bf(dv);
+  } else if (g.act == LTHM_ACT_MUL_AUX) {
+    v *= bf2f(g.aux[b * g.M * g.ldaux + row * g.ldaux + col]);
   }
   if (g.res1) v += ld_any(g.res1, g.res1_dt, b * g.M * g.ldr1 + row * g.ldr1 + col);
   if (g.res2) v += ld_any(g.res2, g.res2_dt, b * g.M * g.ldr2 + row * g.ldr2 + col);
@@ -164,6 +178,15 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, float (&v)[8], int6
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(t[e]);
     }
+  } else if (g.act == LTHM_ACT_GELU_D) {
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh_and_grad(v[e], dv[e]);
+    if (g.aux_out) st8(g.aux_out, LTHM_BF16, ai, nv, dv);
+  } else if (g.act == LTHM_ACT_MUL_AUX) {
+    ld8(g.aux, LTHM_BF16, ai, nv, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= t[e];
   }
   if (g.res1) {
     ld8(g.res1, g.res1_dt, b * g.M * g.ldr1 + row * g.ldr1 + col0, nv, t);
@@ -439,8 +462,8 @@ constexpr int PS_NLW = 4;  // loader waves
 constexpr int PS_THREADS = 64 * (4 + PS_NLW);
 // epilogue forms
 constexpr int EPI_PLAIN = 0;  // (+ bias)
-constexpr int EPI_ACT = 1;    // (+ bias), GELU / QuickGELU, optional pre-activation store
-constexpr int EPI_GRAD = 2;   // * act'(aux)
+constexpr int EPI_ACT = 1;    // (+ bias), GELU / QuickGELU, optional pre-activation (or GELU') store
+constexpr int EPI_GRAD = 2;   // * act'(aux), or * aux
 constexpr int EPI_RES1 = 3;   // (+ bias) + res1 (f32)
 constexpr int EPI_RES2 = 4;   // (+ bias) + res1 + res2 (f32)
 __device__ __attribute__((aligned(16))) unsigned char gemm_zero16[16];
@@ -655,17 +678,27 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
         for (int e = 0; e < 8; ++e) v[e] = alpha * v[e] + bias[e];
         const bool ok = row < g.M && col0 < g.N;
         if constexpr (EPI == EPI_ACT) {
-          if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, v);
-          if (g.act == LTHM_ACT_GELU) {
+          if (g.act == LTHM_ACT_GELU_D) {
+            float dv[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+            for (int e = 0; e < 8; ++e) v[e] = gelu_tanh_and_grad(v[e], dv[e]);
+            if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, dv);
           } else {
+            if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, v);
+            if (g.act == LTHM_ACT_GELU) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = qgelu(v[e]);
+              for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = qgelu(v[e]);
+            }
           }
         }
         if constexpr (EPI == EPI_GRAD) {
-          if (g.act == LTHM_ACT_GELU_GRAD) {
+          if (g.act == LTHM_ACT_MUL_AUX) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= q.x[u][e];
+          } else if (g.act == LTHM_ACT_GELU_GRAD) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(q.x[u][e]);
           } else {
@@ -825,8 +858,9 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   // any shape / stride: aligned full chunks take 16-B loads, ragged tails element loads
   LTHM_REQUIRE(((uintptr_t)d->A % 2) == 0 && ((uintptr_t)d->B % 2) == 0);
   LTHM_REQUIRE(d->lda >= (ka ? d->K : d->M) && d->ldb >= (kb ? d->K : d->N));
-  LTHM_REQUIRE(d->act >= 0 && d->act <= LTHM_ACT_QGELU_GRAD);
-  LTHM_REQUIRE(!(d->act == LTHM_ACT_GELU_GRAD || d->act == LTHM_ACT_QGELU_GRAD) || d->aux != nullptr);
+  LTHM_REQUIRE(d->act >= 0 && d->act <= LTHM_ACT_MUL_AUX);
+  LTHM_REQUIRE(!(d->act == LTHM_ACT_GELU_GRAD || d->act == LTHM_ACT_QGELU_GRAD || d->act == LTHM_ACT_MUL_AUX) ||
+               d->aux != nullptr);
   int splits = d->splits < 1 ? 1 : d->splits;
   LTHM_REQUIRE(splits == 1 || d->workspace != nullptr);
   GemmArgs g;
@@ -890,8 +924,11 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     const int act = d->act;
     if (!a16 || !ax) epi = -1;
     else if (act == LTHM_ACT_NONE && !d->res1 && !d->res2) epi = EPI_PLAIN;
-    else if ((act == LTHM_ACT_GELU || act == LTHM_ACT_QGELU) && !d->res1 && !d->res2) epi = EPI_ACT;
-    else if ((act == LTHM_ACT_GELU_GRAD || act == LTHM_ACT_QGELU_GRAD) && !d->bias && !d->res1 && !d->res2) epi = EPI_GRAD;
+    else if ((act == LTHM_ACT_GELU || act == LTHM_ACT_QGELU || act == LTHM_ACT_GELU_D) && !d->res1 && !d->res2)
+      epi = EPI_ACT;
+    else if ((act == LTHM_ACT_GELU_GRAD || act == LTHM_ACT_QGELU_GRAD || act == LTHM_ACT_MUL_AUX) && !d->bias &&
+             !d->res1 && !d->res2)
+      epi = EPI_GRAD;
     else if (act == LTHM_ACT_NONE && r1 && !d->res2) epi = EPI_RES1;
     else if (act == LTHM_ACT_NONE && r1 && r2) epi = EPI_RES2;
   }

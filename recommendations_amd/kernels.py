@@ -141,6 +141,8 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
 
 # ----------------------------------------------------------------- GEMM
 ACT_NONE, ACT_GELU, ACT_QGELU, ACT_GELU_GRAD, ACT_QGELU_GRAD = 0, 1, 2, 3, 4
+# GELU whose aux_out receives GELU'(x), and the backward's plain multiply by that saved derivative
+ACT_GELU_D, ACT_MUL_AUX = 5, 6
 _ws_cache = {}
 
 

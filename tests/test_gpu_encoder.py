@@ -31,7 +31,7 @@ def bf(x):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(1000, 768, 256), (129, 256, 256), (4096, 1024, 256), (333, 64, 1024), (8, 8, 8)])
-@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("act", [0, 1, 2, 5])
 def test_gemm_nt_epilogues(dev, M, N, Kd, act):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(M + N + Kd + act)
@@ -43,9 +43,14 @@ def test_gemm_nt_epilogues(dev, M, N, Kd, act):
     out = K.linear_fwd(A.to(dev), W.to(dev), bias=bias.to(dev), act=act, aux_out=pre if act else None,
                        res1=res.to(dev), out_dtype=torch.float32)
     z = A.float() @ W.float().T + bias
-    exp = {0: z, 1: F.gelu(z, approximate="tanh"), 2: ref.quick_gelu(z)}[act] + res
+    exp = {0: z, 1: F.gelu(z, approximate="tanh"), 2: ref.quick_gelu(z), 5: F.gelu(z, approximate="tanh")}[act] + res
     assert relerr(out, exp) < 1e-5
-    if act:
+    if act == K.ACT_GELU_D:
+        # the saved aux is GELU'(z), rounded once to bf16
+        zz = z.clone().requires_grad_(True)
+        F.gelu(zz, approximate="tanh").sum().backward()
+        assert (pre.float().cpu() - zz.grad).abs().max() < 1.5 * 2.0 ** -8 * zz.grad.abs().max() + 1e-6
+    elif act:
         assert relerr(pre.float(), bf(z).float()) < 1e-2 and (pre.float().cpu() - z).abs().max() < 0.05
     # bf16 output: within 1 bf16 ulp of the rounded oracle
     outb = K.linear_fwd(A.to(dev), W.to(dev), bias=bias.to(dev), act=act, aux_out=pre if act else None)
@@ -66,6 +71,8 @@ def test_gemm_dgrad_wgrad(dev, M, N, Kd):
     p = pre.float().requires_grad_(True)
     F.gelu(p, approximate="tanh").backward(dy.float() @ W.float())
     assert relerr(dxg, p.grad) < 1e-5
+    dxm = K.linear_dgrad(dy.to(dev), W.to(dev), act_grad=K.ACT_MUL_AUX, aux=pre.to(dev), out_dtype=torch.float32)
+    assert relerr(dxm, (dy.float() @ W.float()) * pre.float()) < 1e-5
     dw = K.linear_wgrad(dy.to(dev), X.to(dev))
     assert relerr(dw, dy.float().T @ X.float()) < 1e-5
 
