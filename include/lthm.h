@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 14 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 15 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -442,12 +442,15 @@ int lthm_contrastive_bwd(const lthm_contrastive_desc* desc, void* stream);
 int lthm_adamw(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                float eps, float weight_decay, int64_t step, float grad_scale, void* bf16_shadow,
                int32_t zero_grad, void* stream);
-/* Multi-tensor form of lthm_adamw (no shadow, no grad zeroing): `count` tensors given by
+/* Multi-tensor form of lthm_adamw (optional bf16 shadows pb, no grad zeroing): `count` tensors given by
  * host arrays of device pointers p/g/m/v and element counts n, all with the same
  * hyper-parameters and step; one launch per 48 tensors (torch.optim.AdamW foreach). */
 int lthm_adamw_multi(int32_t count, float** p, float** g, float** m, float** v,
                      const int64_t* n, float lr, float beta1, float beta2, float eps, float weight_decay,
-                     int64_t step, float grad_scale, void* stream);
+                     int64_t step, float grad_scale, void** pb, void* stream);
+/* pb: NULL, or per tensor NULL / a bf16 buffer of n[t] elements that receives the
+ * updated parameter rounded to bf16 (the next forward's GEMM operand, so no
+ * separate per-step weight cast) */
 /* torch.optim.Adagrad step (embedding_module_gen.py:97,137) */
 int lthm_adagrad(float* p, float* g, float* state_sum, int64_t n, float lr, float lr_decay, float eps,
                  float weight_decay, int64_t step, int32_t zero_grad, void* stream);

@@ -34,6 +34,7 @@ _CTYPE = {
     "char*": ctypes.c_char_p,
     "char**": ctypes.c_void_p,
     "float**": ctypes.c_void_p,
+    "void**": ctypes.c_void_p,
     "int64_t": ctypes.c_int64,
     "uint64_t": ctypes.c_uint64,
     "int32_t": ctypes.c_int32,

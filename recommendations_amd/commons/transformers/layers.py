@@ -25,7 +25,13 @@ from ..._lib import require_gpu
 
 
 def _bf(w):
-    return None if w is None else K.cast(w.detach().contiguous(), torch.bfloat16)
+    """bf16 GEMM operand of a weight: fp32 parameters reuse the shadow FusedAdamW keeps
+    current (K.bf16_shadow); anything else is cast."""
+    if w is None:
+        return None
+    if isinstance(w, nn.Parameter) and w.dtype == torch.float32:
+        return K.bf16_shadow(w)
+    return K.cast(w.detach().contiguous(), torch.bfloat16)
 
 
 def _f(b):

@@ -7,7 +7,7 @@ torch, and launches the gfx950 kernel on torch's current stream.
 from __future__ import annotations
 
 import math
-from typing import Optional
+from typing import Any, Dict, Optional
 
 import torch
 
@@ -125,6 +125,39 @@ def cast(x: torch.Tensor, dtype) -> torch.Tensor:
     out = torch.empty(x.shape, dtype=dtype, device=x.device)
     call("lthm_cast", ptr(x), dcode(x), ptr(out), dcode(out), x.numel(), stream())
     return out
+
+
+# bf16 GEMM operands of fp32 parameters, kept current by FusedAdamW (its multi-tensor
+# step writes the rounded update into the shadow, so the forward needs no per-step
+# cast).  A shadow is used only while the parameter's autograd version is the one it
+# was written at: any torch in-place write (load_state_dict, copy_, set_weights)
+# bumps the version and forces a re-cast; the raw-pointer optimizers that do not
+# maintain shadows drop them (shadow_drop).
+_SHADOWS: Dict[int, Any] = {}
+
+
+def bf16_shadow(w: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of the fp32 parameter w, reused across steps while it is current."""
+    key = id(w)
+    ent = _SHADOWS.get(key)
+    if ent is not None and ent[0]() is w and ent[2] == w._version and ent[1].shape == w.shape:
+        return ent[1]
+    out = cast(w.detach().contiguous(), torch.bfloat16)
+    import weakref
+    _SHADOWS[key] = (weakref.ref(w), out, w._version)
+    return out
+
+
+def shadow_of(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """The registered, current bf16 shadow of w (for the optimizer to update), or None."""
+    ent = _SHADOWS.get(id(w))
+    if ent is not None and ent[0]() is w and ent[2] == w._version and ent[1].shape == w.shape:
+        return ent[1]
+    return None
+
+
+def shadow_drop(w: torch.Tensor) -> None:
+    _SHADOWS.pop(id(w), None)
 
 
 def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
@@ -407,8 +440,9 @@ def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, ze
          grad_scale, ptr(shadow), int(zero_grad), stream())
 
 
-def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0):
-    """lthm_adamw_multi: one launch per 48 fp32 tensors with identical hyper-parameters and step."""
+def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0, pbs=None):
+    """lthm_adamw_multi: one launch per 48 fp32 tensors with identical hyper-parameters and step;
+    pbs: optional per-tensor bf16 buffers (or None) that receive the updated parameters."""
     import ctypes
     n = len(ps)
     for p, g, m, v in zip(ps, gs, ms, vs):
@@ -419,9 +453,16 @@ def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0):
                "adamw_multi_ takes contiguous fp32 tensors")
     arr = lambda ts: (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in ts])  # noqa: E731
     cnt = (ctypes.c_int64 * max(n, 1))(*[p.numel() for p in ps])
+    pb = None
+    if pbs is not None and any(b is not None for b in pbs):
+        for p, b in zip(ps, pbs):
+            if b is not None and (b.dtype != torch.bfloat16 or b.numel() != p.numel() or not b.is_contiguous()
+                                  or b.device != p.device):
+                raise ValueError("adamw_multi_: a shadow must be a contiguous bf16 tensor shaped like its parameter")
+        pb = ctypes.cast((ctypes.c_void_p * n)(*[0 if b is None else b.data_ptr() for b in pbs]), ctypes.c_void_p)
     call("lthm_adamw_multi", n, ctypes.cast(arr(ps), ctypes.c_void_p), ctypes.cast(arr(gs), ctypes.c_void_p),
          ctypes.cast(arr(ms), ctypes.c_void_p), ctypes.cast(arr(vs), ctypes.c_void_p),
-         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, stream(),
+         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, pb, stream(),
          _key="lthm_adamw", _work=28.0 * sum(p.numel() for p in ps), _unit="byte")
 
 

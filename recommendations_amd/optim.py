@@ -39,12 +39,13 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = K.zeros(p.shape, torch.float32, p.device)
                 st["step"] += 1
                 grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                b = buckets.setdefault(st["step"], ([], [], [], []))
-                for lst, t in zip(b, (p.data, grad, st["exp_avg"], st["exp_avg_sq"])):
+                b = buckets.setdefault(st["step"], ([], [], [], [], []))
+                for lst, t in zip(b, (p.data, grad, st["exp_avg"], st["exp_avg_sq"], K.shadow_of(p))):
                     lst.append(t)
-            for step, (ps, gs, ms, vs) in buckets.items():
+            for step, (ps, gs, ms, vs, pbs) in buckets.items():
+                # the bf16 shadows the forward reads (K.bf16_shadow) are rewritten in the same pass
                 K.adamw_multi_(ps, gs, ms, vs, g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
-                               grad_scale=grad_scale)
+                               grad_scale=grad_scale, pbs=pbs)
         return loss
 
 
@@ -67,6 +68,7 @@ class FusedAdagrad(torch.optim.Optimizer):
                 st["step"] += 1
                 K.adagrad_(p.data, p.grad.contiguous(), st["sum"], g["lr"], g["lr_decay"], g["eps"],
                            g["weight_decay"], st["step"])
+                K.shadow_drop(p)  # written through its pointer: a bf16 shadow would be stale
         return loss
 
 
