@@ -26,6 +26,7 @@ import torch  # noqa: E402
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec, bf16 dense MFMA 2.5 PF
 HBM_PEAK_GBS = 8000.0
 BF16_PEAK_TFLOPS = 2500.0
+FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md chip table
 
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
@@ -66,32 +67,40 @@ def pmc_traffic(key, calls_per_step):
     return tot / (calls_per_step * PMC_STEPS)
 
 
-def embedding_gather_hbm(dev, P=4_000_000, D=128, K=16, n=524_288, iters=10):
-    """SURVEY §8(d) embedding roofline on a table past the 256 MiB Infinity Cache
-    (P x D bf16 = 1.02 GB): KShift gather + pool fwd, algorithmic bytes per lookup
-    8 + K*D*2 + D*2 (bf16 out) over the HIP-event time of the kernel."""
+def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=10):
+    """SURVEY §8(d) embedding roofline: KShift gather + pool forward on a table far past
+    the 256 MiB Infinity Cache (P x D bf16 = 4.1 GB), algorithmic bytes per lookup
+    8 + K*D*2 + D*2 (bf16 out) over the HIP-event time of the kernel, for two id sets:
+    ``reference_ids`` -- uniform over the full int64 range, as the reference's hashed ids
+    (feature_utils.py:46); its arithmetic-shift quirk sends every shifted row (c >= 1) of a
+    negative id to row P-1 (commons/layers.py:174-185), so ~47% of the row reads hit one
+    cached row and the algorithmic rate exceeds what HBM could deliver; and
+    ``spread_ids`` -- non-negative ids, whose K rows all land uniformly (8.4M reads of
+    16M rows: ~77% of the reads touch a row once), the HBM-bound case the roofline is for."""
     from recommendations_amd import kernels as K_
     g = torch.Generator(device=dev).manual_seed(7)
     W = torch.randn((P, D), device=dev, generator=g).to(torch.bfloat16)
-    # non-negative ids: negative int64 ids send every shifted row (c >= 1) to one hot
-    # row (the reference's arithmetic-shift quirk), which caches; these spread all K rows
-    ids = torch.randint(0, 2**62, (n,), device=dev, generator=g, dtype=torch.int64)
-    out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
     per = 8 + K * D * 2 + D * 2
-    gbs = n * per / (ms / 1000.0) / 1e9
-    del W, out
-    return {"kernel": "kshift_fwd_k", "table": f"P={P} D={D} bf16 ({P * D * 2 / 1e9:.2f} GB)", "K": K,
-            "ids": "uniform in [0, 2^62)",
-            "lookups": n, "bytes_per_lookup": per, "avg_launch_ms": round(ms, 4), "bound": "hbm",
-            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    res = {"kernel": "kshift_fwd_k", "table": f"P={P} D={D} bf16 ({P * D * 2 / 1e9:.2f} GB)", "K": K,
+           "lookups": n, "bytes_per_lookup": per, "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    for name, lo in (("spread_ids", 0), ("reference_ids", -(2 ** 63))):
+        ids = torch.randint(lo, 2 ** 63 - 1, (n,), device=dev, generator=g, dtype=torch.int64)
+        out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        gbs = n * per / (ms / 1000.0) / 1e9
+        res[name] = {"avg_launch_ms": round(ms, 4), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        del out
+    del W
+    res["achieved"], res["frac"] = res["spread_ids"]["achieved"], res["spread_ids"]["frac"]
+    res["traffic_source"] = "profiles/r02_gather_pmc.txt (tools/gather_bench.py under rocprofv3 --pmc)"
+    return res
 
 
 CONFIGS = {
@@ -134,15 +143,12 @@ def cpu_baseline(cfg, model, cfgd, B_cpu):
     bounded sample of B_cpu sequences of the same workload."""
     from oracle import lthm_ref
     from recommendations_amd.data import synthetic_lthm_batch
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores = cpu_cores()
     torch.set_num_threads(cores)
-    sd = {k: (v.detach().float().cpu().clone().requires_grad_(True) if v.is_floating_point() else v.cpu())
-          for k, v in model.state_dict().items()}
-    params = [v for v in sd.values() if v.is_floating_point() and "product_emb_module" not in k_of(sd, v)]
+    train = {n for n, p in model.named_parameters() if p.requires_grad}
+    sd = {k: (v.detach().float().cpu().clone().requires_grad_(k in train) if v.is_floating_point() else v.cpu())
+          for k, v in model.state_dict().items() if not k.startswith("_log_q_calc")}
+    params = [sd[n] for n in sorted(train)]  # dense AdamW over every trainable parameter (wrapper.py:263-275)
     opt = torch.optim.AdamW(params, lr=cfg.lr, weight_decay=cfg.weight_decay, betas=cfg.betas)
     batch = synthetic_lthm_batch(B_cpu, cfgd["T"], n_cat=cfgd["n_cat"], seed=99)
     n_mb = (B_cpu + cfg.train_mini_batch_size - 1) // cfg.train_mini_batch_size
@@ -154,14 +160,12 @@ def cpu_baseline(cfg, model, cfgd, B_cpu):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    step()  # warm-up (allocates the optimizer state, as the reference's first step would)
-    t0 = time.perf_counter()
-    n = 1
-    step()
-    dt = time.perf_counter() - t0
-    return dict(value=round(B_cpu * n / dt, 3), unit="samples/s", cores=cores, kind="port",
-                sample=f"{B_cpu} sequences of the {cfgd} workload, 1 timed step after 1 warm-up "
-                       f"(fp32 torch-CPU oracle: oracle/lthm_ref.py + torch.optim.AdamW over every parameter)")
+    dt = timed_median(step)
+    return dict(value=round(B_cpu / dt, 3), unit="samples/s", cores=cores, kind="port",
+                sample=f"{B_cpu} sequences of the C2 workload per step, median of {CPU_TIMED} timed steps after "
+                       f"{CPU_WARMUP} warm-ups (BASELINE.md plan), {dt:.2f} s/step (fp32 torch-CPU oracle: "
+                       f"oracle/lthm_ref.py fwd + bwd + torch.optim.AdamW over every trainable parameter, "
+                       f"1.1B with the 32 x 1M x 32 categorical tables, as the reference's dense optimizer)")
 
 
 def cpu_baseline_ranker(cfg, model, cfgd, B_cpu):
@@ -170,11 +174,7 @@ def cpu_baseline_ranker(cfg, model, cfgd, B_cpu):
     full tables), on a bounded sample of B_cpu rows of the C4 workload."""
     from oracle import ranker_ref
     from recommendations_amd.data import synthetic_ranker_batch
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores = cpu_cores()
     torch.set_num_threads(cores)
     sd = {k: (v.detach().float().cpu().clone().requires_grad_(True) if v.is_floating_point() else v.cpu())
           for k, v in model.state_dict().items()}
@@ -194,20 +194,51 @@ def cpu_baseline_ranker(cfg, model, cfgd, B_cpu):
             tabs[0].sub_(cfg.lr * g)
             tabs[0].grad = None
 
-    step()
-    t0 = time.perf_counter()
-    step()
-    dt = time.perf_counter() - t0
+    dt = timed_median(step)
     return dict(value=round(B_cpu / dt, 3), unit="samples/s", cores=cores, kind="port",
-                sample=f"{B_cpu} rows of the {cfgd} workload, 1 timed step after 1 warm-up "
-                       f"(fp32 torch-CPU oracle: oracle/ranker_ref.py + torch.optim.AdamW on the dense parameters)")
+                sample=f"{B_cpu} rows of the C4 workload per step, median of {CPU_TIMED} timed steps after "
+                       f"{CPU_WARMUP} warm-ups, {dt:.3f} s/step (fp32 torch-CPU oracle: oracle/ranker_ref.py + "
+                       f"torch.optim.AdamW on the dense parameters)")
 
 
-def k_of(sd, v):
-    for k, t in sd.items():
-        if t is v:
-            return k
-    return ""
+CPU_WARMUP, CPU_TIMED = 2, 5
+
+
+def launch_ranks(n: int) -> int:
+    """Run this script as n ranks on one node (torch.distributed.run, rendezvous on
+    127.0.0.1 at a free port); return the launcher's exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_cores() -> int:
+    """The host cores this job may use: OMP_NUM_THREADS when the launcher sets it (the GPU
+    box allots 16 CPUs per GPU and exports it), else the process's CPU affinity."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def timed_median(step) -> float:
+    """BASELINE.md CPU plan: 2 warm-ups, then the median of 5 timed steps (seconds)."""
+    for _ in range(CPU_WARMUP):
+        step()
+    ts = []
+    for _ in range(CPU_TIMED):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
 
 
 def main():
@@ -223,13 +254,19 @@ def main():
     ap.add_argument("--no-hbm-gather", action="store_true", help="skip the 1 GB-table embedding roofline")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: this parent never touches the GPU; it starts one rank
+        # per GPU through torch.distributed.run and exits with its status
+        sys.exit(launch_ranks(args.gpus))
+
     from recommendations_amd import _lib
     from recommendations_amd.data import synthetic_lthm_batch, synthetic_ranker_batch
     from recommendations_amd.distributed import GradBucketAllReduce, init_from_env, step_flags
 
     rank, local, world = init_from_env()
-    if world != args.gpus and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    reported = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if world != args.gpus or reported != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} and the process group has {reported} ranks")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cfgd = dict(CONFIGS[args.config])
@@ -345,9 +382,27 @@ def main():
                     e["GB/s"] = round(rate / 1e9, 1)
                     e["frac_hbm_peak"] = round(rate / 1e9 / HBM_PEAK_GBS, 4)
                 else:
+                    pk = FP8_PEAK_TFLOPS if "fp8" in k else BF16_PEAK_TFLOPS
                     e["TFLOP/s"] = round(rate / 1e12, 1)
-                    e["frac_bf16_peak"] = round(rate / 1e12 / BF16_PEAK_TFLOPS, 4)
+                    e["frac_peak"] = round(rate / 1e12 / pk, 4)
+                    e["peak_TFLOP/s"] = pk
             kern[k] = e
+        enc = {k: v for k, v in summ.items() if k.startswith("enc:")}
+        if enc:
+            # north-star MFMA target: every encoder GEMM (QKV, proj, FFN; fwd, dgrad, wgrad),
+            # flop-weighted: time the flops would take at each form's dense peak / time taken
+            at_peak = sum(v["work"] / ((FP8_PEAK_TFLOPS if "fp8" in k else BF16_PEAK_TFLOPS) * 1e12)
+                          for k, v in enc.items())
+            t = sum(v["ms"] for v in enc.values()) / 1000.0
+            fl = sum(v["work"] for v in enc.values())
+            res["encoder_gemm"] = {"bound": "mfma", "achieved": round(fl / t / 1e12, 1), "unit": "TFLOP/s",
+                                   "frac": round(at_peak / t, 4),
+                                   "peak": FP8_PEAK_TFLOPS if all("fp8" in k for k in enc) else BF16_PEAK_TFLOPS,
+                                   "flop_per_step": round(fl / PROF_STEPS / 1e12, 3),
+                                   "ms_per_step": round(1000 * t / PROF_STEPS, 3),
+                                   "forms": sorted(enc),
+                                   "note": "all TransformerBlock GEMMs (c_attn, c_proj, c_fc, mlp.c_proj; forward, "
+                                           "dgrad, wgrad), algorithmic 2MNK flop over HIP-event kernel time"}
         live = timer.summary()
         dom = max(live, key=lambda k: live[k]["ms"])
         s = live[dom]
@@ -356,7 +411,8 @@ def main():
         if s["unit"] == "byte":
             ach, peak, unit, bound = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
         else:
-            ach, peak, unit, bound = per_launch / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s", "mfma"
+            peak = FP8_PEAK_TFLOPS if "fp8" in dom else BF16_PEAK_TFLOPS
+            ach, unit, bound = per_launch / avg_s / 1e12, "TFLOP/s", "mfma"
         traffic = pmc_traffic(dom, s["calls"] / args.steps)
         res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                            "frac": round(ach / peak, 4),

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 15 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 17 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -425,6 +425,10 @@ typedef struct lthm_contrastive_desc {
   const float* gscale;    /* device scalar: upstream gradient of the loss (backward) */
   float* d_out;           /* f32 [B, T+1, n_heads, De]: every row of this head is written (no pre-zeroing) */
   float* d_in;            /* f32 [B, T, De] (accumulated over heads) */
+  const float* logq;      /* NULL, or f32 [B, logq_stride]: additive logit correction -beta * logQ(id)
+                             of every input token (wrapper.py:131-135, 204-208; zero on the positive) */
+  int64_t logq_stride;
+  float* logq_col;        /* with logq: [n_mb, n_max] scratch written by the forward, read by the backward */
 } lthm_contrastive_desc;
 
 /* Forward for one head over all mini-batches.  stats [n_mb, nstat] f32:
@@ -447,10 +451,7 @@ int lthm_adamw(float* p, float* g, float* m, float* v, int64_t n, float lr, floa
  * hyper-parameters and step; one launch per 48 tensors (torch.optim.AdamW foreach). */
 int lthm_adamw_multi(int32_t count, float** p, float** g, float** m, float** v,
                      const int64_t* n, float lr, float beta1, float beta2, float eps, float weight_decay,
-                     int64_t step, float grad_scale, void** pb, void* stream);
-/* pb: NULL, or per tensor NULL / a bf16 buffer of n[t] elements that receives the
- * updated parameter rounded to bf16 (the next forward's GEMM operand, so no
- * separate per-step weight cast) */
+                     int64_t step, float grad_scale, void* stream);
 /* torch.optim.Adagrad step (embedding_module_gen.py:97,137) */
 int lthm_adagrad(float* p, float* g, float* state_sum, int64_t n, float lr, float lr_decay, float eps,
                  float weight_decay, int64_t step, int32_t zero_grad, void* stream);
@@ -473,10 +474,39 @@ int lthm_scale_by_norm(const void* x, void* y, int32_t dtype, int64_t n, const f
 /* streaming helpers                                                         */
 /* ------------------------------------------------------------------------- */
 int lthm_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, int64_t n, void* stream);
+/* out[t][i] = bf16(in[t][i]) for count tensors of n[t] f32 elements (host arrays of
+ * device pointers): the bf16 GEMM operands of a model's fp32 weights, cast in one
+ * launch per 48 tensors at the start of each forward (no cross-step copies to go stale) */
+int lthm_cast_multi_bf16(int32_t count, float** in, void** out, const int64_t* n, void* stream);
 /* out[c] (+)= sum_r in[r*ld + c], c < cols (f32 out) */
 int lthm_colsum(const void* in, int32_t dtype, int64_t rows, int64_t cols, int64_t ld, float* out,
                 int32_t accumulate, void* stream);
 int lthm_fill_f32(float* p, float value, int64_t n, void* stream);
+/* nn.Dropout(p) (commons/transformers/layers.py:253-256, 264, 283; query_tower.py:133).
+ * Element i is kept iff (splitmix64(seed + i * 0x9E3779B97F4A7C15) >> 40) / 2^24 >= p,
+ * kept values are scaled by 1 / (1 - p); the backward calls the same entry point with
+ * the forward's seed.  0 <= p < 1.
+ * lthm_dropout:      y = [res1] + [res2] + dropout(x)   (res1 / res2: f32 or NULL)
+ * lthm_dropout_rows: x [rows, groups * cols] in place, row r of group g scaled by the
+ *                    decision for index g * rows + r (token dropout of q / k / v)
+ * lthm_dropout_mask: out[i] = keep decision (uint8), for tests and inspection */
+int lthm_dropout(const void* x, int32_t x_dtype, void* y, int32_t y_dtype, int64_t n, float p, uint64_t seed,
+                 const float* res1, const float* res2, void* stream);
+int lthm_dropout_rows(void* x, int32_t dtype, int64_t rows, int32_t cols, int32_t groups, float p, uint64_t seed,
+                      void* stream);
+int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed, void* stream);
+/* Streaming logQ for the LTHM loss (commons/layers.py:189-237 CascadedStreamingLogQ-
+ * CorrectionModule, as wrapper.py:126-130 drives it per mini-batch of mb_size sequences):
+ * for mini-batch k in order, train_step on its non-pad ids at batch index batch_idx0 + k,
+ * then out[b, t] = -beta * min_m(-log b_m[(id + hash_offsets[m]) mod num_buckets]) for
+ * all its ids.  b_tables / a_tables: f32 [n_modules, num_buckets] (the modules' b / a
+ * buffers stacked), updated in place.  ids [B, ids_stride], mask [B, mask_stride]
+ * (1 = pad; NULL = no pads), out f32 [B, T] or NULL.  update = 0 skips the train_step
+ * (the module's plain forward; beta = -1 then returns min_m -log b). */
+int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride, int64_t B,
+                     int32_t T, int32_t mb_size, float* b_tables, float* a_tables, const int64_t* hash_offsets,
+                     int32_t n_modules, int64_t num_buckets, float alpha, int64_t batch_idx0, float beta,
+                     int32_t update, float* out, void* stream);
 /* History-trim statistics of mask [B, T] (uint8, 1 = pad) for query_tower.py:73-86:
  * work[0] = first column holding a non-pad entry (T if none), work[1] = number of
  * all-pad columns; work is a device int32 buffer of T + 2 entries (work[2..] scratch). */

@@ -34,7 +34,7 @@ def _p(sd: Dict[str, torch.Tensor], name: str) -> torch.Tensor:
 
 
 def lthm_forward_loss(sd: Dict[str, torch.Tensor], cfg, batch: Dict[str, torch.Tensor], offsets: np.ndarray,
-                      return_outputs: bool = False):
+                      return_outputs: bool = False, logq: Optional[torch.Tensor] = None):
     """Returns the training loss (and intermediate outputs) of one LTHM step on CPU, fp32."""
     pt = cfg.product_tower
     lm = pt.latent_model_config
@@ -95,7 +95,7 @@ def lthm_forward_loss(sd: Dict[str, torch.Tensor], cfg, batch: Dict[str, torch.T
     xq = xq + ref.flat_fwd(outcomes, _p(sd, q + "outcome_conditioning._emb_table.weight"), False)
     y = torch.stack([F.linear(xq, _p(sd, f"{q}emb_heads.{i}.weight")) for i in range(cfg.export_tokens)], dim=2)
     loss, stats = contrastive_loss(y, target, mask, offsets, cfg.train_mini_batch_size, cfg.softmax_temperature,
-                                   list(cfg.metrics_k_all))
+                                   list(cfg.metrics_k_all), logq=logq)
     if return_outputs:
         return loss, dict(y=y, target=target, mask=mask, trim=trim, stats=stats)
     return loss
@@ -105,9 +105,16 @@ def user_context(sd, cfg, cat_ids):
     c = cfg.categorical
     W = _p(sd, "user_context.tables.weight")
     P = c.vocab_size
-    parts = [ref.kshift_fwd_torch(cat_ids[:, f], W[f * P:(f + 1) * P], c.num_shifts, False)
-             for f in range(c.n_features)]
-    e = ref.cap_gradients(torch.stack(parts, 1).reshape(cat_ids.shape[0], -1))
+    # feature f reads rows [f P, (f + 1) P) of the batched table; one gather over all
+    # features and shifts (one dense table gradient, not one per feature and shift)
+    off = (torch.arange(c.n_features, dtype=torch.int64) * P).view(1, -1, 1)
+    rows = torch.stack([ref.kshift_row_idx_torch(cat_ids, k, P) for k in range(c.num_shifts)], -1) + off
+    g = F.embedding(rows, W)  # [B, F, K, D]
+    x = g[:, :, 0]
+    for k in range(1, c.num_shifts):  # in-order sum (commons/layers.py:163-166)
+        x = x + g[:, :, k]
+    x = x / math.sqrt(c.num_shifts)
+    e = ref.cap_gradients(x.reshape(cat_ids.shape[0], -1))
     n = len(c.gate_sizes) + 1
     ws = [_p(sd, f"user_context.mlp.model.{2 * i}.weight") for i in range(n)]
     bs = [_p(sd, f"user_context.mlp.model.{2 * i}.bias") for i in range(n)]
@@ -115,8 +122,11 @@ def user_context(sd, cfg, cat_ids):
 
 
 def contrastive_loss(next_emb, cur_emb, mask, offsets: np.ndarray, mbs: int, tau: float, ks: List[int],
-                     normalize: bool = True):
-    """wrapper.py:78-245 with beta = 0 (logQ term vanishes), offsets given per mini-batch.
+                     normalize: bool = True, logq: Optional[torch.Tensor] = None):
+    """wrapper.py:78-245, offsets given per mini-batch.  ``logq``: None (beta = 0, the
+    term vanishes) or the per-token additive correction -beta * logQ [B, T] that
+    wrapper.py:131-135, 204-208 subtracts from every logit but the positive's, inside
+    the cross entropy only (the rank metrics use the plain logits).
     ``normalize=False`` takes already-normalised embeddings (kernel-level tests feed
     the same bf16-rounded unit vectors the GPU path uses)."""
     B = next_emb.shape[0]
@@ -157,7 +167,12 @@ def contrastive_loss(next_emb, cur_emb, mask, offsets: np.ndarray, mbs: int, tau
             logits = logits[~not_use]
             labels = labels[~not_use]
             num_negatives = num_negatives[~not_use]
-            lu = F.cross_entropy(logits, labels, reduction="none")
+            ce_logits = logits
+            if logq is not None:
+                corr = logq[sl][:, offset:].reshape(1, -1).repeat(bs_, 1)
+                corr[torch.arange(bs_), torch.arange(bs_)] = 0.0  # :136-141 zero on the positive
+                ce_logits = logits + corr[~not_use]
+            lu = F.cross_entropy(ce_logits, labels, reduction="none")
             lu = lu[~lu.isnan()]
             if lu.numel() == 0:
                 st.append(None)

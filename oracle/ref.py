@@ -185,17 +185,60 @@ def causal_mask(L: int) -> torch.Tensor:
     return m.float().masked_fill(~m, -float("inf"))[None, None]
 
 
-def mha(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix="attn."):
-    """commons/transformers/layers.py:247-265 (dropout p = 0)."""
+class _QB(torch.autograd.Function):
+    """bf16 rounding of a value and of its gradient: where the HIP path stores a GEMM
+    operand (forward) and the gradient it feeds back (backward) as bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+class _QG(torch.autograd.Function):
+    """Identity forward, bf16-rounded gradient: a GEMM output kept in fp32 whose
+    incoming gradient the HIP path casts to bf16 before the dgrad / wgrad GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _q(x, on):
+    return _QB.apply(x) if on else x
+
+
+def _qg(x, on):
+    return _QG.apply(x) if on else x
+
+
+def mha(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix="attn.", drop=None, bf16=False):
+    """commons/transformers/layers.py:247-265.  ``drop``: None (p = 0) or the dropout
+    scale factors {"q", "k", "v": [B, T], "resid": [B, T, C]} (0 or 1 / (1 - p)).
+    ``bf16``: round at the HIP path's bf16 points (layer input, weights, qkv, output)."""
     B, T, C = x.shape
-    qkv = F.linear(x, p[prefix + "c_attn.weight"], p.get(prefix + "c_attn.bias"))
+    qkv = _q(F.linear(_q(x, bf16), _q(p[prefix + "c_attn.weight"], bf16), p.get(prefix + "c_attn.bias")), bf16)
     q, k, v = qkv.split(C, dim=2)
+    if drop is not None:  # :253-259 token dropout (k_do, q_do, v_do over [B, 1, T, 1])
+        q = _q(q * drop["q"][..., None], bf16)
+        k = _q(k * drop["k"][..., None], bf16)
+        v = _q(v * drop["v"][..., None], bf16)
     q = q.view(B, T, H, C // H).transpose(1, 2)
     k = k.view(B, T, H, C // H).transpose(1, 2)
     v = v.view(B, T, H, C // H).transpose(1, 2)
     y = sdpa(q, k, v, mask, p.get(prefix + "attn.pos_bias.bias"))
-    y = y.transpose(1, 2).contiguous().view(B, T, C)
-    return F.linear(y, p[prefix + "c_proj.weight"], p.get(prefix + "c_proj.bias"))
+    y = _q(y.transpose(1, 2).contiguous().view(B, T, C), bf16)
+    y = _qg(F.linear(y, _q(p[prefix + "c_proj.weight"], bf16), p.get(prefix + "c_proj.bias")), bf16)
+    if drop is not None:  # :264 resid_dropout
+        y = y * drop["resid"]
+    return y
 
 
 def mqa(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix=""):
@@ -213,20 +256,27 @@ def mqa(x, p: Dict[str, torch.Tensor], H: int, mask=None, prefix=""):
     return F.linear(y, p[prefix + "out_proj.weight"], p.get(prefix + "out_proj.bias"))
 
 
-def mlp_gelu(x, p, prefix="mlp."):
-    """commons/transformers/layers.py:279-284 (GELU tanh, hidden 4d as executed)."""
-    h = F.gelu(F.linear(x, p[prefix + "c_fc.weight"], p.get(prefix + "c_fc.bias")), approximate="tanh")
-    return F.linear(h, p[prefix + "c_proj.weight"], p.get(prefix + "c_proj.bias"))
+def mlp_gelu(x, p, prefix="mlp.", drop=None, bf16=False):
+    """commons/transformers/layers.py:279-284 (GELU tanh, hidden 4d as executed);
+    ``drop``: None or {"mlp": [B, T, C] scale factors} (:283)."""
+    h = _qg(F.linear(_q(x, bf16), _q(p[prefix + "c_fc.weight"], bf16), p.get(prefix + "c_fc.bias")), bf16)
+    h = _q(F.gelu(h, approximate="tanh"), bf16)
+    y = _qg(F.linear(h, _q(p[prefix + "c_proj.weight"], bf16), p.get(prefix + "c_proj.bias")), bf16)
+    if drop is not None:
+        y = y * drop["mlp"]
+    return y
 
 
-def transformer_block(x, p: Dict[str, torch.Tensor], H: int, causal: bool, attn_mask=None):
-    """commons/transformers/layers.py:382-415 (dense path, no sparse tokens)."""
+def transformer_block(x, p: Dict[str, torch.Tensor], H: int, causal: bool, attn_mask=None, drop=None,
+                      bf16=False):
+    """commons/transformers/layers.py:382-415 (dense path, no sparse tokens); the causal
+    mask is added to ``attn_mask`` when both are given (:404-408)."""
     mask = attn_mask
     if causal:
         cm = causal_mask(x.size(-2))
         mask = cm if mask is None else mask + cm
-    x = x + mha(layer_norm(x, p["ln_1.weight"], p.get("ln_1.bias")), p, H, mask)
-    x = x + mlp_gelu(layer_norm(x, p["ln_2.weight"], p.get("ln_2.bias")), p)
+    x = x + mha(layer_norm(x, p["ln_1.weight"], p.get("ln_1.bias")), p, H, mask, drop=drop, bf16=bf16)
+    x = x + mlp_gelu(layer_norm(x, p["ln_2.weight"], p.get("ln_2.bias")), p, drop=drop, bf16=bf16)
     return x
 
 

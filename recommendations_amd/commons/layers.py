@@ -26,6 +26,7 @@ class _SparseRowsMixin:
     def _init_sparse_state(self):
         self._shadow = None
         self._shadow_version = -1
+        self._shadow_src = (0, None)  # (data_ptr, device) of the master the shadow was cast from
         self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
         self.sparse_pending = 0
         self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
@@ -44,14 +45,35 @@ class _SparseRowsMixin:
                 new[: self.sparse_rows.numel()].copy_(self.sparse_rows)
             self.sparse_rows = new
 
+    def shadow_current(self):
+        """The bf16 gather shadow if it still mirrors the fp32 master, else None.  The
+        row-wise optimizers rewrite the rows they update; torch in-place writes bump
+        the version, replaced storage (module.to(), p.data = t) changes the pointer,
+        and load_state_dict drops the shadow.  A write through ``weight.data`` in place
+        is invisible to both checks: call ``invalidate_shadow()`` after one."""
+        w = self.weight
+        if self._shadow is None or self._shadow_version != w._version or \
+                self._shadow_src != (w.data_ptr(), w.device):
+            return None
+        return self._shadow
+
+    def invalidate_shadow(self):
+        self._shadow = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self.invalidate_shadow()
+
     def gather_weight(self):
         if self._gather_dtype == torch.float32:
             return self.weight
-        if self._shadow is None or self._shadow_version != self.weight._version or \
-                self._shadow.device != self.weight.device:
-            self._shadow = K.cast(self.weight.detach(), self._gather_dtype)
-            self._shadow_version = self.weight._version
-        return self._shadow
+        sh = self.shadow_current()
+        if sh is None:
+            w = self.weight
+            sh = self._shadow = K.cast(w.detach(), self._gather_dtype)
+            self._shadow_version = w._version
+            self._shadow_src = (w.data_ptr(), w.device)
+        return sh
 
 
 class KShiftEmbedding(_SparseRowsMixin, nn.Module):
@@ -340,7 +362,8 @@ class QREmbedding(nn.Module):
 
 
 class StreamingLogQCorrectionModule(nn.Module):
-    """commons/layers.py:189-213 (train_step fixed: `self.a[hash] = batch_idx`, SURVEY.md §3.5 #7)."""
+    """commons/layers.py:189-213 (train_step fixed: `self.a[hash] = batch_idx`).
+    On the GPU the lookups and updates run in lthm_logq_stream (through the cascade)."""
 
     def __init__(self, num_buckets, hash_offset, alpha: float = 0.05, p_init: float = 0.01):
         super().__init__()
@@ -352,28 +375,70 @@ class StreamingLogQCorrectionModule(nn.Module):
         return (products + self.hash_offset) % self.num_buckets
 
     def forward(self, products: torch.Tensor) -> torch.Tensor:
-        return -self.b[self.hash_fn(products)].log().reshape(*products.shape)
+        return _logq_call([self], products.reshape(1, -1), None, 1, 0, -1.0, False).view(products.shape)
 
     def train_step(self, products: torch.Tensor, batch_idx: int):
-        h = self.hash_fn(products)
-        self.b[h] = ((1 - self.alpha) * self.b[h]) + (self.alpha * (batch_idx - self.a[h])).float()
-        self.a[h] = float(batch_idx)
+        _logq_call([self], products.reshape(1, -1), None, 1, batch_idx, 0.0, True, want_out=False)
+
+
+def _logq_tables(mods):
+    """[n, N] b and a tables whose rows the modules' buffers are views of (re-stacked,
+    and the buffers re-pointed, whenever a buffer no longer lives there: after .to(),
+    load_state_dict into a fresh tensor, ...)."""
+    owner = mods[0]
+    st = getattr(owner, "_logq_stack", None)
+    nb = mods[0].num_buckets
+    ok = st is not None and len(st[2]) == len(mods)
+    if ok:
+        bt, at, ids = st
+        ok = all(id(m) == i and m.b.data_ptr() == bt[j].data_ptr() and m.a.data_ptr() == at[j].data_ptr()
+                 for j, (m, i) in enumerate(zip(mods, ids)))
+    if not ok:
+        bt = torch.stack([m.b.detach().float() for m in mods]).contiguous()
+        at = torch.stack([m.a.detach().float() for m in mods]).contiguous()
+        for j, m in enumerate(mods):
+            m.b = bt[j]
+            m.a = at[j]
+        owner._logq_stack = (bt, at, [id(m) for m in mods])
+    return owner._logq_stack[0], owner._logq_stack[1], nb
+
+
+def _logq_call(mods, ids, mask, mb_size, batch_idx0, beta, update, want_out=True):
+    from .._lib import call, ptr, require_gpu, stream
+    ids_c = ids.contiguous()
+    require_gpu(ids_c, mask)
+    shp = ids_c.shape
+    ids2 = ids_c.view(-1, shp[-1]) if ids_c.dim() >= 1 and ids_c.numel() else ids_c.view(1, -1)
+    if ids2.numel() == 0:
+        return torch.empty(shp, dtype=torch.float32, device=ids.device)
+    bt, at, nb = _logq_tables(mods)
+    offs = torch.tensor([int(m.hash_offset) for m in mods], dtype=torch.int64).to(ids.device, non_blocking=True)
+    B, T = ids2.shape
+    out = torch.empty((B, T), dtype=torch.float32, device=ids.device) if want_out else None
+    call("lthm_logq_stream", ptr(ids2), ids2.stride(0), ptr(mask), 0 if mask is None else mask.stride(0), B, T,
+         mb_size, ptr(bt), ptr(at), ptr(offs), len(mods), nb, float(mods[0].alpha), int(batch_idx0), float(beta),
+         int(update), ptr(out), stream())
+    return out.view(shp) if want_out else None
 
 
 class CascadedStreamingLogQCorrectionModule(nn.Module):
-    """commons/layers.py:217-237 (train_step loop fixed, SURVEY.md §3.5 #8)."""
+    """commons/layers.py:217-237 (train_step loop fixed): the min over the
+    offset modules of -log b, every module's lookup and update in one HIP launch."""
 
     def __init__(self, num_buckets, hash_offsets, alpha: float = 0.05, p_init: float = 0.01):
         super().__init__()
         self.models = nn.ModuleList([StreamingLogQCorrectionModule(num_buckets, o, alpha, p_init) for o in hash_offsets])
 
     def forward(self, products):
-        result = None
-        for mod in self.models:
-            v = mod(products)
-            result = v if result is None else torch.minimum(result, v)
-        return result
+        return _logq_call(list(self.models), products.reshape(1, -1), None, 1, 0, -1.0, False).view(products.shape)
 
     def train_step(self, products, batch_idx):
-        for mod in self.models:
-            mod.train_step(products, batch_idx)
+        _logq_call(list(self.models), products.reshape(1, -1), None, 1, batch_idx, 0.0, True, want_out=False)
+
+    def stream_correction(self, ids: torch.Tensor, mask: torch.Tensor, mb_size: int, batch_idx0: int,
+                          beta: float) -> torch.Tensor:
+        """The LTHM loss's use (wrapper.py:126-130, 204-208) over all mini-batches of mb_size
+        sequences in order: train_step on each mini-batch's non-pad ids at batch index
+        batch_idx0 + k, then -beta * logQ of its ids.  ids int64 [B, T], mask [B, T] (1 = pad)."""
+        m = (mask if mask.dtype == torch.uint8 else mask.to(torch.uint8)).contiguous()
+        return _logq_call(list(self.models), ids.contiguous(), m, mb_size, batch_idx0, beta, True)

@@ -25,17 +25,22 @@ from ..._lib import require_gpu
 
 
 def _bf(w):
-    """bf16 GEMM operand of a weight: fp32 parameters reuse the shadow FusedAdamW keeps
-    current (K.bf16_shadow); anything else is cast."""
+    """bf16 GEMM operand of a weight: the copy cast at the start of this forward by the
+    enclosing K.bf16_operands scope, else a fresh cast."""
     if w is None:
         return None
-    if isinstance(w, nn.Parameter) and w.dtype == torch.float32:
-        return K.bf16_shadow(w)
-    return K.cast(w.detach().contiguous(), torch.bfloat16)
+    return K.bf16_operand(w)
 
 
 def _f(b):
     return None if b is None else b.detach().contiguous()
+
+
+def dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
+    """nn.Dropout(p)(x): identity in eval mode or at p = 0, else the HIP hash-mask kernel."""
+    if not training or p == 0.0:
+        return x
+    return K.DropoutFn.apply(x, float(p), K.new_dropout_seed())
 
 
 # bf16 copy of the input gradient a block's backward produces (its final LayerNorm
@@ -60,11 +65,27 @@ def _grad_bf16(g32: torch.Tensor) -> torch.Tensor:
 
 
 class TransformerBlockFn(torch.autograd.Function):
-    """x -> x + attn(ln_1 x) -> + mlp(ln_2 .)  [+ x again when double_residual]."""
+    """x -> x + attn(ln_1 x) -> + mlp(ln_2 .)  [+ x again when double_residual].
+
+    ``drop`` = None (eval, or every dropout p = 0), or (p_attn, p_resid, seed) for
+    training with the reference's dropouts (commons/transformers/layers.py:253-256
+    token dropout of q / k / v, :264 residual dropout after c_proj, :283 MLP dropout,
+    both at ``config.dropout``).  With dropout the two output GEMMs drop their fused
+    residual epilogue and lthm_dropout adds the residual instead."""
 
     @staticmethod
-    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal, double_residual,
-                fp8=False):
+    def forward(ctx, *args):
+        with K.gemm_tag("enc"):
+            return TransformerBlockFn._forward(ctx, *args)
+
+    @staticmethod
+    def backward(ctx, dout):
+        with K.gemm_tag("enc"):
+            return TransformerBlockFn._backward(ctx, dout)
+
+    @staticmethod
+    def _forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal,
+                 double_residual, fp8=False, drop=None):
         require_gpu(x)
         B, T, d = x.shape
         E = d // H
@@ -81,45 +102,66 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             def lin(xb, wb, b, **kw):
                 return K.linear_fwd(xb, wb, b, **kw)
+        pa, pr, seed = drop if drop is not None else (0.0, 0.0, 0)
         h1, mu1, rs1 = K.layernorm_fwd(x2, ln1w.detach(), _f(ln1b))
         qkv = lin(h1, wqkv_b, _f(bqkv))
+        if pa > 0.0:
+            K.dropout_rows_(qkv, 3, pa, seed)  # the attention sees (and the backward saves) the scaled q / k / v
         tab = None if table is None else table.detach().contiguous()
         o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
-        x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
+        if pr > 0.0:
+            x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32), pr, seed + 1, res1=x2)
+        else:
+            x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
         g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre)
-        out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
+        if pr > 0.0:
+            out = K.dropout(lin(g, w2_b, _f(b2), out_dtype=torch.float32), pr, seed + 2, res1=x1,
+                            res2=x2 if double_residual else None)
+        else:
+            out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
         ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
-                   b1 is not None, b2 is not None, None if table is None else table.shape)
+                   b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
         return out.view(B, T, d)
 
     @staticmethod
-    def backward(ctx, dout):
+    def _backward(ctx, dout):
         (x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g, wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w,
          tab) = ctx.saved_tensors
-        B, T, d, H, E, causal, dbl, has_ln1b, has_bqkv, has_bp, has_b1, has_b2, tshape = ctx.cfg
+        B, T, d, H, E, causal, dbl, has_ln1b, has_bqkv, has_bp, has_b1, has_b2, tshape, pa, pr, seed = ctx.cfg
         M = B * T
         dy = dout.contiguous().view(M, d)
         if dy.dtype != torch.float32:
             dy = dy.float()
-        dyb = _grad_bf16(dy)
-        # MLP half
+        # MLP half (dym: the gradient behind the MLP dropout)
+        if pr > 0.0:
+            dym = K.dropout(dy, pr, seed + 2)
+            dyb = K.cast(dym, torch.bfloat16)
+        else:
+            dym, dyb = dy, _grad_bf16(dy)
         dw2 = K.linear_wgrad(dyb, g)
-        db2 = K.colsum(dy) if has_b2 else None
+        db2 = K.colsum(dym) if has_b2 else None
         dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_MUL_AUX, aux=pre)
         dw1 = K.linear_wgrad(dpre, h2)
         db1 = K.colsum(dpre) if has_b1 else None
         dh2 = K.linear_dgrad(dpre, w1_b)
         dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy)
-        # attention half
+        # attention half (dx1r: the gradient behind the residual dropout)
+        if pr > 0.0:
+            dx1r = K.dropout(dx1, pr, seed + 1)
+            dx1b = K.cast(dx1r, torch.bfloat16)
+        else:
+            dx1r = dx1
         dwp = K.linear_wgrad(dx1b, o)
-        dbp = K.colsum(dx1) if has_bp else None
+        dbp = K.colsum(dx1r) if has_bp else None
         do = K.linear_dgrad(dx1b, wp_b)
         dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+        if pa > 0.0:
+            K.dropout_rows_(dqkv, 3, pa, seed)
         dwqkv = K.linear_wgrad(dqkv, h1)
         dbqkv = K.colsum(dqkv) if has_bqkv else None
         dh1 = K.linear_dgrad(dqkv, wqkv_b)
@@ -131,7 +173,7 @@ class TransformerBlockFn(torch.autograd.Function):
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
         return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
-                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None)
+                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None)
 
 
 # ------------------------------------------------------------------ modules
@@ -218,6 +260,13 @@ class SelfAttention(nn.Module):
         return MultiHeadAttention(config)
 
 
+def _drop_args(mod: nn.Module, p_attn: float, p_resid: float):
+    """(p_attn, p_resid, seed) for a fused op in training mode with some p > 0, else None."""
+    if not mod.training or (p_attn == 0.0 and p_resid == 0.0):
+        return None
+    return (float(p_attn), float(p_resid), K.new_dropout_seed())
+
+
 def _mask_is_causal(mask: Optional[torch.Tensor], T: int) -> bool:
     """True for the reference's causal additive mask (commons/transformers/layers.py:
     397-402: -inf above the diagonal and the constant 1.0 elsewhere, a softmax-invariant
@@ -240,8 +289,9 @@ class _SelfAttnFn(torch.autograd.Function):
     expanded per head and sums their gradients over the heads."""
 
     @staticmethod
-    def forward(ctx, x, w_in, b_in, w_kv, b_kv, w_out, b_out, table, H, causal, shared_kv):
+    def forward(ctx, x, w_in, b_in, w_kv, b_kv, w_out, b_out, table, H, causal, shared_kv, drop=None):
         require_gpu(x)
+        pa, pr, seed = drop if drop is not None else (0.0, 0.0, 0)
         B, T, C = x.shape
         E = C // H
         M = B * T
@@ -252,25 +302,36 @@ class _SelfAttnFn(torch.autograd.Function):
             w_kv_b = _bf(w_kv)
             q = K.linear_fwd(xb, w_in_b, _f(b_in))
             kv = K.linear_fwd(xb, w_kv_b, _f(b_kv))
+            if pa > 0.0:  # q (one group over the heads), then k and v of the shared head
+                K.dropout_rows_(q, 1, pa, seed)
+                K.dropout_rows_(kv, 2, pa, seed + 3)
             o, lse = K.attn_fwd_mqa(q, kv, B, T, H, E, tab, causal)
             saved = (xb, q, kv, o, lse, w_in_b, w_kv_b, w_out_b)
         else:
             qkv = K.linear_fwd(xb, w_in_b, _f(b_in))
+            if pa > 0.0:
+                K.dropout_rows_(qkv, 3, pa, seed)
             o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
             saved = (xb, qkv, o, lse, w_in_b, w_out_b)
         y = K.linear_fwd(o, w_out_b, _f(b_out), out_dtype=torch.float32)
+        if pr > 0.0:
+            y = K.dropout(y, pr, seed + 1)
         ctx.save_for_backward(*saved, tab)
         ctx.cfg = (B, T, C, H, E, causal, shared_kv, b_in is not None, b_kv is not None, b_out is not None,
                    None if table is None else table.shape)
+        ctx.drop = (pa, pr, seed)
         return y.view(B, T, C)
 
     @staticmethod
     def backward(ctx, dy):
         B, T, C, H, E, causal, shared_kv, has_bin, has_bkv, has_bout, tshape = ctx.cfg
+        pa, pr, seed = ctx.drop
         M = B * T
         saved = ctx.saved_tensors
         tab = saved[-1]
         dy = dy.contiguous().view(M, C).float()
+        if pr > 0.0:
+            dy = K.dropout(dy, pr, seed + 1)
         dyb = K.cast(dy, torch.bfloat16)
         if shared_kv:
             xb, q, kv, o, lse, w_in_b, w_kv_b, w_out_b = saved[:-1]
@@ -286,6 +347,9 @@ class _SelfAttnFn(torch.autograd.Function):
             dq = dqkv[:, :C].contiguous()
             dkv = torch.cat([dqkv[:, C:2 * C].float().view(M, H, E).sum(1),
                              dqkv[:, 2 * C:].float().view(M, H, E).sum(1)], dim=1).contiguous()
+            if pa > 0.0:
+                K.dropout_rows_(dq, 1, pa, seed)
+                K.dropout_rows_(dkv, 2, pa, seed + 3)
             dkvb = K.cast(dkv, torch.bfloat16)
             dw_in = K.linear_wgrad(dq, xb)
             db_in = K.colsum(dq) if has_bin else None
@@ -295,6 +359,8 @@ class _SelfAttnFn(torch.autograd.Function):
             dx = K.linear_dgrad(dkvb, w_kv_b, out_dtype=torch.float32, res1=dx)
         else:
             dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+            if pa > 0.0:
+                K.dropout_rows_(dqkv, 3, pa, seed)
             dw_in = K.linear_wgrad(dqkv, xb)
             db_in = K.colsum(dqkv) if has_bin else None
             dx = K.linear_dgrad(dqkv, w_in_b, out_dtype=torch.float32)
@@ -302,7 +368,7 @@ class _SelfAttnFn(torch.autograd.Function):
         if tshape is not None:
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
-        return dx.view(B, T, C), dw_in, db_in, dw_kv, db_kv, dw_out, db_out, dtable, None, None, None
+        return dx.view(B, T, C), dw_in, db_in, dw_kv, db_kv, dw_out, db_out, dtable, None, None, None, None
 
 
 class MultiHeadAttention(SelfAttention):
@@ -323,7 +389,8 @@ class MultiHeadAttention(SelfAttention):
             self.attn.pos_bias.check(T, T)
         causal = _mask_is_causal(mask, T)
         return _SelfAttnFn.apply(x.float(), self.c_attn.weight, self.c_attn.bias, None, None, self.c_proj.weight,
-                                 self.c_proj.bias, self.attn.table, self.n_head, causal, False)
+                                 self.c_proj.bias, self.attn.table, self.n_head, causal, False,
+                                 _drop_args(self, self.attn_dropout.p, self.resid_dropout.p))
 
 
 class MultiQueryAttention(SelfAttention):
@@ -346,7 +413,7 @@ class MultiQueryAttention(SelfAttention):
         causal = _mask_is_causal(mask, T)
         return _SelfAttnFn.apply(x.float(), self.q_proj.weight, self.q_proj.bias, self.kv_proj.weight,
                                  self.kv_proj.bias, self.out_proj.weight, self.out_proj.bias, self.attn.table,
-                                 self.n_head, causal, True)
+                                 self.n_head, causal, True, _drop_args(self, self.attn_dropout.p, self.resid_dropout.p))
 
 
 class _MLP(nn.Module):
@@ -358,6 +425,11 @@ class _MLP(nn.Module):
         self.gelu = nn.GELU(approximate="tanh")
         self.c_proj = nn.Linear(int(hidden_mult * n_embd), n_embd, bias=bias)
         self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """:279-284 standalone (the block fuses this into TransformerBlockFn)."""
+        y = K.mlp_chain(x, [self.c_fc, self.c_proj], [K.ACT_GELU, K.ACT_NONE], out_f32=True)
+        return dropout(y, self.dropout.p, self.training)
 
 
 class TransformerBlock(nn.Module):
@@ -409,6 +481,13 @@ class TransformerBlock(nn.Module):
                 a.attn.table, self.ln_2.weight, self.ln_2.bias, m.c_fc.weight, m.c_fc.bias, m.c_proj.weight,
                 m.c_proj.bias)
 
+    def gemm_weights(self):
+        """The weights the fused block reads as bf16 GEMM operands."""
+        if self.is_moe:
+            return []
+        a, m = self.attn, self.mlp
+        return [a.c_attn.weight, a.c_proj.weight, m.c_fc.weight, m.c_proj.weight]
+
     def _fused(self, x, double_residual: bool):
         if x.dim() != 3:
             raise ValueError("TransformerBlock expects [B, T, d]")
@@ -423,8 +502,12 @@ class TransformerBlock(nn.Module):
             return y + x if double_residual else y
         if self.attn.attn.table is not None:
             self.attn.attn.pos_bias.check(x.shape[1], x.shape[1])
-        return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal, double_residual,
-                                        self.fp8_gemm)
+        drop = _drop_args(self, self.attn.attn_dropout.p, self.attn.resid_dropout.p)
+        if drop is not None and self.mlp.dropout.p != drop[1]:
+            raise NotImplementedError("the fused block applies one dropout p to the attention output and the MLP")
+        with K.bf16_operands(self.gemm_weights()):
+            return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal,
+                                            double_residual, self.fp8_gemm, drop)
 
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if attn_mask is not None:
@@ -731,4 +814,4 @@ class _MoEMLP(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h = self.c_fc(x)
         h = K.ActivationFn.apply(h.contiguous(), K.ACT_GELU)
-        return self.c_proj(h)
+        return dropout(self.c_proj(h), self.dropout.p, self.training)  # :316

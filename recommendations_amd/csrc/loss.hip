@@ -224,6 +224,14 @@ struct ClArgs {
   float* d_in;                                     // f32 [B, T, DE] (accumulated)
   float* colb;  // forward only: per-column exp2 bias (-1/tau log2 e, -inf for pad / beyond n),
                 // kept in the row-weight buffer until cl_stats_k overwrites it
+  // logQ correction (wrapper.py:131-135, 204-208): lq [B, lq_stride] is the additive
+  // logit correction -beta * logQ(id) of every input token (natural log units), or
+  // null; lqcol [n_mb, n_max] its per-column copy (0 for pad / beyond n), written by
+  // cl_diag_k and read by both passes.  With lq the kernels take the online-max
+  // (non-FIXED) path, whose per-element masking applies it to every c != r.
+  const float* lq;
+  int64_t lq_stride;
+  float* lqcol;
 };
 
 struct Geo {
@@ -287,6 +295,14 @@ __global__ __launch_bounds__(256) void cl_diag_k(ClArgs a) {
     if (lane == 0) {
       a.diag[(int64_t)mb * a.n_max + r] = s;
       if (a.colb) a.colb[(int64_t)mb * a.n_max + r] = s == -INFINITY ? -INFINITY : -(1.f / a.tau) * 1.4426950408889634f;
+      if (a.lq) {
+        float q = 0.f;
+        if (s != -INFINITY) {
+          const int b = r / g.L, t = r - (r / g.L) * g.L;
+          q = a.lq[(g.b0 + b) * a.lq_stride + t + g.off];
+        }
+        a.lqcol[(int64_t)mb * a.n_max + r] = q;
+      }
     }
   }
 }
@@ -631,19 +647,21 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
     const int buf = t % CL_NBUF;
     cur_in.stage(sh.img[buf], g.n, w, lane);
     glds4(t * 64 + lane < a.n_max ? a.colb + base + t * 64 + lane : &cl_ninf, sh.m0[buf][w]);
+    if (!FIXED) glds4(a.lq && t * 64 + lane < a.n_max ? a.lqcol + base + t * 64 + lane : &cl_zero_f, sh.m1[buf][w]);
   };
   retire_loads();
   stage(0);
   if (ntile > 1) stage(1);
   for (int tI = 0; tI < ntile; ++tI) {
     const int cur = tI % CL_NBUF, c0 = tI * 64;
-    if (tI + 1 < ntile) wait_vm<5>();
+    if (tI + 1 < ntile) wait_vm<FIXED ? 5 : 6>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (tI + 2 < ntile) stage(tI + 2);
     f32x4 acc[2][4];
     st_tile(acc, qf, sh.img[cur], lane);
     const float* cdg = sh.m0[cur][w];  // column exp2 bias: cs, or -inf for a pad column / beyond n
+    const float* clq = sh.m1[cur][w];  // !FIXED: logQ correction of the columns (0 without logQ)
     const bool special = !FIXED || (c0 < spec_hi && c0 + 64 > spec_lo);
     if (!special) {
       float cb[4][4];
@@ -687,7 +705,8 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int c = c0 + yb * 16 + rg + j;
-              if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) bm = fmaxf(bm, acc[mi][yb][j] * it);
+              const float vq = acc[mi][yb][j] * it + (c == r ? 0.f : clq[yb * 16 + rg + j]);
+              if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) bm = fmaxf(bm, vq);
             }
           bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
           bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
@@ -705,7 +724,8 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
             const float v = acc[mi][yb][j] * it;
             if (c == r) pv[mi] = v;
             if (cok[yb][j] && (csq[yb][j] != rsq[mi] || c == r)) {
-              l[mi] += __expf(v - m[mi]);
+              // the CE sees the logQ-corrected logit, the rank the plain one (wrapper.py:204-233)
+              l[mi] += __expf((FIXED || c == r ? v : v + clq[yb * 16 + rg + j]) - m[mi]);
               cn[mi] += 1;
               rk[mi] += (c != r && v > dg[mi]) ? 1 : 0;
             }
@@ -774,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     else reg_frags(qf[mi], lane, g.n, x0 + 32 * w + 16 * mi, [&](int c) { return in_row(a, g, c); });
   }
   // this lane's register row per mi (x = x0 + 32 w + 16 mi + col)
-  float xsh[2], xw[2], xcap[2];
+  float xsh[2], xw[2], xcap[2], xq[2];
   bool xpad[2];
   int xsq[2], xx[2];
 #pragma unroll
@@ -787,6 +807,8 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     xcap[mi] = xw[mi] != 0.f ? __log2f(xw[mi]) : -INFINITY;
     xpad[mi] = in ? (ROWS ? false : pad_of(a, g, x)) : true;
     xsq[mi] = in ? x / g.L : -2;
+    // COLS: the logQ correction of this register row's column (log2 units)
+    xq[mi] = (!FIXED && !ROWS && a.lq && in) ? a.lqcol[base + x] * LOG2E : 0.f;
   }
   f32x4 dacc[2][8];
 #pragma unroll
@@ -808,6 +830,8 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
       const bool inr = y0 + lane < a.n_max;  // past n_max: shift -inf, weight 0
       glds4(inr ? shift + base + y0 + lane : &cl_ninf, sh.m0[buf][w]);
       glds4(inr ? a.w + base + y0 + lane : &cl_zero_f, sh.m1[buf][w]);
+    } else if (!FIXED) {  // ROWS: the logQ correction of the image rows (columns)
+      glds4(a.lq && y0 + lane < a.n_max ? a.lqcol + base + y0 + lane : &cl_zero_f, sh.m0[buf][w]);
     }
   };
   retire_loads();
@@ -816,7 +840,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   for (int tI = 0; tI < ntile; ++tI) {
     const int cur = tI % CL_NBUF, y0 = tI * 64;
     if (tI + 1 < ntile) {
-      if (ROWS) wait_vm<4>();
+      if (ROWS) wait_vm<FIXED ? 4 : 5>();
       else wait_vm<6>();
     } else {
       wait_vm<0>();
@@ -856,6 +880,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
           const int yl = yb * 16 + rg + j, y = y0 + yl;
           const int ysq = y < g.n ? y / g.L : -1;
           const float ysh = ROWS ? 0.f : sh.m0[cur][w][yl], yw = ROWS ? 0.f : sh.m1[cur][w][yl];
+          const float yq = (ROWS && !FIXED) ? sh.m0[cur][w][yl] * LOG2E : 0.f;
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi) {
             const int x = xx[mi];
@@ -863,13 +888,14 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
             const bool keep = (ysq != xsq[mi] || x == y);
             if (ROWS) {
               if (keep && xw[mi] != 0.f) {
-                float t = __builtin_fmaf(acc[mi][yb][j], c1, xsh[mi]);
+                float t = __builtin_fmaf(acc[mi][yb][j], c1, xsh[mi] + (x == y ? 0.f : yq));
                 if (!FIXED) t = fminf(t, xcap[mi]);
                 ds = __builtin_amdgcn_exp2f(t) - (x == y ? xw[mi] : 0.f);
               }
             } else {
               if (!xpad[mi] && keep && yw != 0.f)
-                ds = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, ysh)) - (x == y ? yw : 0.f);
+                ds = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[mi][yb][j], c1, ysh + (x == y ? 0.f : xq[mi]))) -
+                     (x == y ? yw : 0.f);
             }
             acc[mi][yb][j] = ds;
           }
@@ -933,6 +959,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.gscale = d->gscale;
   a.d_out = d->d_out; a.d_in = d->d_in;
   a.colb = nullptr;
+  a.lq = d->logq; a.lq_stride = d->logq_stride; a.lqcol = d->logq_col;
   return a;
 }
 
@@ -941,6 +968,7 @@ static int cl_check(const lthm_contrastive_desc* d) {
   if ((int64_t)d->mb_size * d->T > d->n_max || d->n_max > 4096) return 1;
   if ((int64_t)d->mb_size * (d->T + 1) * d->n_heads * DE >= (1ll << 31)) return 1;  // RowCursor offsets
   if (d->head < 0 || d->head >= d->n_heads) return 1;
+  if (d->logq && (!d->logq_col || d->logq_stride < d->T)) return 1;
   return 0;
 }
 
@@ -1011,7 +1039,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
-  if (2.f / d->tau <= 80.f) hipLaunchKernelGGL((cl_fwd_k<true>), grid, dim3(256), 0, s, a);
+  // the fixed softmax shift 1/tau bounds the plain logits only: logQ takes the online max
+  if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((cl_fwd_k<false>), grid, dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb), dim3(256), 0, s, a, stats, nstat, (const int*)ks, nk, loss_scale,
@@ -1027,7 +1056,7 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
   hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb), dim3(256), 0, s, a, d->diag);
   LTHM_CHECK_LAUNCH();
   dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
-  if (2.f / d->tau <= 80.f) {
+  if (2.f / d->tau <= 80.f && !d->logq) {
     hipLaunchKernelGGL((cl_bwd_k<true, true>), grid, dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     hipLaunchKernelGGL((cl_bwd_k<false, true>), grid, dim3(256), 0, s, a);

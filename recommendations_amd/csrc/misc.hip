@@ -16,6 +16,146 @@ __global__ __launch_bounds__(256) void cast_k(const TI* __restrict__ in, TO* __r
     Elem<TO>::st(out + i, Elem<TI>::ld(in + i));
 }
 
+// ---------------------------------------------------------------- dropout
+// nn.Dropout(p) (commons/transformers/layers.py:253-256, 264, 283; query_tower.py:133):
+// keep element i with probability 1 - p, scale kept values by 1 / (1 - p).  The keep
+// decision is a counter-based hash of (seed, i), so the backward regenerates the
+// forward's mask from the seed alone (no mask tensor is stored).
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int64_t i, uint32_t thresh24) {
+  uint64_t z = seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 40) >= thresh24;  // u = (z >> 40) / 2^24 >= p
+}
+
+// y = [res1] + [res2] + x * keep / (1 - p)
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void dropout_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t n,
+                                                 uint32_t thresh24, float scale, uint64_t seed,
+                                                 const float* __restrict__ res1, const float* __restrict__ res2) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = dropout_keep(seed, i, thresh24) ? Elem<TI>::ld(x + i) * scale : 0.f;
+    if (res1) v += res1[i];
+    if (res2) v += res2[i];
+    Elem<TO>::st(y + i, v);
+  }
+}
+
+// x [rows, groups * cols] in place: element (r, g, c) *= keep(g * rows + r) / (1 - p)
+// (the reference's token dropout: attn_dropout(ones[B, 1, T, 1]) for q, k and v)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_rows_k(T* __restrict__ x, int64_t rows, int cols, int groups,
+                                                      uint32_t thresh24, float scale, uint64_t seed) {
+  const int64_t n = rows * groups * (int64_t)cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ((int64_t)groups * cols);
+    const int g = (int)((i / cols) % groups);
+    const float f = dropout_keep(seed, (int64_t)g * rows + r, thresh24) ? scale : 0.f;
+    Elem<T>::st(x + i, Elem<T>::ld(x + i) * f);
+  }
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_k(uint8_t* __restrict__ out, int64_t n, uint32_t thresh24,
+                                                      uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = dropout_keep(seed, i, thresh24) ? 1 : 0;
+}
+
+static inline uint32_t dropout_thresh(float p) {
+  const double t = (double)p * 16777216.0;
+  return t >= 16777216.0 ? 16777216u : (uint32_t)t;
+}
+
+// ---------------------------------------------------------------- streaming logQ
+// CascadedStreamingLogQCorrectionModule (commons/layers.py:189-237, train_step as fixed
+// in SURVEY §3.5 #7-8) driven the way the LTHM loss drives it (wrapper.py:126-130): for
+// each mini-batch in order, first the train_step on its non-pad ids at batch index
+// batch_idx0 + mb (b[h] <- (1 - alpha) b[h] + alpha (idx - a[h]); a[h] <- idx, every
+// duplicate computing from the pre-update state, as the reference's index_put does),
+// then the correction of all its ids: out = -beta * min_m (-log b_m[(id + off_m) mod N]).
+// One workgroup walks the mini-batches in order (the updates chain through b and a).
+__device__ __forceinline__ int64_t logq_bucket(int64_t id, int64_t off, int64_t nb) {
+  const int64_t h = (int64_t)((uint64_t)id + (uint64_t)off) % nb;  // int64 wrap, then torch remainder
+  return h < 0 ? h + nb : h;
+}
+
+__global__ __launch_bounds__(1024) void logq_stream_k(const int64_t* __restrict__ ids, const uint8_t* __restrict__ mask,
+                                                      int64_t B, int T, int64_t ids_stride, int64_t mask_stride, int mbs,
+                                                      float* __restrict__ btab, float* __restrict__ atab,
+                                                      const int64_t* __restrict__ offs, int n_mod, int64_t nb,
+                                                      float alpha, int64_t batch_idx0, float beta, int update,
+                                                      float* __restrict__ out) {
+  const int n_mb = (int)((B + mbs - 1) / mbs);
+  for (int mb = 0; mb < n_mb; ++mb) {
+    const int64_t b0 = (int64_t)mb * mbs;
+    const int64_t cnt = min((int64_t)mbs, B - b0) * T;
+    const float idx = (float)(batch_idx0 + mb);
+    for (int m = 0; m < (update ? n_mod : 0); ++m) {
+      float* bt = btab + (int64_t)m * nb;
+      float* at = atab + (int64_t)m * nb;
+      for (int64_t i0 = 0; i0 < cnt; i0 += 1024) {
+        const int64_t i = i0 + threadIdx.x;
+        int64_t h = -1;
+        float nbv = 0.f;
+        if (i < cnt) {
+          const int64_t bb = b0 + i / T, t = i % T;
+          if (!mask || !mask[bb * mask_stride + t]) {
+            h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
+            nbv = (1.f - alpha) * bt[h] + alpha * (idx - at[h]);
+          }
+        }
+        __syncthreads();  // every read of this chunk before any write
+        if (h >= 0) {
+          bt[h] = nbv;
+          at[h] = idx;
+        }
+        __syncthreads();
+      }
+    }
+    for (int64_t i = threadIdx.x; out && i < cnt; i += 1024) {
+      const int64_t bb = b0 + i / T, t = i % T;
+      const int64_t id = ids[bb * ids_stride + t];
+      float q = INFINITY;
+      for (int m = 0; m < n_mod; ++m) q = fminf(q, -__logf(btab[(int64_t)m * nb + logq_bucket(id, offs[m], nb)]));
+      out[bb * T + t] = -beta * q;
+    }
+    __syncthreads();
+  }
+}
+
+// Multi-tensor f32 -> bf16 cast (lthm_cast_multi_bf16): a block per 1024-element
+// chunk of the concatenation; the tensor is found by a search of the chunk-prefix
+// table, so every lane of a chunk works on one tensor.
+constexpr int CM_MT = 48;
+struct CastList {
+  const float* in[CM_MT];
+  bf16_t* out[CM_MT];
+  int64_t n[CM_MT];
+  int64_t chunk_off[CM_MT + 1];  // prefix of ceil(n / 1024)
+  int nt;
+};
+__global__ __launch_bounds__(256) void cast_multi_k(CastList L) {
+  const int64_t c = blockIdx.x;
+  int lo = 0, hi = L.nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.chunk_off[mid] <= c) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t base = (c - L.chunk_off[lo]) * 1024 + threadIdx.x * 4;
+  const int64_t n = L.n[lo];
+  const float* __restrict__ in = L.in[lo];
+  bf16_t* __restrict__ out = L.out[lo];
+  if (base + 4 <= n && ((((uintptr_t)(in + base)) | ((uintptr_t)(out + base))) & 7) == 0) {
+    float v[4];
+    load_vec<float, 16>(in + base, v);
+    store_vec<bf16_t, 4>(out + base, v);
+  } else {
+    for (int64_t i = base; i < base + 4 && i < n; ++i) out[i] = f2bf(in[i]);
+  }
+}
+
 // out[c] (+)= sum_r in[r*ld + c]; grid (col tiles of 64, row chunks); one atomic per column per block
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ in, int64_t rows, int64_t cols, int64_t ld,
@@ -62,6 +202,96 @@ extern "C" int lthm_cast(const void* in, int32_t in_dtype, void* out, int32_t ou
   else
     return (int)hipErrorInvalidValue;
   LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_dropout(const void* x, int32_t x_dtype, void* y, int32_t y_dtype, int64_t n, float p,
+                            uint64_t seed, const float* res1, const float* res2, void* stream) {
+  LTHM_REQUIRE(n >= 0 && p >= 0.f && p < 1.f);
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(n, 256, 256 * 16);
+  const uint32_t th = dropout_thresh(p);
+  const float sc = 1.f / (1.f - p);
+  if (x_dtype == LTHM_F32 && y_dtype == LTHM_F32)
+    hipLaunchKernelGGL((dropout_k<float, float>), dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, n, th, sc,
+                       seed, res1, res2);
+  else if (x_dtype == LTHM_F32 && y_dtype == LTHM_BF16)
+    hipLaunchKernelGGL((dropout_k<float, bf16_t>), dim3(grid), dim3(256), 0, s, (const float*)x, (bf16_t*)y, n, th,
+                       sc, seed, res1, res2);
+  else if (x_dtype == LTHM_BF16 && y_dtype == LTHM_F32)
+    hipLaunchKernelGGL((dropout_k<bf16_t, float>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (float*)y, n, th,
+                       sc, seed, res1, res2);
+  else if (x_dtype == LTHM_BF16 && y_dtype == LTHM_BF16)
+    hipLaunchKernelGGL((dropout_k<bf16_t, bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n,
+                       th, sc, seed, res1, res2);
+  else
+    return (int)hipErrorInvalidValue;
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_dropout_rows(void* x, int32_t dtype, int64_t rows, int32_t cols, int32_t groups, float p,
+                                 uint64_t seed, void* stream) {
+  LTHM_REQUIRE(rows >= 0 && cols > 0 && groups > 0 && p >= 0.f && p < 1.f);
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(rows * groups * (int64_t)cols, 256, 256 * 16);
+  const uint32_t th = dropout_thresh(p);
+  const float sc = 1.f / (1.f - p);
+  if (dtype == LTHM_F32)
+    hipLaunchKernelGGL((dropout_rows_k<float>), dim3(grid), dim3(256), 0, s, (float*)x, rows, cols, groups, th, sc, seed);
+  else if (dtype == LTHM_BF16)
+    hipLaunchKernelGGL((dropout_rows_k<bf16_t>), dim3(grid), dim3(256), 0, s, (bf16_t*)x, rows, cols, groups, th, sc,
+                       seed);
+  else
+    return (int)hipErrorInvalidValue;
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed, void* stream) {
+  LTHM_REQUIRE(n >= 0 && p >= 0.f && p < 1.f);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dropout_mask_k, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, out, n,
+                     dropout_thresh(p), seed);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride,
+                                int64_t B, int32_t T, int32_t mb_size, float* b_tables, float* a_tables,
+                                const int64_t* hash_offsets, int32_t n_modules, int64_t num_buckets, float alpha,
+                                int64_t batch_idx0, float beta, int32_t update, float* out, void* stream) {
+  LTHM_REQUIRE(B >= 0 && T > 0 && mb_size > 0 && n_modules > 0 && num_buckets > 0);
+  LTHM_REQUIRE(ids_stride >= T && (!mask || mask_stride >= T));
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(logq_stream_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, ids, mask, B, T, ids_stride,
+                     mask_stride, mb_size, b_tables, a_tables, hash_offsets, n_modules, num_buckets, alpha, batch_idx0,
+                     beta, update, out);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_cast_multi_bf16(int32_t count, float** in, void** out, const int64_t* n, void* stream) {
+  LTHM_REQUIRE(count >= 0 && (count == 0 || (in && out && n)));
+  for (int t0 = 0; t0 < count; t0 += CM_MT) {
+    CastList L;
+    L.nt = 0;
+    L.chunk_off[0] = 0;
+    for (int t = t0; t < count && t < t0 + CM_MT; ++t) {
+      LTHM_REQUIRE(n[t] >= 0 && (n[t] == 0 || (in[t] && out[t])));
+      if (n[t] == 0) continue;
+      L.in[L.nt] = in[t];
+      L.out[L.nt] = static_cast<bf16_t*>(out[t]);
+      L.n[L.nt] = n[t];
+      L.chunk_off[L.nt + 1] = L.chunk_off[L.nt] + (n[t] + 1023) / 1024;
+      ++L.nt;
+    }
+    if (L.nt == 0) continue;
+    hipLaunchKernelGGL(cast_multi_k, dim3((unsigned)L.chunk_off[L.nt]), dim3(256), 0, (hipStream_t)stream, L);
+    LTHM_CHECK_LAUNCH();
+  }
   return 0;
 }
 

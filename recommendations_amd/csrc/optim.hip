@@ -43,7 +43,6 @@ struct AdamWList {
   float* g[AW_MT];
   float* m[AW_MT];
   float* v[AW_MT];
-  bf16_t* pb[AW_MT];  // bf16 copy of the updated parameter (the forward's GEMM operand), or null
   int64_t off[AW_MT + 1];
   int nt;
 };
@@ -69,7 +68,6 @@ __global__ __launch_bounds__(256) void adamw_multi_k(AdamWList L, float lr, floa
     v[j] = vi;
     const float pn = pi - (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
     p[j] = pn;
-    if (L.pb[lo]) L.pb[lo][j] = f2bf(pn);
   }
 }
 
@@ -189,7 +187,7 @@ extern "C" int lthm_adamw(float* p, float* g, float* m, float* v, int64_t n, flo
 
 extern "C" int lthm_adamw_multi(int32_t count, float** p, float** g, float** m, float** v,
                                 const int64_t* n, float lr, float beta1, float beta2, float eps, float weight_decay,
-                                int64_t step, float grad_scale, void** pb, void* stream) {
+                                int64_t step, float grad_scale, void* stream) {
   LTHM_REQUIRE(count >= 0 && step >= 1 && (count == 0 || (p && g && m && v && n)));
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
@@ -201,7 +199,6 @@ extern "C" int lthm_adamw_multi(int32_t count, float** p, float** g, float** m, 
       LTHM_REQUIRE(n[t] >= 0 && (n[t] == 0 || (p[t] && g[t] && m[t] && v[t])));
       if (n[t] == 0) continue;
       L.p[L.nt] = p[t]; L.g[L.nt] = g[t]; L.m[L.nt] = m[t]; L.v[L.nt] = v[t];
-      L.pb[L.nt] = pb ? static_cast<bf16_t*>(pb[t]) : nullptr;
       L.off[L.nt + 1] = L.off[L.nt] + n[t];
       ++L.nt;
     }

@@ -127,37 +127,65 @@ def cast(x: torch.Tensor, dtype) -> torch.Tensor:
     return out
 
 
-# bf16 GEMM operands of fp32 parameters, kept current by FusedAdamW (its multi-tensor
-# step writes the rounded update into the shadow, so the forward needs no per-step
-# cast).  A shadow is used only while the parameter's autograd version is the one it
-# was written at: any torch in-place write (load_state_dict, copy_, set_weights)
-# bumps the version and forces a re-cast; the raw-pointer optimizers that do not
-# maintain shadows drop them (shadow_drop).
-_SHADOWS: Dict[int, Any] = {}
+# bf16 GEMM operands of fp32 weights.  They are cast from the live fp32 parameter
+# at every forward, never kept across steps: a copy that outlives its forward can go
+# stale behind writes torch does not version (p.data.copy_, a collective writing
+# into p, module.to()).  A model casts all its encoder weights in ONE launch at
+# the start of its forward (``bf16_operands`` scope, lthm_cast_multi_bf16); inside
+# the scope ``bf16_operand`` returns those copies, outside it casts on the spot.
+_CAST_SCOPES: list = []
 
 
-def bf16_shadow(w: torch.Tensor) -> torch.Tensor:
-    """bf16 copy of the fp32 parameter w, reused across steps while it is current."""
-    key = id(w)
-    ent = _SHADOWS.get(key)
-    if ent is not None and ent[0]() is w and ent[2] == w._version and ent[1].shape == w.shape:
-        return ent[1]
-    out = cast(w.detach().contiguous(), torch.bfloat16)
-    import weakref
-    _SHADOWS[key] = (weakref.ref(w), out, w._version)
-    return out
+def cast_multi_bf16(ts):
+    """[bf16(t) for t in ts] for contiguous fp32 CUDA tensors, one launch per 48 tensors."""
+    import ctypes
+    ts = [t.detach() for t in ts]
+    for t in ts:
+        require_gpu(t)
+        _check(t.dtype == torch.float32, "cast_multi_bf16 takes fp32 tensors")
+    outs = [torch.empty(t.shape, dtype=torch.bfloat16, device=t.device) for t in ts]
+    n = len(ts)
+    if n == 0:
+        return outs
+    arr = lambda xs: ctypes.cast((ctypes.c_void_p * n)(*[x.data_ptr() for x in xs]), ctypes.c_void_p)  # noqa: E731
+    cnt = (ctypes.c_int64 * n)(*[t.numel() for t in ts])
+    call("lthm_cast_multi_bf16", n, arr(ts), arr(outs), ctypes.cast(cnt, ctypes.c_void_p), stream(),
+         _key="cast_multi_k", _work=6.0 * sum(t.numel() for t in ts), _unit="byte")
+    return outs
 
 
-def shadow_of(w: torch.Tensor) -> Optional[torch.Tensor]:
-    """The registered, current bf16 shadow of w (for the optimizer to update), or None."""
-    ent = _SHADOWS.get(id(w))
-    if ent is not None and ent[0]() is w and ent[2] == w._version and ent[1].shape == w.shape:
-        return ent[1]
-    return None
+class bf16_operands:
+    """Context: the bf16 copies of ``params`` (fp32), cast in one launch on entry and
+    served by ``bf16_operand`` until exit.  Scopes nest; the innermost match wins."""
+
+    def __init__(self, params):
+        # weights an enclosing scope already cast are served from there
+        self.params = [p for p in params if p is not None and p.dtype == torch.float32 and not _in_scope(p)]
+
+    def __enter__(self):
+        outs = cast_multi_bf16(self.params)
+        _CAST_SCOPES.append({id(p): (p, o) for p, o in zip(self.params, outs)})
+        return self
+
+    def __exit__(self, *exc):
+        _CAST_SCOPES.pop()
+        return False
 
 
-def shadow_drop(w: torch.Tensor) -> None:
-    _SHADOWS.pop(id(w), None)
+def _in_scope(w) -> bool:
+    return any(id(w) in sc and sc[id(w)][0] is w for sc in _CAST_SCOPES)
+
+
+def bf16_operand(w: torch.Tensor) -> torch.Tensor:
+    """bf16 GEMM operand of the weight w: the scope's copy if w was cast on scope entry
+    (same tensor object, same storage), else a fresh cast."""
+    for scope in reversed(_CAST_SCOPES):
+        ent = scope.get(id(w))
+        if ent is not None and ent[0] is w:
+            return ent[1]
+    if w.dtype == torch.bfloat16:
+        return w.detach().contiguous()
+    return cast(w.detach().contiguous(), torch.bfloat16)
 
 
 def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
@@ -170,6 +198,55 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
         accumulate = False
     call("lthm_colsum", ptr(x), dcode(x), rows, C, C, ptr(out), int(accumulate), stream())
     return out
+
+
+# ----------------------------------------------------------------- dropout
+def new_dropout_seed() -> int:
+    """A fresh 62-bit dropout seed from torch's default (CPU) generator, so
+    torch.manual_seed makes the masks reproducible; no device sync."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def dropout(x, p: float, seed: int, res1=None, res2=None, out_dtype=None):
+    """[res1] + [res2] + dropout_p(x) with the hash mask of ``seed`` (lthm_dropout)."""
+    require_gpu(x, res1, res2)
+    _check(0.0 <= p < 1.0, f"dropout p must be in [0, 1), got {p}")
+    for r in (res1, res2):
+        _check(r is None or (r.dtype == torch.float32 and r.numel() == x.numel()), "dropout residual: f32, x's size")
+    y = torch.empty(x.shape, dtype=out_dtype or x.dtype, device=x.device)
+    call("lthm_dropout", ptr(x), dcode(x), ptr(y), dcode(y), x.numel(), float(p), seed, ptr(res1), ptr(res2),
+         stream())
+    return y
+
+
+def dropout_rows_(x, groups: int, p: float, seed: int):
+    """In place: x [rows, groups * cols], row r of group g scaled by keep(g * rows + r) / (1 - p)."""
+    require_gpu(x)
+    _check(0.0 <= p < 1.0 and x.dim() == 2 and x.shape[1] % groups == 0, "dropout_rows_: bad arguments")
+    call("lthm_dropout_rows", ptr(x), dcode(x), x.shape[0], x.shape[1] // groups, groups, float(p), seed, stream())
+    return x
+
+
+def dropout_mask(n: int, p: float, seed: int, device) -> torch.Tensor:
+    """The keep decisions lthm_dropout applies to elements 0..n-1 (uint8)."""
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    require_gpu(out)
+    call("lthm_dropout_mask", ptr(out), n, float(p), seed, stream())
+    return out
+
+
+class DropoutFn(torch.autograd.Function):
+    """nn.Dropout(p) in training mode on the hash-mask kernel; the backward re-derives
+    the mask from the saved seed."""
+
+    @staticmethod
+    def forward(ctx, x, p: float, seed: int):
+        ctx.p, ctx.seed = p, seed
+        return dropout(x.contiguous(), p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dropout(dy.contiguous(), ctx.p, ctx.seed), None, None
 
 
 # ----------------------------------------------------------------- GEMM
@@ -237,10 +314,27 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
                "fp8 GEMM takes uint8 (e4m3) A and B with device scales")
         d.ab_dtype, d.a_scale, d.b_scale = FP8_E4M3, ptr(a_scale), ptr(b_scale)
     import ctypes
-    call("lthm_gemm", ctypes.addressof(d), stream(),
-         _key="gemm_fp8" if fp8 else f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>",
+    key = "gemm_fp8" if fp8 else f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>"
+    call("lthm_gemm", ctypes.addressof(d), stream(), _key=(_GEMM_TAG[-1] + ":" + key) if _GEMM_TAG else key,
          _work=2.0 * M * N * K * batch, _unit="flop")
     return out
+
+
+# Kernel-timer key prefix for the GEMMs launched inside a ``gemm_tag`` scope (bench.py
+# reports the encoder GEMMs -- the north star's MFMA target -- apart from the rest).
+_GEMM_TAG: list = []
+
+
+class gemm_tag:
+    def __init__(self, tag: str):
+        self.tag = tag
+
+    def __enter__(self):
+        _GEMM_TAG.append(self.tag)
+
+    def __exit__(self, *exc):
+        _GEMM_TAG.pop()
+        return False
 
 
 FP8_E4M3 = 2
@@ -440,9 +534,8 @@ def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, ze
          grad_scale, ptr(shadow), int(zero_grad), stream())
 
 
-def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0, pbs=None):
-    """lthm_adamw_multi: one launch per 48 fp32 tensors with identical hyper-parameters and step;
-    pbs: optional per-tensor bf16 buffers (or None) that receive the updated parameters."""
+def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0):
+    """lthm_adamw_multi: one launch per 48 fp32 tensors with identical hyper-parameters and step."""
     import ctypes
     n = len(ps)
     for p, g, m, v in zip(ps, gs, ms, vs):
@@ -453,16 +546,9 @@ def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0, pbs=N
                "adamw_multi_ takes contiguous fp32 tensors")
     arr = lambda ts: (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in ts])  # noqa: E731
     cnt = (ctypes.c_int64 * max(n, 1))(*[p.numel() for p in ps])
-    pb = None
-    if pbs is not None and any(b is not None for b in pbs):
-        for p, b in zip(ps, pbs):
-            if b is not None and (b.dtype != torch.bfloat16 or b.numel() != p.numel() or not b.is_contiguous()
-                                  or b.device != p.device):
-                raise ValueError("adamw_multi_: a shadow must be a contiguous bf16 tensor shaped like its parameter")
-        pb = ctypes.cast((ctypes.c_void_p * n)(*[0 if b is None else b.data_ptr() for b in pbs]), ctypes.c_void_p)
     call("lthm_adamw_multi", n, ctypes.cast(arr(ps), ctypes.c_void_p), ctypes.cast(arr(gs), ctypes.c_void_p),
          ctypes.cast(arr(ms), ctypes.c_void_p), ctypes.cast(arr(vs), ctypes.c_void_p),
-         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, pb, stream(),
+         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, stream(),
          _key="lthm_adamw", _work=28.0 * sum(p.numel() for p in ps), _unit="byte")
 
 

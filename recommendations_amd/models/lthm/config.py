@@ -126,5 +126,6 @@ def lthm_config(T: int, d: int, n_layers: int, n_head: int, cat_features: int = 
     pt = ProductTowerConfig(out_emb_dim=out_emb_dim or d,
                             latent_model_config=LatentModelConfig(vocab_size_latent=item_vocab))
     cat = CategoricalContextConfig(n_features=cat_features, vocab_size=cat_vocab)
+    lq = LogQConfig(beta=kw.pop("log_q_beta", 0.0), num_buckets=kw.pop("log_q_buckets", 2 ** 24))
     return LTHMModelConfig(context_width=T, num_layers=n_layers, transformer_config=tc, product_tower=pt,
-                           categorical=cat, **kw)
+                           categorical=cat, log_q_config=lq, **kw)

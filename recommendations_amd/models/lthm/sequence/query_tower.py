@@ -24,7 +24,7 @@ import torch.nn as nn
 from .... import kernels as K
 from ...._lib import STRUCTS, call, dcode, ptr, require_gpu, stream
 from ....commons.layers import FlatEmbedding, PatternFromTimelocal
-from ....commons.transformers.layers import TransformerBlock
+from ....commons.transformers.layers import TransformerBlock, dropout
 
 
 class LinearFn(torch.autograd.Function):
@@ -205,7 +205,12 @@ class QueryTower(nn.Module):
         }
 
     def transformer_encoder(self, x: torch.Tensor) -> torch.Tensor:
-        # dropout p = 0 in every north-star config (identity); x = x + block(x) fused per block
-        for mod in self.transformer.residual_attn:
-            x = mod.forward_double_residual(x)
+        # query_tower.py:131-137: dropout, then x = x + block(x) per block (fused per block);
+        # every block's GEMM weights are cast to bf16 in one launch for this forward
+        x = dropout(x, self.transformer.dropout.p, self.training)
+        blocks = self.transformer.residual_attn
+        ws = [w for mod in blocks for w in mod.gemm_weights()]
+        with K.bf16_operands(ws):
+            for mod in blocks:
+                x = mod.forward_double_residual(x)
         return x

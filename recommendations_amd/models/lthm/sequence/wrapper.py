@@ -27,6 +27,7 @@ import torch.nn as nn
 from .... import kernels as K
 from ...._lib import STRUCTS, call, ptr, stream
 from ....commons.base_model_wrapper import BaseModelWrapper
+from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
 from .encoder import Encoder
 
@@ -35,9 +36,10 @@ NSTAT_BASE = 7
 
 class ContrastiveLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, target, mask, offsets_dev, cfg):
+    def forward(ctx, y, target, mask, offsets_dev, cfg, logq=None):
         """y [B, T+1, NH, De] (next_token_emb), target [B, T, De] (current_token_emb),
-        mask [B, T] uint8 (row stride = mask.stride(0)), offsets_dev int32 [n_mb, NH]."""
+        mask [B, T] uint8 (row stride = mask.stride(0)), offsets_dev int32 [n_mb, NH];
+        logq: None or f32 [B, T], the additive logit correction -beta * logQ of each input token."""
         B, Tp, NH, De = y.shape
         T = Tp - 1
         mbs, tau, ks = cfg["mb"], cfg["tau"], cfg["ks"]
@@ -60,10 +62,12 @@ class ContrastiveLossFn(torch.autograd.Function):
         nstat = NSTAT_BASE + len(ks)
         stats = torch.empty((NH, n_mb, nstat), **f32)
         ks_dev = torch.tensor(ks, dtype=torch.int32).to(dev, non_blocking=True)
+        lqc = torch.empty((NH, n_mb, n_max), **f32) if logq is not None else None
         descs = []
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
-                                        lse[h], pos[h], cnt[h], rank[h], diag[h], w[h])
+                                        lse[h], pos[h], cnt[h], rank[h], diag[h], w[h], logq,
+                                        None if lqc is None else lqc[h])
             call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats[h]), nstat, ptr(ks_dev), len(ks),
                  1.0 / n_mb, stream(), _key="cl_fwd_k", _work=cfg["flops"][h], _unit="flop")
             descs.append(d)
@@ -71,15 +75,18 @@ class ContrastiveLossFn(torch.autograd.Function):
         loss = torch.empty(1, **f32)
         call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
         loss = loss / n_mb
-        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev)
+        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc)
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
         ctx.flops = cfg["flops"]
         return loss
 
     @staticmethod
-    def _desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev, lse, pos, cnt, rank, diag, w):
+    def _desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev, lse, pos, cnt, rank, diag, w,
+              logq=None, lqc=None):
         d = STRUCTS["lthm_contrastive_desc"]()
+        if logq is not None:
+            d.logq, d.logq_stride, d.logq_col = ptr(logq), logq.stride(0), ptr(lqc)
         d.out_n, d.in_n, d.mask, d.mask_stride = ptr(yn), ptr(tn), ptr(mask), mask.stride(0)
         d.B, d.T, d.n_heads, d.head, d.De = B, T, NH, h, De
         d.mb_size, d.n_mb, d.n_max, d.tau = mbs, n_mb, n_max, tau
@@ -89,7 +96,7 @@ class ContrastiveLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dloss):
-        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev = ctx.saved_tensors
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc = ctx.saved_tensors
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         dev = yc.device
         g = dloss.contiguous().float()
@@ -99,13 +106,16 @@ class ContrastiveLossFn(torch.autograd.Function):
         d_in = K.zeros((B, T, De), torch.float32, dev)
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
-                                        lse[h], None, None, None, diag[h], w[h])  # diag: shift scratch
+                                        lse[h], None, None, None, diag[h], w[h],  # diag: shift scratch
+                                        logq, None if lqc is None else lqc[h])
             d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
+            # algorithmic work 3 x 2 n^2 De per head (one S recompute, dS . in, dS^T . out);
+            # the ROWS and COLS kernels each recompute S, so they execute 4 x
             call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
-                 _work=4.0 * ctx.flops[h], _unit="flop")
+                 _work=3.0 * ctx.flops[h], _unit="flop")
         dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
         dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
-        return dy.view(yc.shape), dt.view(tc.shape), None, None, None
+        return dy.view(yc.shape), dt.view(tc.shape), None, None, None, None
 
 
 class LTHMModelWrapper(BaseModelWrapper):
@@ -119,10 +129,12 @@ class LTHMModelWrapper(BaseModelWrapper):
         self._loss_type = model_config.loss_type
         self._metrics_k_all = list(model_config.metrics_k_all)
         self._lookahead = list(model_config.lookahead)
-        self._log_q_beta = model_config.log_q_config.beta
-        if self._log_q_beta != 0.0:
-            raise NotImplementedError("log_q_config.beta != 0: logQ-corrected logits are not fused yet")
         self._model = Encoder(model_config)
+        # wrapper.py:34-42 (built whatever beta is, so the state_dict carries its a / b buffers)
+        lq = model_config.log_q_config
+        self._log_q_beta = float(lq.beta)
+        self._log_q_calc = CascadedStreamingLogQCorrectionModule(
+            num_buckets=lq.num_buckets, hash_offsets=lq.hash_offsets, alpha=lq.alpha, p_init=lq.p_init)
         self.batch_idx = 0
         self._rng = random.Random(model_config.seed)
         self.last_stats = None
@@ -180,8 +192,14 @@ class LTHMModelWrapper(BaseModelWrapper):
                 tot += 2.0 * n * n * y.shape[-1]
             flops.append(tot)
         cfg = dict(mb=mbs, tau=self._softmax_temperature, ks=self._metrics_k_all, flops=flops)
-        loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg)
-        self.batch_idx += 1
+        logq = None
+        if self._log_q_beta != 0.0:
+            # wrapper.py:126-130 per mini-batch in order: logQ train_step on its non-pad ids,
+            # then the correction -beta * logQ of its ids (zeroed on the positive in-kernel)
+            logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
+                                                      self._log_q_beta)
+        loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg, logq)
+        self.batch_idx += n_mb  # the reference counts helper calls, one per mini-batch
         self.last_stats = (loss.grad_fn, offs, step_type, B)
         return loss, {}
 

@@ -39,13 +39,12 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = K.zeros(p.shape, torch.float32, p.device)
                 st["step"] += 1
                 grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                b = buckets.setdefault(st["step"], ([], [], [], [], []))
-                for lst, t in zip(b, (p.data, grad, st["exp_avg"], st["exp_avg_sq"], K.shadow_of(p))):
+                b = buckets.setdefault(st["step"], ([], [], [], []))
+                for lst, t in zip(b, (p.data, grad, st["exp_avg"], st["exp_avg_sq"])):
                     lst.append(t)
-            for step, (ps, gs, ms, vs, pbs) in buckets.items():
-                # the bf16 shadows the forward reads (K.bf16_shadow) are rewritten in the same pass
+            for step, (ps, gs, ms, vs) in buckets.items():
                 K.adamw_multi_(ps, gs, ms, vs, g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
-                               grad_scale=grad_scale, pbs=pbs)
+                               grad_scale=grad_scale)
         return loss
 
 
@@ -68,7 +67,6 @@ class FusedAdagrad(torch.optim.Optimizer):
                 st["step"] += 1
                 K.adagrad_(p.data, p.grad.contiguous(), st["sum"], g["lr"], g["lr_decay"], g["eps"],
                            g["weight_decay"], st["step"])
-                K.shadow_drop(p)  # written through its pointer: a bf16 shadow would be stale
         return loss
 
 
@@ -91,7 +89,7 @@ class SparseRowAdamW:
             if st is None:
                 st = self.state[id(m)] = (K.zeros(m.weight.shape, torch.float32, m.weight.device),
                                           K.zeros(m.weight.shape, torch.float32, m.weight.device))
-            shadow = m._shadow if (m._shadow is not None and m._shadow_version == m.weight._version) else None
+            shadow = m.shadow_current()
             K.sparse_adamw_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
                             m.sparse_grad, st[0], st[1], m.sparse_flags, self.lr, self.betas, self.eps,
                             self.weight_decay, self.step_count, shadow=shadow)
@@ -116,7 +114,7 @@ class SparseRowAdagrad(SparseRowAdamW):
             st = self.state.get(id(m))
             if st is None:
                 st = self.state[id(m)] = K.zeros(m.weight.shape, torch.float32, m.weight.device)
-            shadow = m._shadow if (m._shadow is not None and m._shadow_version == m.weight._version) else None
+            shadow = m.shadow_current()
             K.sparse_adagrad_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
                               m.sparse_grad, st, m.sparse_flags, self.lr, self.lr_decay, self.eps, self.step_count,
                               shadow=shadow)

@@ -9,6 +9,8 @@ import numpy as np
 import pandas as pd
 import pytest
 import torch
+
+from parity import check, relerr
 import torch.nn.functional as F
 
 from oracle import ref
@@ -16,9 +18,6 @@ from oracle import ref
 pytestmark = pytest.mark.gpu
 
 
-def relerr(a, b):
-    a, b = a.detach().double().cpu(), b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def _df(n, D, seed=0):
@@ -47,7 +46,7 @@ def test_train_model_matches_dense_adagrad(dev):
             F.mse_loss(y, x[it]).backward()
             opt.step()
             opt.zero_grad()
-    assert relerr(m.emb.weight, W) < 1e-5
+    check('m.emb.weight, W', relerr(m.emb.weight, W), 1e-5)
 
 
 def test_train_mask_model_matches_dense_adagrad(dev):
@@ -92,11 +91,11 @@ def test_train_mask_model_matches_dense_adagrad(dev):
             opt.step()
             opt.zero_grad()
     # the mask MLP runs on bf16 MFMA operands (the reference's MLP is fp32): 1e-2 on the weights
-    assert relerr(model[0].emb.weight, W) < 1e-2
+    check('model[0].emb.weight, W', relerr(model[0].emb.weight, W), 1e-2)
     glins = [l for l in model[1].model if isinstance(l, torch.nn.Linear)]
     for gl, w, b in zip(glins, ws, bs):
-        assert relerr(gl.weight, w) < 1e-2
-        assert relerr(gl.bias, b) < 1e-2
+        check('gl.weight, w', relerr(gl.weight, w), 1e-2)
+        check('gl.bias, b', relerr(gl.bias, b), 1e-2)
 
 
 def test_model_wrapper_forward(dev):
@@ -114,7 +113,7 @@ def test_model_wrapper_forward(dev):
     mk = ref.mlp_quickgelu(ref.kshift_fwd_torch(ids, mask[0].emb.weight.detach().cpu(), 16, False),
                            [l.weight.detach().cpu() for l in lins], [l.bias.detach().cpu() for l in lins])
     exp = mk.sigmoid() * e
-    assert relerr(got, exp) < 2e-2  # the mask MLP runs on bf16 MFMA operands
+    check('got, exp', relerr(got, exp), 2e-2)  # the mask MLP runs on bf16 MFMA operands
 
 
 def _artifact_ref(ids, sd, K, normalize, Km):
@@ -147,7 +146,7 @@ def test_item_artifact_fused_vs_oracle(dev, D, K, Km, Dm, H1, norm, tdt):
     ids[0, :5] = torch.tensor([0, 1, -1, 2 ** 63 - 1, -2 ** 63])
     got = m(ids.to(dev)).cpu()
     assert got.shape == (3, 333, D)
-    assert relerr(got, _artifact_ref(ids.view(-1), sd, K, norm, Km).view(3, 333, D)) < 1e-5
+    check('got, _artifact_ref(ids.view(-1), sd, K, norm, Km).view(3, 333, D)', relerr(got, _artifact_ref(ids.view(-1), sd, K, norm, Km).view(3, 333, D)), 1e-5)
     assert m(torch.empty(0, dtype=torch.int64, device=dev)).shape == (0, D)
 
 
@@ -168,9 +167,9 @@ def test_item_artifact_round_trip_and_encoder(dev, tmp_path):
     w = w.to(dev)
     ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (4096,), dtype=torch.int64, device=dev)
     with torch.no_grad():
-        assert relerr(a(ids), w(ids)) < 2e-2       # the unfused mask MLP uses bf16 MFMA operands
+        check('a(ids), w(ids)', relerr(a(ids), w(ids)), 2e-2)  # the unfused mask MLP uses bf16 MFMA operands
     sd = {k: v.detach().cpu() for k, v in w.state_dict().items()}
-    assert relerr(a(ids).cpu(), _artifact_ref(ids.cpu(), sd, 16, True, 16)) < 1e-5
+    check('a(ids).cpu(), _artifact_ref(ids.cpu(), sd, 16, True, 16)', relerr(a(ids).cpu(), _artifact_ref(ids.cpu(), sd, 16, True, 16)), 1e-5)
 
     from recommendations_amd.models.lthm.builder import LTHMModelBuilder
     from recommendations_amd.models.lthm.config import lthm_config

@@ -14,6 +14,8 @@ import math
 
 import pytest
 import torch
+
+from parity import check, relerr
 import torch.nn.functional as F
 
 from oracle import ref
@@ -21,9 +23,6 @@ from oracle import ref
 pytestmark = pytest.mark.gpu
 
 
-def relerr(a, b):
-    a, b = a.detach().double().cpu(), b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def _deq(q, s):
@@ -67,9 +66,9 @@ def test_fp8_gemm_vs_dequantised(dev, M, N, K, act, res):
         exp = exp + r1.double()
     if r2 is not None:
         exp = exp + r2.double()
-    assert relerr(out, exp) < 3e-5
+    check('out, exp', relerr(out, exp), 3e-5)
     if act:
-        assert relerr(pre.float(), z) < 1e-2
+        check('pre.float(), z', relerr(pre.float(), z), 1e-2)
 
 
 def test_transformer_block_fp8_c5_shape(dev):
@@ -94,11 +93,11 @@ def test_transformer_block_fp8_c5_shape(dev):
     pr = {k: v.clone().requires_grad_(True) if v.is_floating_point() else v for k, v in sd.items()}
     yr = ref.transformer_block(xr, pr, H, True)
     # residual stream included: compare the block's update y - x (the part the GEMMs produce)
-    assert relerr(y.detach().cpu() - x, yr.detach() - x) < 5e-2
+    check('y.detach().cpu() - x, yr.detach() - x', relerr(y.detach().cpu() - x, yr.detach() - x), 5e-2)
     dy = torch.randn(B, T, d)
     y.backward(dy.to(dev))
     yr.backward(dy)
-    assert relerr(xd.grad, xr.grad) < 1e-1
+    check('xd.grad, xr.grad', relerr(xd.grad, xr.grad), 1e-1)
     for n, p in blk.named_parameters():
         if pr[n].grad is not None and float(pr[n].grad.norm()) > 0:
-            assert relerr(p.grad, pr[n].grad) < 1.5e-1, n
+            check(f"p.grad, pr[n].grad {n}", relerr(p.grad, pr[n].grad), 1.5e-1)

@@ -10,6 +10,8 @@ itself (fp32) matches torch to 1e-6.
 import numpy as np
 import pytest
 import torch
+
+from parity import check, relerr
 import torch.nn.functional as F
 
 from oracle import ranker_ref
@@ -17,10 +19,6 @@ from oracle import ranker_ref
 pytestmark = pytest.mark.gpu
 
 
-def relerr(a, b):
-    a = a.detach().double().cpu()
-    b = b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def _small(dev, seed=0, **kw):
@@ -42,7 +40,7 @@ def test_bce_with_logits_kernel(dev):
     assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
     loss.backward()
     ref.backward()
-    assert relerr(zd.grad, zr.grad) < 1e-6
+    check('zd.grad, zr.grad', relerr(zd.grad, zr.grad), 1e-6)
 
 
 @pytest.mark.parametrize("B", [1000, 4096])
@@ -57,7 +55,7 @@ def test_ranker_step_vs_oracle(dev, B):
     logits_ref = ranker_ref.ranker_forward(sd, cfg, batch)
     loss_ref = F.binary_cross_entropy_with_logits(logits_ref.reshape(-1), batch["label"])
     # bf16 MLP operands + bf16-gathered categorical rows: 2e-2 on logits, 1e-2 on the loss
-    assert relerr(out["logits"], logits_ref) < 2e-2
+    check('out["logits"], logits_ref', relerr(out["logits"], logits_ref), 2e-2)
     assert abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)) < 1e-2
     loss.backward()
     loss_ref.backward()
@@ -69,7 +67,7 @@ def test_ranker_step_vs_oracle(dev, B):
         want = sd[n].grad
         if want is None or float(want.norm()) == 0.0:
             continue
-        assert relerr(got, want) < 5e-2, (n, relerr(got, want))
+        check(f"got, want {(n, relerr(got, want))}", relerr(got, want), 5e-2)
 
 
 def test_ranker_training_steps(dev):

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from parity import check, relerr
+
 import torch.nn.functional as F
 
 from oracle import ref
@@ -18,9 +20,6 @@ from recommendations_amd import kernels as K
 pytestmark = pytest.mark.gpu
 
 
-def relerr(a, b):
-    a, b = a.detach().double().cpu(), b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def table_ref(rows, dy, R, segments=None):
@@ -230,5 +229,5 @@ def test_product_tower_fwd_vs_oracle(dev, Dout):
     e = e.masked_fill(mref.unsqueeze(-1), 0.0)
     pr = F.linear(e, sd["product_mapper.weight"])
     assert (mask.cpu().bool() == mref).all()
-    assert relerr(emb.float(), e) < 2e-2
-    assert relerr(prod.float(), pr) < 2e-2
+    check('emb.float(), e', relerr(emb.float(), e), 2e-2)
+    check('prod.float(), pr', relerr(prod.float(), pr), 2e-2)

@@ -10,8 +10,12 @@ mkdir -p gpurun_out
 for s in $STAGES; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-        > gpurun_out/${TAG}_tests.log 2>&1
+      # exit status 1 = assertion failures only: go on; anything else (fault, abort, time limit): stop
+      rc=0
+      PARITY_LOG=gpurun_out/${TAG}_parity.json timeout -k 10 900 python -u -m pytest tests -m gpu -v \
+        --timeout 240 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || rc=$?
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest exit $rc: stopping"; exit $rc; fi
+      [ $rc -eq 1 ] && echo "TESTS FAILED (assertions)"
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     bench)
       timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 ;;
