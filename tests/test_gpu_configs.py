@@ -39,12 +39,23 @@ def test_c2_full_batch_step_properties(dev, c2):
     B, T = 4096, 128
     batch = synthetic_lthm_batch(B, T, n_cat=32, seed=1234, device=dev)
     # item KShift gather (P = 1M, D = 32, K = 16) bit-exact vs the C oracle on all 524,288 ids
+    # (the raw in-order f32 pool bit-exact; the L2-normalised module output to the golden
+    # tests' 1e-6: the norm's sum of squares is a reduction whose order differs)
+    from recommendations_amd import kernels as K
     pe = m._model.product_emb_module
-    with torch.no_grad():
-        got = pe(batch["product_ids"]).cpu().numpy()
+    ids_np = batch["product_ids"].cpu().numpy()
     W = pe.emb.weight.detach().float().cpu().numpy()
-    want = ref.kshift_fwd_c(batch["product_ids"].cpu().numpy(), W, 16, 1 if pe._normalize_output else 0)
-    assert np.array_equal(got, want)
+    with torch.no_grad():
+        raw = K.kshift(batch["product_ids"], pe.emb.weight, W.shape[0], 16, K.KSHIFT_NONE,
+                       out_dtype=torch.float32).cpu().numpy()
+        got = pe(batch["product_ids"]).float().cpu().numpy()
+    assert np.array_equal(raw, ref.kshift_fwd_c(ids_np, W, 16, 2))
+    mode = 1 if pe._normalize_output else 0
+    want = ref.kshift_fwd_c(ids_np, W, 16, mode)
+    if mode == 0:
+        assert np.array_equal(got, want)
+    else:
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-7)
     # categorical tables (32 x 1M x 32, gathered from their bf16 shadow, K = 8): two features vs the oracle
     tabs = m._model.user_context.tables
     with torch.no_grad():
@@ -105,7 +116,7 @@ def test_c2_slice_vs_oracle(dev, c2):
     for n, p in m.named_parameters():
         if p.grad is None or n not in sd or sd[n].grad is None or float(sd[n].grad.norm()) == 0.0:
             continue
-        check(f"C2 slice grad {n}", relerr(p.grad, sd[n].grad), 0.1)
+        check(f"C2 slice grad {n}", relerr(p.grad, sd[n].grad), 6e-2)  # measured max 3.0e-2 (query_tower.pad)
         n_chk += 1
     assert n_chk > 30
     m.zero_grad(set_to_none=True)

@@ -134,7 +134,7 @@ def test_lthm_step_vs_oracle(dev, B, T, d, L, H):
         gr = sd[key].grad
         if gr is None or float(gr.norm()) == 0.0:
             continue
-        check(f"grad {n}", relerr(gp, gr), 0.1)
+        check(f"grad {n}", relerr(gp, gr), 4e-2)  # measured max 2.0e-2 (r02a)
         checked += 1
     assert checked > 30
 
@@ -162,7 +162,8 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     """BASELINE configs[4] (C5) shape at a small batch: T = 512 (T' = 513, the windowed
     attention), d = 512, H = 8, fp8 e4m3 forward encoder GEMMs, 8-sequence loss
     mini-batches, vs the fp32 oracle.  e4m3 operands (3 mantissa bits, per-tensor
-    scales): 5e-2 on the loss and the head outputs, 0.2 relative on gradients."""
+    scales): 5e-2 on the loss and the head outputs, 8e-2 relative on gradients (2x the
+    measured maximum)."""
     from recommendations_amd.data import synthetic_lthm_batch
     B, T = 16, 512
     cfg, m = _model(dev, T=T, d=512, L=2, H=8, n_cat=0, fp8=True, train_mini_batch_size=8)
@@ -183,7 +184,7 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     for n, p in m.named_parameters():
         if p.grad is None or sd[n].grad is None or float(sd[n].grad.norm()) == 0.0:
             continue
-        check(f"grad {n}", relerr(p.grad, sd[n].grad), 0.2)
+        check(f"grad {n}", relerr(p.grad, sd[n].grad), 8e-2)  # measured max 4.0e-2 (r02a)
         checked += 1
     assert checked > 20
 

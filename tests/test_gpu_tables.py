@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from parity import check, relerr
+from parity import check as pcheck, relerr
 
 import torch.nn.functional as F
 
@@ -229,5 +229,5 @@ def test_product_tower_fwd_vs_oracle(dev, Dout):
     e = e.masked_fill(mref.unsqueeze(-1), 0.0)
     pr = F.linear(e, sd["product_mapper.weight"])
     assert (mask.cpu().bool() == mref).all()
-    check('emb.float(), e', relerr(emb.float(), e), 2e-2)
-    check('prod.float(), pr', relerr(prod.float(), pr), 2e-2)
+    pcheck('product tower emb', relerr(emb.float(), e), 2e-2)
+    pcheck('product tower prod', relerr(prod.float(), pr), 2e-2)
