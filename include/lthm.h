@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 17 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 18 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -222,11 +222,19 @@ typedef struct lthm_attn_desc {
   void* dv;
   float* dtable_part;
   float* delta;
+  const float* mask;          /* optional additive mask, f32 [., ., T, T] (NULL: none) */
+  int64_t mask_batch_stride;  /* 0 broadcasts one mask over the batch */
+  int64_t mask_head_stride;   /* 0 broadcasts over the heads */
+  int64_t mask_row_stride;    /* >= T */
 } lthm_attn_desc;
 
 /* bf16 q/k/v/out, f32 table [table_rows, H] (row q-k+T), lse f32 [B, H, T].
  * T <= 256: one workgroup per (batch, head) holds K and V whole in LDS.
- * 256 < T <= 4096 (E = 32/64/128): 64-row workgroups stream K/V windows. */
+ * 256 < T <= 4096 (E = 32/64/128): 64-row workgroups stream K/V windows.
+ * mask != NULL: S[b, h, q, k] += mask[b * mask_batch_stride + h * mask_head_stride
+ * + q * mask_row_stride + k] (the reference's general additive attn_mask, SDPA :57-58,
+ * TransformerBlock.inner_forward :404-408, on top of the causal flag); served by the
+ * whole-head VALU kernels, so T <= 256 and K, V, Q, dO of one head fit in LDS. */
 int lthm_attn_fwd(const lthm_attn_desc* desc, void* stream);
 /* dq/dk/dv bf16 (same strides as q/k/v); dtable_part f32 [parts, 2T+1, H] with
  * parts = lthm_attn_bwd_parts(B, T) (reduce over the first dim; = B for T <= 256);

@@ -125,6 +125,26 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+TORCH_OPS_PATH = os.path.join(_PKG_DIR, "liblthm_torch_ops.so")
+_TORCH_OPS = False
+
+
+def load_torch_ops() -> None:
+    """Register the TORCH_LIBRARY(lthm) ops (csrc/torch_ops/lthm_ops.cpp) with the
+    dispatcher: the scriptable boundary (torch.ops.lthm.*) over the same kernels.
+    Raises if the op library is not built (no fallback)."""
+    global _TORCH_OPS
+    if _TORCH_OPS:
+        return
+    if not os.path.exists(TORCH_OPS_PATH):
+        raise RuntimeError(
+            f"{TORCH_OPS_PATH} not found: the TORCH_LIBRARY(lthm) op layer is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'`).")
+    load()  # liblthm_hip.so first (RTLD_GLOBAL), the op library links against it
+    torch.ops.load_library(TORCH_OPS_PATH)
+    _TORCH_OPS = True
+
+
 class KernelTimer:
     """Live per-entry-point timing with HIP events on torch's current stream (the
     stream every launch goes to).  bench.py enables it over the timed region;

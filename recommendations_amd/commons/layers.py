@@ -111,6 +111,14 @@ class KShiftEmbedding(_SparseRowsMixin, nn.Module):
         return self.emb.weight
 
     def forward(self, id_: torch.Tensor) -> torch.Tensor:
+        if torch.jit.is_scripting():
+            # TorchScript (embedding_module_gen.py:191): the TORCH_LIBRARY(lthm) op, same kernel
+            return torch.ops.lthm.kshift(id_, self.emb.weight, self._num_embeddings, self._num_shifts, self._mode,
+                                         1, self._out_dtype)
+        return self._forward_eager(id_)
+
+    @torch.jit.unused
+    def _forward_eager(self, id_: torch.Tensor) -> torch.Tensor:
         if self.sparse and self.emb.weight.requires_grad and torch.is_grad_enabled():
             if self._out_dtype is None:
                 self._out_dtype = self.emb.weight.dtype
@@ -285,7 +293,13 @@ class RowShardedKShiftEmbedding(nn.Module):
 class QuickGELU(nn.Module):
     """commons/layers.py:9-11."""
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.jit.is_scripting():
+            return torch.ops.lthm.activation(x, K.ACT_QGELU)
+        return self._forward_eager(x)
+
+    @torch.jit.unused
+    def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
         return K.ActivationFn.apply(x, K.ACT_QGELU)
 
 
@@ -304,6 +318,19 @@ class MLP(nn.Module):
         self.model = nn.Sequential(*blocks)
 
     def forward(self, x: torch.Tensor):
+        if torch.jit.is_scripting():
+            ws: List[torch.Tensor] = []
+            bs: List[torch.Tensor] = []
+            for m in self.model:
+                if isinstance(m, nn.Linear):
+                    ws.append(m.weight)
+                    bs.append(m.bias)
+            acts = [K.ACT_QGELU] * (len(ws) - 1) + [K.ACT_NONE]
+            return torch.ops.lthm.mlp_chain(x, ws, bs, acts, True)
+        return self._forward_eager(x)
+
+    @torch.jit.unused
+    def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
         lins = [m for m in self.model if isinstance(m, nn.Linear)]
         acts = [K.ACT_QGELU] * (len(lins) - 1) + [K.ACT_NONE]
         return K.mlp_chain(x, lins, acts, out_f32=True)
@@ -356,8 +383,10 @@ class QREmbedding(nn.Module):
         y = K.kshift(q.contiguous(), self.emb_q.weight, self._div, 1, K.KSHIFT_NONE) + \
             K.kshift(r.contiguous(), self.emb_r.weight, self._div, 1, K.KSHIFT_NONE)
         if self.normalize_output:
-            y = K.kshift(torch.arange(y.shape[0], device=y.device), y, y.shape[0], 1, K.KSHIFT_NORMALIZE) \
-                if y.dim() == 2 else y / y.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+            # F.normalize(y, 2, -1) as the K = 1 normalising gather of y's own rows
+            y2 = y.reshape(-1, self.emb_dim)
+            n = y2.shape[0]
+            y = K.kshift(torch.arange(n, device=y.device), y2, max(n, 1), 1, K.KSHIFT_NORMALIZE).view(y.shape)
         return y
 
 

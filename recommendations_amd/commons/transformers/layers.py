@@ -85,7 +85,7 @@ class TransformerBlockFn(torch.autograd.Function):
 
     @staticmethod
     def _forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal,
-                 double_residual, fp8=False, drop=None):
+                 double_residual, fp8=False, drop=None, mask=None):
         require_gpu(x)
         B, T, d = x.shape
         E = d // H
@@ -108,7 +108,8 @@ class TransformerBlockFn(torch.autograd.Function):
         if pa > 0.0:
             K.dropout_rows_(qkv, 3, pa, seed)  # the attention sees (and the backward saves) the scaled q / k / v
         tab = None if table is None else table.detach().contiguous()
-        o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
+        mop = K.attn_mask_operand(mask, B, H, T)
+        o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop)
         if pr > 0.0:
             x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32), pr, seed + 1, res1=x2)
         else:
@@ -126,6 +127,7 @@ class TransformerBlockFn(torch.autograd.Function):
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
                    b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
+        ctx.mop = mop
         return out.view(B, T, d)
 
     @staticmethod
@@ -159,7 +161,7 @@ class TransformerBlockFn(torch.autograd.Function):
         dwp = K.linear_wgrad(dx1b, o)
         dbp = K.colsum(dx1r) if has_bp else None
         do = K.linear_dgrad(dx1b, wp_b)
-        dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+        dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal, ctx.mop)
         if pa > 0.0:
             K.dropout_rows_(dqkv, 3, pa, seed)
         dwqkv = K.linear_wgrad(dqkv, h1)
@@ -173,7 +175,7 @@ class TransformerBlockFn(torch.autograd.Function):
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
         return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
-                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None)
+                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None, None)
 
 
 # ------------------------------------------------------------------ modules
@@ -267,18 +269,20 @@ def _drop_args(mod: nn.Module, p_attn: float, p_resid: float):
     return (float(p_attn), float(p_resid), K.new_dropout_seed())
 
 
-def _mask_is_causal(mask: Optional[torch.Tensor], T: int) -> bool:
-    """True for the reference's causal additive mask (commons/transformers/layers.py:
-    397-402: -inf above the diagonal and the constant 1.0 elsewhere, a softmax-invariant
-    shift); other additive masks are not fused in the kernel."""
+def _split_mask(mask: Optional[torch.Tensor], T: int):
+    """(causal, extra) for an additive attention mask.  The reference's causal mask
+    (commons/transformers/layers.py:397-402: -inf above the diagonal and one constant
+    elsewhere, a softmax-invariant shift) runs as the kernels' causal flag; any other
+    additive mask is added to the scores as given (SDPA :57-58) by the whole-head
+    kernels (T <= 256)."""
     if mask is None:
-        return False
+        return False, None
     m = mask.reshape(-1, T, T)
     tri = torch.ones((T, T), dtype=torch.bool, device=mask.device).triu(1)
     kept = m[:, ~tri]
-    if not (bool(torch.isneginf(m[:, tri]).all()) and bool((kept == kept.reshape(-1)[0]).all())):
-        raise NotImplementedError("additive attention masks other than the causal mask are not fused in the kernel")
-    return True
+    if bool(torch.isneginf(m[:, tri]).all()) and bool((kept == kept.reshape(-1)[0]).all()):
+        return True, None
+    return False, mask
 
 
 class _SelfAttnFn(torch.autograd.Function):
@@ -289,7 +293,7 @@ class _SelfAttnFn(torch.autograd.Function):
     expanded per head and sums their gradients over the heads."""
 
     @staticmethod
-    def forward(ctx, x, w_in, b_in, w_kv, b_kv, w_out, b_out, table, H, causal, shared_kv, drop=None):
+    def forward(ctx, x, w_in, b_in, w_kv, b_kv, w_out, b_out, table, H, causal, shared_kv, drop=None, mask=None):
         require_gpu(x)
         pa, pr, seed = drop if drop is not None else (0.0, 0.0, 0)
         B, T, C = x.shape
@@ -298,6 +302,7 @@ class _SelfAttnFn(torch.autograd.Function):
         xb = K.cast(x.contiguous().view(M, C), torch.bfloat16)
         w_in_b, w_out_b = _bf(w_in), _bf(w_out)
         tab = None if table is None else table.detach().contiguous()
+        mop = ctx.mop = K.attn_mask_operand(mask, B, H, T)
         if shared_kv:
             w_kv_b = _bf(w_kv)
             q = K.linear_fwd(xb, w_in_b, _f(b_in))
@@ -305,13 +310,13 @@ class _SelfAttnFn(torch.autograd.Function):
             if pa > 0.0:  # q (one group over the heads), then k and v of the shared head
                 K.dropout_rows_(q, 1, pa, seed)
                 K.dropout_rows_(kv, 2, pa, seed + 3)
-            o, lse = K.attn_fwd_mqa(q, kv, B, T, H, E, tab, causal)
+            o, lse = K.attn_fwd_mqa(q, kv, B, T, H, E, tab, causal, mop)
             saved = (xb, q, kv, o, lse, w_in_b, w_kv_b, w_out_b)
         else:
             qkv = K.linear_fwd(xb, w_in_b, _f(b_in))
             if pa > 0.0:
                 K.dropout_rows_(qkv, 3, pa, seed)
-            o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal)
+            o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop)
             saved = (xb, qkv, o, lse, w_in_b, w_out_b)
         y = K.linear_fwd(o, w_out_b, _f(b_out), out_dtype=torch.float32)
         if pr > 0.0:
@@ -343,7 +348,7 @@ class _SelfAttnFn(torch.autograd.Function):
         dw_kv = db_kv = None
         if shared_kv:
             qkv_e = torch.cat([q, kv[:, :E].repeat(1, H), kv[:, E:].repeat(1, H)], dim=1).contiguous()
-            dqkv, dtab = K.attn_bwd_qkv(qkv_e, o, do, lse, B, T, H, E, tab, causal)
+            dqkv, dtab = K.attn_bwd_qkv(qkv_e, o, do, lse, B, T, H, E, tab, causal, ctx.mop)
             dq = dqkv[:, :C].contiguous()
             dkv = torch.cat([dqkv[:, C:2 * C].float().view(M, H, E).sum(1),
                              dqkv[:, 2 * C:].float().view(M, H, E).sum(1)], dim=1).contiguous()
@@ -358,7 +363,7 @@ class _SelfAttnFn(torch.autograd.Function):
             dx = K.linear_dgrad(dq, w_in_b, out_dtype=torch.float32)
             dx = K.linear_dgrad(dkvb, w_kv_b, out_dtype=torch.float32, res1=dx)
         else:
-            dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal)
+            dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal, ctx.mop)
             if pa > 0.0:
                 K.dropout_rows_(dqkv, 3, pa, seed)
             dw_in = K.linear_wgrad(dqkv, xb)
@@ -368,7 +373,7 @@ class _SelfAttnFn(torch.autograd.Function):
         if tshape is not None:
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
-        return dx.view(B, T, C), dw_in, db_in, dw_kv, db_kv, dw_out, db_out, dtable, None, None, None, None
+        return dx.view(B, T, C), dw_in, db_in, dw_kv, db_kv, dw_out, db_out, dtable, None, None, None, None, None
 
 
 class MultiHeadAttention(SelfAttention):
@@ -387,10 +392,10 @@ class MultiHeadAttention(SelfAttention):
         T = x.shape[1]
         if self.attn.table is not None:
             self.attn.pos_bias.check(T, T)
-        causal = _mask_is_causal(mask, T)
+        causal, extra = _split_mask(mask, T)
         return _SelfAttnFn.apply(x.float(), self.c_attn.weight, self.c_attn.bias, None, None, self.c_proj.weight,
                                  self.c_proj.bias, self.attn.table, self.n_head, causal, False,
-                                 _drop_args(self, self.attn_dropout.p, self.resid_dropout.p))
+                                 _drop_args(self, self.attn_dropout.p, self.resid_dropout.p), extra)
 
 
 class MultiQueryAttention(SelfAttention):
@@ -410,10 +415,11 @@ class MultiQueryAttention(SelfAttention):
         T = x.shape[1]
         if self.attn.table is not None:
             self.attn.pos_bias.check(T, T)
-        causal = _mask_is_causal(mask, T)
+        causal, extra = _split_mask(mask, T)
         return _SelfAttnFn.apply(x.float(), self.q_proj.weight, self.q_proj.bias, self.kv_proj.weight,
                                  self.kv_proj.bias, self.out_proj.weight, self.out_proj.bias, self.attn.table,
-                                 self.n_head, causal, True, _drop_args(self, self.attn_dropout.p, self.resid_dropout.p))
+                                 self.n_head, causal, True, _drop_args(self, self.attn_dropout.p, self.resid_dropout.p),
+                                 extra)
 
 
 class _MLP(nn.Module):
@@ -488,15 +494,16 @@ class TransformerBlock(nn.Module):
         a, m = self.attn, self.mlp
         return [a.c_attn.weight, a.c_proj.weight, m.c_fc.weight, m.c_proj.weight]
 
-    def _fused(self, x, double_residual: bool):
+    def _fused(self, x, double_residual: bool, attn_mask: Optional[torch.Tensor] = None):
         if x.dim() != 3:
             raise ValueError("TransformerBlock expects [B, T, d]")
         if self.is_moe:
             T = x.shape[1]
-            mask = None
+            mask = attn_mask
             if self.is_causal:
                 tri = torch.ones((T, T), dtype=torch.bool, device=x.device).tril(0)
-                mask = tri.float().masked_fill(~tri, -float("inf"))[None, None]
+                causal = tri.float().masked_fill(~tri, -float("inf"))[None, None]
+                mask = causal if mask is None else mask + causal  # :404-408
             y = x + self.attn(self.ln_1(x), mask)
             y = y + self.mlp(self.ln_2(y))
             return y + x if double_residual else y
@@ -506,17 +513,16 @@ class TransformerBlock(nn.Module):
         if drop is not None and self.mlp.dropout.p != drop[1]:
             raise NotImplementedError("the fused block applies one dropout p to the attention output and the MLP")
         with K.bf16_operands(self.gemm_weights()):
+            # a general attn_mask is added to the scores on top of the causal flag (:404-408)
             return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal,
-                                            double_residual, self.fp8_gemm, drop)
+                                            double_residual, self.fp8_gemm, drop, attn_mask)
 
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        if attn_mask is not None:
-            raise NotImplementedError("additive attn_mask: only the causal mask is fused in the kernel")
         # Activation checkpointing (:375-380) changes memory, not numbers: at 288 GB HBM
         # the fused op keeps its bf16 activations instead of recomputing them.
         if not self.is_sparse:
-            return self._fused(x, False)
-        return self._sparse_forward(x)
+            return self._fused(x, False, attn_mask)
+        return self._sparse_forward(x, attn_mask)
 
     def _null(self, x):
         from ...models.lthm.sequence.query_tower import LinearFn
@@ -525,7 +531,7 @@ class TransformerBlock(nn.Module):
                            self.null_connector.bias)
         return y.float().view(shp)
 
-    def _sparse_forward(self, x_orig: torch.Tensor) -> torch.Tensor:
+    def _sparse_forward(self, x_orig: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """:383-420: the dense block on the kept tokens (gather), the null connector on the
         others, scattered back into place."""
         T = x_orig.size(1)
@@ -533,7 +539,9 @@ class TransformerBlock(nn.Module):
         if idx.numel() <= 1:
             return x_orig + self._null(x_orig)
         not_idx = self.input_mask_not_idx[self.input_mask_not_idx < T]
-        x = self._fused(x_orig[:, idx].contiguous(), False)
+        if attn_mask is not None:  # :389-390
+            attn_mask = attn_mask[:, :, idx, :][:, :, :, idx]
+        x = self._fused(x_orig[:, idx].contiguous(), False, attn_mask)
         x_final = torch.zeros_like(x_orig)
         x_final[:, idx] = x
         if not_idx.numel():

@@ -31,7 +31,13 @@ struct AttnArgs {
   float* dtable_part;        // [B, 2T+1, H] (T' <= 256) / [parts, 2T+1, H] (windowed)
   float* delta;              // [B, H, T] workspace of the windowed backward
   int B;
+  const float* mask;         // additive [., ., T, T] or null (VALU kernels only)
+  int64_t m_bs, m_hs, m_rs;
 };
+
+__device__ __forceinline__ const float* mask_head(const AttnArgs& a, int b, int h) {
+  return a.mask ? a.mask + (int64_t)b * a.m_bs + (int64_t)h * a.m_hs : nullptr;
+}
 
 constexpr int ROWPAD = 2;  // bf16 elements of row padding (bank spread)
 
@@ -88,6 +94,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(AttnArgs a) {
   for (int i = tid; i <= 2 * T; i += 256) bias[i] = a.table ? a.table[(int64_t)i * a.H + h] : 0.f;
   __syncthreads();
   const float sq = sqrtf((float)E);
+  const float* mk = mask_head(a, b, h);
   float qr[E];
   for (int qi = wave; qi < T; qi += 4) {
     load_row_reg<E>(qr, a.q + b * a.q_bs + h * a.q_hs + (int64_t)qi * a.q_ts);
@@ -99,6 +106,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(AttnArgs a) {
       s[j] = -INFINITY;
       if (k < T && (!a.causal || k <= qi)) {
         s[j] = dot_row_reg<E>(Ks + k * (E + ROWPAD), qr) / sq + bias[qi - k + T];
+        if (mk) s[j] += mk[(int64_t)qi * a.m_rs + k];
       }
       mx = fmaxf(mx, s[j]);
     }
@@ -165,6 +173,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnArgs a) {
   }
   __syncthreads();
   const float sq = sqrtf((float)E);
+  const float* mk = mask_head(a, b, h);
   float r1[E], r2[E];
   float* dsrow = rowbuf + wave * 2 * T;
   float* prow = dsrow + T;
@@ -179,8 +188,9 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnArgs a) {
       if (k < T) {
         float ds = 0.f;
         if (!a.causal || k <= qi) {
-          const float s = dot_row_reg<E>(Ks + k * RS, r1) / sq + bias[qi - k + T];
-          const float p = __expf(s - lq);
+          const float s = dot_row_reg<E>(Ks + k * RS, r1) / sq + bias[qi - k + T] +
+                          (mk ? mk[(int64_t)qi * a.m_rs + k] : 0.f);
+          const float p = (s == -INFINITY) ? 0.f : __expf(s - lq);
           const float dp = dot_row_reg<E>(Vs + k * RS, r2);
           ds = p * (dp - dq_);
           atomicAdd(&dbias[qi - k + T], ds);
@@ -207,8 +217,9 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnArgs a) {
       if (qi < T) {
         float ds = 0.f, p = 0.f;
         if (!a.causal || ki <= qi) {
-          const float s = dot_row_reg<E>(Qs + qi * RS, r1) / sq + bias[qi - ki + T];
-          p = __expf(s - lse[qi]);
+          const float s = dot_row_reg<E>(Qs + qi * RS, r1) / sq + bias[qi - ki + T] +
+                          (mk ? mk[(int64_t)qi * a.m_rs + ki] : 0.f);
+          p = (s == -INFINITY) ? 0.f : __expf(s - lse[qi]);
           const float dp = dot_row_reg<E>(dOs + qi * RS, r2);
           ds = p * (dp - delta[qi]);
         }
@@ -1122,6 +1133,16 @@ static int attn_launch(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
 }
 
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
+  if (a.mask) {  // general additive mask: the whole-head VALU kernels
+    if (a.T > 256) return (int)hipErrorInvalidValue;
+    switch (E) {
+      case 16: return attn_launch<16>(a, B, bwd, s);
+      case 32: return attn_launch<32>(a, B, bwd, s);
+      case 64: return attn_launch<64>(a, B, bwd, s);
+      case 128: return attn_launch<128>(a, B, bwd, s);
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   if (attn_windowed(a.T)) {
     switch (E) {
       case 32: return attn_launch_win<32>(a, B, bwd, s);
@@ -1154,12 +1175,18 @@ static void fill_common(AttnArgs& a, const lthm_attn_desc* d) {
   a.dtable_part = d->dtable_part;
   a.delta = d->delta;
   a.B = d->B;
+  a.mask = d->mask;
+  a.m_bs = d->mask_batch_stride;
+  a.m_hs = d->mask_head_stride;
+  a.m_rs = d->mask_row_stride;
 }
 
 static int check_desc(const lthm_attn_desc* d) {
   if (!d || d->B < 0 || d->T <= 0 || d->T > 4096 || d->H <= 0) return 1;
   if (d->T > 256 && d->E == 16) return 1;  // the windowed path is MFMA-only (E = 32, 64, 128)
   if (d->table && d->table_rows < 2 * d->T + 1) return 1;
+  if (d->mask && (d->T > 256 || d->mask_row_stride < d->T || d->mask_batch_stride < 0 || d->mask_head_stride < 0))
+    return 1;
   if ((d->q_tok_stride % 8) || (d->k_tok_stride % 8) || (d->v_tok_stride % 8) || (d->o_tok_stride % 8)) return 1;
   // 16-B rows: LDS-DMA image staging and vector row stores
   if ((d->q_head_stride % 8) || (d->k_head_stride % 8) || (d->v_head_stride % 8) || (d->o_head_stride % 8)) return 1;

@@ -435,7 +435,24 @@ def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True
 
 
 # ----------------------------------------------------------------- attention
-def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs):
+def attn_mask_operand(mask, B, H, T):
+    """The reference's additive attn_mask (broadcast onto the [B, H, T, T] scores,
+    commons/transformers/layers.py:57-58) as an f32 operand with its broadcast
+    strides: [T, T], [B or 1, T, T] or [B or 1, H or 1, T, T]."""
+    if mask is None:
+        return None
+    require_gpu(mask)
+    m = mask.to(torch.float32)
+    while m.dim() < 4:
+        m = m.unsqueeze(0 if m.dim() != 3 else 1)
+    _check(m.dim() == 4 and tuple(m.shape[-2:]) == (T, T) and m.shape[0] in (1, B) and m.shape[1] in (1, H),
+           f"attn_mask of shape {tuple(mask.shape)} does not broadcast onto [B={B}, H={H}, T={T}, T]")
+    _check(T <= 256, "a general additive attn_mask is supported for T <= 256")
+    m = m.contiguous()
+    return m, (0 if m.shape[0] == 1 else m.stride(0)), (0 if m.shape[1] == 1 else m.stride(1)), m.stride(2)
+
+
+def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs, mask=None):
     from ._lib import STRUCTS
     _check(min(B, T, H, E) >= 1 and T <= 4096 and (T <= 256 or E in (32, 64, 128)),
            f"attention takes 1 <= T <= 4096 (E in 32/64/128 beyond T = 256; got B={B} T={T} H={H} E={E})")
@@ -454,10 +471,12 @@ def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs)
     d.table_rows = table.shape[0] if table is not None else 0
     d.lse = ptr(lse)
     d.B, d.T, d.H, d.E, d.causal = B, T, H, E, int(causal)
+    if mask is not None:  # (tensor, batch stride, head stride, row stride) from attn_mask_operand
+        d.mask, d.mask_batch_stride, d.mask_head_stride, d.mask_row_stride = ptr(mask[0]), mask[1], mask[2], mask[3]
     return d
 
 
-def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True):
+def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True, mask=None):
     """qkv bf16 [B*T, 3*H*E] (c_attn output) -> out bf16 [B*T, H*E], lse f32 [B, H, T]."""
     import ctypes
     C = H * E
@@ -466,13 +485,13 @@ def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True):
     q = qkv
     k = qkv[:, C:]
     v = qkv[:, 2 * C:]
-    d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
+    d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask)
     call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
          _unit="flop")
     return out, lse
 
 
-def attn_fwd_mqa(q, kv, B, T, H, E, table=None, causal=True):
+def attn_fwd_mqa(q, kv, B, T, H, E, table=None, causal=True, mask=None):
     """Multi-query attention forward: q bf16 [B*T, H*E], kv bf16 [B*T, 2E] (one K/V head
     shared by all query heads: head stride 0) -> out bf16 [B*T, H*E], lse f32 [B, H, T]."""
     import ctypes
@@ -481,13 +500,13 @@ def attn_fwd_mqa(q, kv, B, T, H, E, table=None, causal=True):
     _check(q.shape[-1] == C and kv.shape[-1] == 2 * E, "attn_fwd_mqa takes q [M, H*E] and kv [M, 2E]")
     out = torch.empty((B * T, C), dtype=torch.bfloat16, device=q.device)
     lse = torch.empty((B, H, T), dtype=torch.float32, device=q.device)
-    d = _attn_desc(q, kv, kv[:, E:], B, T, H, E, out, lse, table, causal, C, 2 * E, 0)
+    d = _attn_desc(q, kv, kv[:, E:], B, T, H, E, out, lse, table, causal, C, 2 * E, 0, mask)
     call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
          _unit="flop")
     return out, lse
 
 
-def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
+def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=None):
     """-> dqkv bf16 [B*T, 3C], dtable f32 [2T+1, H] (or None)."""
     import ctypes
     C = H * E
@@ -496,7 +515,7 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True):
     parts = int(load().lthm_attn_bwd_parts(B, T))
     part = torch.empty((parts, 2 * T + 1, H), dtype=torch.float32, device=qkv.device) if table is not None else None
     delta = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device) if T > 256 else None
-    d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E)
+    d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask)
     d.dout, d.dq, d.dk, d.dv = ptr(dout), ptr(dqkv), ptr(dqkv[:, C:]), ptr(dqkv[:, 2 * C:])
     d.dtable_part, d.delta = ptr(part), ptr(delta)
     call("lthm_attn_bwd", ctypes.addressof(d), stream(), _key="attn_bwd_k", _work=10.0 * B * H * T * T * E,

@@ -230,6 +230,36 @@ def gen_transformer():
     save("simhash", x=x, projection_mat=sv.projection_mat, out=sv(x))
 
 
+def gen_transformer_mask():
+    """TransformerBlock.forward(x, attn_mask) with a general additive mask
+    (commons/transformers/layers.py:374, :404-408): [B, 1, T, T] random scores plus
+    -inf on padded key columns (never a whole row), on top of the causal mask or not."""
+    from commons.transformers.layers import TransformerBlock
+    from commons.transformers.configs import TransformerConfig
+    for idx, (d, H, T, B, causal) in enumerate([(64, 2, 21, 3, True), (64, 1, 12, 2, False)]):
+        torch.manual_seed(600 + idx)
+        cfg = TransformerConfig(rotator_config={"ff_mult": 4}, is_causal=causal,
+                                attn_config=dict(attn_dropout=0.0, bias=True, dropout=0.0, n_head=H, n_embd=d,
+                                                 attn_type="multi_head", pos_bias={"context_window": 32}))
+        blk = TransformerBlock(cfg, seed=idx)
+        with torch.no_grad():
+            for n, p in blk.named_parameters():
+                if "ln_" in n or "pos_bias" in n:
+                    p.add_(0.1 * torch.randn(p.shape))
+        mask = 0.5 * torch.randn(B, 1, T, T)
+        for b in range(B):
+            mask[b, :, :, T - 1 - b:] = -float("inf")  # padded keys of sequence b
+            mask[b, :, :, 0] = 0.0                    # key 0 always visible
+        x = torch.randn(B, T, d, requires_grad=True)
+        y = blk(x, mask)
+        dy = torch.randn(y.shape)
+        (y * dy).sum().backward()
+        save(f"transformer_block_mask_{idx}", d=d, H=H, T=T, B=B, bias=1, causal=int(causal), context_window=32,
+             mask=mask, x=x.detach(), out=y.detach(), dy=dy, dx=x.grad,
+             **{f"p_{k}": v for k, v in blk.state_dict().items()},
+             **{f"g_{n}": p.grad for n, p in blk.named_parameters()})
+
+
 if __name__ == "__main__":
     if not any("reference" in p for p in sys.path + os.environ.get("PYTHONPATH", "").split(":")):
         sys.exit("run with PYTHONPATH=/root/reference (build container only)")

@@ -363,12 +363,12 @@ def test_moe_transformer_block_vs_oracle(dev, top_k):
 
 
 # ---------------------------------------------------------------- bf16-mirrored oracle
-def _block_oracle(sd, x, dy, H, causal, drop=None, dbl=False):
+def _block_oracle(sd, x, dy, H, causal, drop=None, dbl=False, attn_mask=None):
     """oracle/ref.transformer_block with bf16 rounding at the HIP path's own points
     (ref._QB / _QG): what remains is accumulation order and exp / rsqrt rounding."""
     p = {k: v.detach().cpu().float().clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
     xr = x.detach().cpu().float().clone().requires_grad_(True)
-    y = ref.transformer_block(xr, p, H, causal, drop=drop, bf16=True)
+    y = ref.transformer_block(xr, p, H, causal, attn_mask=attn_mask, drop=drop, bf16=True)
     if dbl:
         y = y + xr
     y.backward(dy.detach().cpu().float())
@@ -466,3 +466,38 @@ def test_block_dropout_vs_oracle(dev, p):
         y0 = blk(x.to(dev))
     yr0, _, _ = _block_oracle(sd, x, dy, H, True)
     check(f"dropout {p} eval fwd", relerr(y0.cpu() - x, yr0 - x), 1e-3)
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_transformer_block_attn_mask_golden(dev, idx):
+    """TransformerBlock.forward(x, attn_mask) with a general additive [B, 1, T, T] mask
+    (random scores, -inf on padded keys), causal and not (commons/transformers/layers.py:
+    374, :404-408; SDPA :57-58), vs the reference's own outputs and gradients
+    (tests/golden/transformer_block_mask_*.npz) and vs the bf16-operand oracle."""
+    from recommendations_amd.commons.transformers.layers import TransformerBlock
+    g = golden(f"transformer_block_mask_{idx}")
+    d, H, causal, pos = int(g["d"]), int(g["H"]), bool(g["causal"]), int(g["context_window"])
+    blk = TransformerBlock(_cfg(d, H, True, causal, pos)).to(dev)
+    sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("p_")}
+    blk.load_state_dict(sd)
+    mask = torch.from_numpy(g["mask"])
+    x = torch.from_numpy(g["x"]).to(dev).requires_grad_(True)
+    dy = torch.from_numpy(g["dy"])
+    y = blk(x, mask.to(dev))
+    check("masked block fwd vs reference", relerr(y.detach(), g["out"]), 2e-2)
+    yr, dxr, gr = _block_oracle(sd, x, dy, H, causal, attn_mask=mask)
+    check("masked block fwd vs bf16 oracle", relerr(y.detach() - x.detach(), yr - x.detach().cpu()), 1e-3)
+    y.backward(dy.to(dev))
+    check("masked block dx vs reference", relerr(x.grad, g["dx"]), 3e-2)
+    check("masked block dx vs bf16 oracle", relerr(x.grad, dxr), 1e-2)
+    for n, p in blk.named_parameters():
+        check(f"masked block d{n} vs reference", relerr(p.grad, g["g_" + n]), 3e-2)
+        check(f"masked block d{n} vs bf16 oracle", relerr(p.grad, gr[n]), 1e-2)
+
+
+def test_attn_mask_errors(dev):
+    from recommendations_amd import kernels as K
+    with pytest.raises(RuntimeError):  # does not broadcast onto [B, H, T, T]
+        K.attn_mask_operand(torch.zeros(3, 5, 7, device=dev), 2, 1, 7)
+    with pytest.raises(RuntimeError):  # general masks: T <= 256
+        K.attn_mask_operand(torch.zeros(300, 300, device=dev), 1, 1, 300)

@@ -102,3 +102,29 @@ def test_row_sharded_single_rank_bit_exact(dev, normalize):
         a = full(ids)
         b = sh(ids)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("normalize", [False, True])
+def test_qr_embedding_vs_oracle(dev, normalize):
+    """QREmbedding (commons/layers.py:102-123, constructor and rounding_mode fixed, SURVEY
+    §3.5 #5): Wq[(x mod d^2) // d mod d] + Wr[x mod d] (+ L2 normalise) on full-range
+    int64 ids, forward and the gradients of both tables vs the torch-CPU oracle."""
+    from recommendations_amd.commons.layers import QREmbedding
+    torch.manual_seed(5)
+    m = QREmbedding(1 << 20, 32, normalize_output=normalize)
+    Wq, Wr = m.emb_q.weight.detach().clone(), m.emb_r.weight.detach().clone()
+    m = m.to(dev)
+    ids = torch.randint(-2 ** 63, 2 ** 63 - 1, (512, 40), dtype=torch.int64)
+    ids[:, -5:] = 0
+    y = m(ids.to(dev))
+    wq, wr = Wq.clone().requires_grad_(True), Wr.clone().requires_grad_(True)
+    yr = ref.qr_fwd(ids, wq, wr, normalize)
+    if normalize:
+        np.testing.assert_allclose(y.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-6, atol=1e-7)
+    else:
+        assert torch.equal(y.detach().cpu(), yr.detach())
+    dy = torch.randn(y.shape)
+    (y * dy.to(dev)).sum().backward()
+    (yr * dy).sum().backward()
+    for got, want in ((m.emb_q.weight.grad, wq.grad), (m.emb_r.weight.grad, wr.grad)):
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-5, atol=1e-5)

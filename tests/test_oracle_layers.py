@@ -81,6 +81,21 @@ def test_transformer_block(idx):
             close(v.grad, g["g_" + k], 2e-4)
 
 
+@pytest.mark.parametrize("idx", [0, 1])
+def test_transformer_block_attn_mask(idx):
+    """TransformerBlock.forward(x, attn_mask) with a general additive mask (:374, :404-408)."""
+    g = golden(f"transformer_block_mask_{idx}")
+    p = _params(g)
+    x = T(g["x"]).clone().requires_grad_(True)
+    y = ref.transformer_block(x, p, int(g["H"]), bool(g["causal"]), attn_mask=T(g["mask"]))
+    close(y, g["out"], 1e-4)
+    y.backward(T(g["dy"]))
+    close(x.grad, g["dx"], 1e-4)
+    for k, v in p.items():
+        if v.requires_grad and "g_" + k in g.files:
+            close(v.grad, g["g_" + k], 2e-4)
+
+
 def test_mqa():
     g = golden("mqa")
     p = _params(g)
