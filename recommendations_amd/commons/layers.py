@@ -321,8 +321,8 @@ class MLP(nn.Module):
         if torch.jit.is_scripting():
             ws: List[torch.Tensor] = []
             bs: List[torch.Tensor] = []
-            for m in self.model:
-                if isinstance(m, nn.Linear):
+            for m in self.model:  # unrolled over the Sequential; QuickGELU has no weight
+                if hasattr(m, "weight"):
                     ws.append(m.weight)
                     bs.append(m.bias)
             acts = [K.ACT_QGELU] * (len(ws) - 1) + [K.ACT_NONE]

@@ -64,6 +64,8 @@ def test_c2_full_batch_step_properties(dev, c2):
     for f in (0, 31):
         Wf = tabs.gather_weight()[f * P:(f + 1) * P].float().cpu().numpy()
         wf = ref.kshift_fwd_c(batch["categorical_ids"][:, f].cpu().numpy(), Wf, tabs._num_shifts, 0)
+        # the in-order f32 pool, rounded once to the module's output dtype
+        wf = torch.from_numpy(wf).to(tabs._out_dtype or torch.float32).float().numpy()
         assert np.array_equal(cg[:, f], wf), f
     tabs.sparse_pending = 0  # the probe forward above ran outside a training step
     opts = m.optimizers_for_param_groups(m.param_groups())

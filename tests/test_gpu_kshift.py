@@ -126,5 +126,7 @@ def test_qr_embedding_vs_oracle(dev, normalize):
     dy = torch.randn(y.shape)
     (y * dy.to(dev)).sum().backward()
     (yr * dy).sum().backward()
+    # f32 scatter-adds in another order: 1e-5 of the largest row gradient
     for got, want in ((m.emb_q.weight.grad, wq.grad), (m.emb_r.weight.grad, wr.grad)):
-        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-5,
+                                   atol=1e-5 * float(want.abs().max()))

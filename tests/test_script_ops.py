@@ -83,8 +83,9 @@ def test_scripted_kshift_matches_eager(dev, normalize):
     dy = torch.randn_like(y)
     (g,) = torch.autograd.grad((y * dy).sum(), m.emb.weight)
     (gs,) = torch.autograd.grad((ys * dy).sum(), m.emb.weight)
-    # same kernel; the f32 atomic adds of duplicate rows land in any order across blocks
-    torch.testing.assert_close(gs, g, rtol=1e-6, atol=1e-7)
+    # same kernel; the f32 atomic adds of a hot row's blocks land in any order: 1e-5 of the
+    # largest row gradient (the hot rows P-1.. collect ~half of all adds)
+    torch.testing.assert_close(gs, g, rtol=1e-5, atol=1e-5 * float(g.abs().max()))
     rows = torch.ops.lthm.kshift_rows(ids, 100_003, 16)
     assert torch.equal(rows, torch.stack([m.get_row_idx(ids, c) for c in range(16)], -1))
 
@@ -105,13 +106,14 @@ def test_scripted_model_wrapper_matches_eager(dev):
         buf.seek(0)
         got2 = torch.jit.load(buf, map_location=dev)(ids)
     assert torch.equal(got, want) and torch.equal(got2, want)
-    # the fused one-kernel artifact op over the same weights (f32 arithmetic, __expf): 1e-5
+    # the fused one-kernel artifact op over the same weights: its mask MLP runs in f32, the
+    # module's MLP on bf16 MFMA operands (1e-5 vs the f32 oracle: test_gpu_embgen.py)
     mlp = w.mask_model[1].model
     fused = torch.ops.lthm.item_artifact(ids, w.model.emb.weight, 16, 1, w.mask_model[0].emb.weight, 16,
                                          mlp[0].weight, mlp[0].bias, mlp[2].weight.view(-1), mlp[2].bias,
                                          torch.float32)
     from parity import check, relerr
-    check("fused item artifact vs scripted ModelWrapper", relerr(fused, want), 1e-5)
+    check("fused item artifact vs scripted ModelWrapper", relerr(fused, want), 1e-3)
 
 
 @pytest.mark.gpu
@@ -130,4 +132,7 @@ def test_scripted_mlp_grads_match_eager(dev):
     g = torch.autograd.grad((y * dy).sum(), ps)
     gs = torch.autograd.grad((ys * dy).sum(), ps)
     for a, b in zip(g, gs):
-        assert torch.equal(a, b)
+        if a.dim() == 1:  # bias: lthm_colsum folds its row chunks with f32 atomics (any order)
+            torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-6 * float(a.abs().max()))
+        else:  # dgrad / split-K wgrad: fixed summation order
+            assert torch.equal(a, b)
