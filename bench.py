@@ -99,7 +99,15 @@ def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=10):
         del out
     del W
     res["achieved"], res["frac"] = res["spread_ids"]["achieved"], res["spread_ids"]["frac"]
-    res["traffic_source"] = "profiles/r02_gather_pmc.txt (tools/gather_bench.py under rocprofv3 --pmc)"
+    try:  # HBM bytes per launch from the committed counter passes (tools/pmc_gather.sh)
+        with open(os.path.join(ROOT, "profiles", "r02_gather_pmc.json")) as f:
+            pmc = json.load(f)
+        for name in ("spread_ids", "reference_ids"):
+            res[name]["traffic"] = pmc[name]["hbm_bytes"]
+        res["traffic"] = pmc["spread_ids"]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        res["traffic"] = None
+    res["traffic_source"] = "profiles/r02_gather_pmc.json (tools/pmc_gather.sh: rocprofv3 --pmc over tools/gather_bench.py)"
     return res
 
 
