@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 18 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 19 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -171,6 +171,20 @@ int lthm_gemm(const lthm_gemm_desc* desc, void* stream);
  * (n % 8 == 0, 16-B aligned); q: n bytes; scale: device f32; work: 4-byte scratch. */
 int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_t* q, float* scale, int32_t* work,
                       void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Fused encoder MLP: _MLP.forward, commons/transformers/layers.py:279-284      */
+/* (c_fc -> GELU(tanh) -> c_proj, dropout 0) with the [M, HID] hidden kept on   */
+/* chip.  x: ln_2 output bf16 [M, D]; W1 = c_fc.weight bf16 [HID, D];           */
+/* W2T = c_proj.weight^T bf16 [HID, D]; biases f32 (NULL for bias=False).        */
+/* Supported shapes: lthm_mlp_supported(D, HID) (D 128 or 256, HID % 32 == 0).  */
+/* ------------------------------------------------------------------------- */
+int lthm_mlp_supported(int32_t D, int32_t HID);
+/* out f32 [M, D] = res1 [+ res2] + c_proj(GELU(c_fc(x))); res1 / res2 f32 [M, D] or NULL
+ * (replaces TransformerBlock's x + mlp(ln_2 x), commons/transformers/layers.py:371). */
+int lthm_mlp_fwd(const void* x, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
+                 const void* W2T, const float* b2, const float* res1, const float* res2, float* out,
+                 void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm (commons/transformers/layers.py:142-149, eps 1e-5)               */

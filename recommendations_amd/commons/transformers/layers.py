@@ -85,7 +85,7 @@ class TransformerBlockFn(torch.autograd.Function):
 
     @staticmethod
     def _forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal,
-                 double_residual, fp8=False, drop=None, mask=None):
+                 double_residual, fp8=False, drop=None, mask=None, infer=False):
         require_gpu(x)
         B, T, d = x.shape
         E = d // H
@@ -115,6 +115,11 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+        if infer and not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]):
+            # inference (no backward will run): the fused MLP keeps the [M, 4d] hidden on chip
+            out = K.mlp_fwd(h2, w1_b, _f(b1), w2_b.t().contiguous(), _f(b2), res1=x1,
+                            res2=x2 if double_residual else None)
+            return out.view(B, T, d)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
         g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre)
@@ -175,7 +180,7 @@ class TransformerBlockFn(torch.autograd.Function):
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
         return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
-                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None, None)
+                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None, None, None)
 
 
 # ------------------------------------------------------------------ modules
@@ -512,10 +517,14 @@ class TransformerBlock(nn.Module):
         drop = _drop_args(self, self.attn.attn_dropout.p, self.attn.resid_dropout.p)
         if drop is not None and self.mlp.dropout.p != drop[1]:
             raise NotImplementedError("the fused block applies one dropout p to the attention output and the MLP")
+        args = self._args()
+        # no backward can run: the forward may keep intermediates on chip (fused MLP)
+        infer = not (torch.is_grad_enabled() and (x.requires_grad or any(
+            a is not None and a.requires_grad for a in args)))
         with K.bf16_operands(self.gemm_weights()):
             # a general attn_mask is added to the scores on top of the causal flag (:404-408)
-            return TransformerBlockFn.apply(x.float(), *self._args(), self.attn.n_head, self.is_causal,
-                                            double_residual, self.fp8_gemm, drop, attn_mask)
+            return TransformerBlockFn.apply(x.float(), *args, self.attn.n_head, self.is_causal,
+                                            double_residual, self.fp8_gemm, drop, attn_mask, infer)
 
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         # Activation checkpointing (:375-380) changes memory, not numbers: at 288 GB HBM

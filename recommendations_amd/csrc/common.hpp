@@ -125,6 +125,38 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
   }
 }
 
+// ---- activations (GEMM epilogues, fused MLP) ----
+// tanh-GELU through r = 1 / (e^(2u) + 1), u = sqrt(2/pi) (x + 0.044715 x^3):
+// tanh(u) = 1 - 2r, so gelu(x) = 0.5 x (1 + tanh u) = x (1 - r) and
+// gelu'(x) = (1 - r) (1 + 2 sqrt(2/pi) x r (1 + 3 * 0.044715 x^2)).
+// One v_exp + one v_rcp per element (|error| ~ 1e-7 absolute); saturates
+// correctly for large |x| (exp2 -> inf gives r = 0, exp2 -> 0 gives r = 1).
+__device__ __forceinline__ float gelu_r(float x) {
+  constexpr float kb2 = 2.f * 1.4426950408889634f * 0.7978845608028654f;   // 2 log2(e) sqrt(2/pi)
+  constexpr float kk2 = kb2 * 0.044715f;
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * __builtin_fmaf(kk2, x * x, kb2)) + 1.f);
+}
+__device__ __forceinline__ float gelu_tanh(float x) { return __builtin_fmaf(-x, gelu_r(x), x); }
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  constexpr float kb = 0.7978845608028654f, k3 = 3.f * 0.044715f;
+  const float r = gelu_r(x);
+  return (1.f - r) * __builtin_fmaf(2.f * kb * x * r, __builtin_fmaf(k3, x * x, 1.f), 1.f);
+}
+// gelu(x) and gelu'(x) from one v_exp + one v_rcp (the forward that saves the
+// derivative for the backward's plain multiply, LTHM_ACT_GELU_D)
+__device__ __forceinline__ float gelu_tanh_and_grad(float x, float& dg) {
+  constexpr float kb = 0.7978845608028654f, k3 = 3.f * 0.044715f;
+  const float r = gelu_r(x), q = 1.f - r;
+  dg = q * __builtin_fmaf(2.f * kb * x * r, __builtin_fmaf(k3, x * x, 1.f), 1.f);
+  return x * q;
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float qgelu(float x) { return x * sigmoidf_(1.702f * x); }
+__device__ __forceinline__ float qgelu_grad(float x) {
+  const float s = sigmoidf_(1.702f * x);
+  return s + 1.702f * x * s * (1.f - s);
+}
+
 // ---- wave reductions (64 lanes) ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

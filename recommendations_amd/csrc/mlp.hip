@@ -1,0 +1,302 @@
+// Fused encoder MLP for gfx950: _MLP (commons/transformers/layers.py:279-284)
+//
+//   out = res1 [+ res2] + c_proj( GELU( c_fc(x) ) )      x = ln_2 output, bf16
+//
+// with the [M, 4d] hidden never written to HBM.  The forward keeps it in
+// registers; the backward recomputes it (two kernels, below).  All three kernels
+// share one structure:
+//
+//  * v_mfma_f32_32x32x16_bf16 throughout; a wave owns 32 token rows (dX-style
+//    kernels) or 32 hidden units (the weight-gradient kernel);
+//  * the hidden dimension is walked in chunks of 32 units.  A chunk's first
+//    product is computed TRANSPOSED (pre^T = W1_j . x^T: hidden on the
+//    accumulator's registers, token rows on its lanes), so the accumulator,
+//    packed to bf16, is directly the A operand of the second product, which sums
+//    over the hidden index (cdna_hip_programming.md §3, accumulator as operand):
+//    no LDS round trip, no transpose;
+//  * the weights stream through LDS in [32 x d] chunk images (c_fc.weight rows
+//    and c_proj.weight^T rows, both contiguous 32 x d blocks), double-buffered
+//    by LDS-DMA (global_load_lds_dwordx4), one barrier per chunk.  The same
+//    image serves row reads (ds_read_b128: the chunk as an A operand over d) and
+//    transposed reads (ds_read_b64_tr_b16: the chunk as a B operand over the
+//    permuted hidden index of the packed accumulator); the XOR swizzle
+//    ch ^ ((r & 3) << 2 | (r >> 2) & 3) makes both conflict-free.
+//
+// Per token row and layer the forward moves x (2d B), res1 (4d B) and out (4d B)
+// instead of the unfused chain's 4d-wide bf16 hidden + GELU' aux writes and their
+// re-reads (2 x 2 x 4d B written, read twice more in the backward).
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace lthm {
+
+struct MlpArgs {
+  const bf16_t* X;    // [M, D] ln_2 output (bf16)
+  const bf16_t* W1;   // [HID, D] c_fc.weight (bf16)
+  const bf16_t* W2T;  // [HID, D] c_proj.weight^T (bf16)
+  const float* b1;    // [HID] or null
+  const float* b2;    // [D] or null
+  const float* res1;  // [M, D] f32 or null
+  const float* res2;  // [M, D] f32 or null
+  float* out;         // [M, D] f32
+  int64_t M;
+  int HID;
+  int ntiles;
+};
+
+typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
+typedef short s16x4m __attribute__((ext_vector_type(4)));
+typedef short s16x8m __attribute__((ext_vector_type(8)));
+
+// [rows][D] bf16 images as 8-row x 32-column subtiles of 512 B (cdna_hip_programming.md T10,
+// layout (a)): byte offset of 16-B chunk c (8 columns) of row r.  Every offset is a per-lane
+// base plus a multiple of 512 in the chunk's high bits, so an unrolled loop over k-steps or
+// output tiles needs two base registers, not one per read.  Conflict-free for the 32x32x16
+// row reads (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16) alike.
+template <int D>
+__device__ __forceinline__ int mlp_off(int r, int c) {
+  return (16 * D) * (r >> 3) + 512 * (c >> 2) + 64 * (r & 7) + 16 * ((c & 3) ^ ((r >> 2) & 3));
+}
+
+// LDS-DMA of a [32 x D] bf16 block (rows contiguous, row stride D) into a mlp_off image:
+// the DMA writes 16-B slot base + lane of each wave-instruction, so the layout is applied
+// to the source address (slot -> row, chunk by inverting mlp_off).
+template <int D, int NTH>
+__device__ __forceinline__ void mlp_dma32(unsigned char* img, const bf16_t* P, int tid) {
+  constexpr int SLOTS = 32 * D / 8;
+  static_assert(SLOTS % NTH == 0, "image slots must divide over the workgroup");
+  const int wbase = tid & ~63;
+#pragma unroll
+  for (int m = 0; m < SLOTS / NTH; ++m) {
+    const int o = (m * NTH + tid) * 16;
+    const int r1 = o % (16 * D);
+    const int r = 8 * (o / (16 * D)) + (r1 % 512) / 64;
+    const int c = 4 * (r1 / 512) + (((r1 % 64) / 16) ^ ((r >> 2) & 3));
+    glds16(P + (int64_t)r * D + c * 8, img + (m * NTH + wbase) * 16);
+  }
+}
+
+// A operand of 32x32x16 from a [32][D] image: lane (r = l & 31, h = l >> 5) row r, k 16 ks + 8 h ..
+template <int D>
+__device__ __forceinline__ bf16x8m mlp_row_frag(const unsigned char* img, int lane, int ks) {
+  return *reinterpret_cast<const bf16x8m*>(img + mlp_off<D>(lane & 31, 2 * ks + (lane >> 5)));
+}
+
+// B operand of 32x32x16 over the PERMUTED k order of a packed accumulator (k-step s2 of a
+// 32-row block of the image, output columns 32 t ..): element e of lane half h is image row
+// 16 s2 + 8 (e >> 2) + 4 h + (e & 3), column 32 t + (lane & 31) -- two transposed reads.
+template <int D>
+__device__ __forceinline__ bf16x8m mlp_tr_frag(const unsigned char* img, int lane, int s2, int t) {
+  const int h = lane >> 5, q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  const int c = 4 * t + 2 * g1 + (p >> 1);
+  const int r0 = 16 * s2 + 4 * h + q;
+  typedef __attribute__((address_space(3))) s16x4m lds_s16x4;
+  const s16x4m lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mlp_off<D>(r0, c) + 8 * (p & 1)));
+  const s16x4m hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mlp_off<D>(r0 + 8, c) + 8 * (p & 1)));
+  const s16x8m v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8m, v);
+}
+
+// registers 8 s .. 8 s + 7 of a 32x32 accumulator, packed to bf16: the k-step s fragment
+__device__ __forceinline__ bf16x8m mlp_pack(const float* v) {
+  u32x4 w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+  return __builtin_bit_cast(bf16x8m, w);
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8m a, bf16x8m b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------- forward
+// Workgroup = NW waves, persistent over a contiguous range of token rows, in tiles of 32 NW
+// rows (a wave owns 32).  The hidden chunks of consecutive tiles form ONE stream c = 0, 1, ...
+// (chunk c % NC of the WG's tile c / NC); step c of the software pipeline is
+//   S'  = W1_{c+1} . x^T            phase 1 of the NEXT chunk (A: W1 image rows; B: x in registers)
+//   Hp  = bf16(GELU(S + b1_c))      issued between those MFMAs (independent VALU)
+//   Y  += Hp . W2T_c                phase 2 of this chunk (B: W2T image, transposed reads)
+// W1 and W2T images ride separate 2-slot rings: step c consumes W2T_c and W1_{c+1} and its
+// LDS-DMAs fetch W2T_{c+1} and W1_{c+2} into the slots step c - 1 released; one barrier per
+// step.  The residual (+ b2) is loaded INTO the accumulator when a tile starts, so the
+// epilogue only stores (LDS-restaged 16-B rows, no load after a store on the in-order vmcnt);
+// the next tile's x rows are loaded one step before the tile's last phase 1 needs them.
+// out[row, :] = acc + b2 + res1 [+ res2] for the wave's rows rb .. min(rb + 32, lim): each
+// 32-column tile t of the accumulator goes through the wave's 4-KiB LDS strip (C layout in,
+// 128-B rows out), then every lane finishes four 16-B pieces with vector loads / stores; the
+// residual pieces of tile t are loaded before the tile is restaged.
+template <int D, int NT, int NRES>
+__device__ __forceinline__ void mlp_fwd_epi(const MlpArgs& a, const f32x16 (&acc)[NT], const float* b2s,
+                                            float* stg, int64_t rb, int64_t lim, int lane) {
+  const int r32 = lane & 31, h = lane >> 5;
+  const int pr = lane >> 3, pc = 4 * (lane & 7);  // piece m: row pr + 8 m, columns pc .. pc + 3
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f32x4 rv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // in flight while the tile is restaged
+      const int64_t o = min(rb + pr + 8 * m, lim - 1) * D + 32 * t + pc;
+      rv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (NRES >= 1) rv[m] = *reinterpret_cast<const f32x4*>(a.res1 + o);
+      if constexpr (NRES >= 2) rv[m] += *reinterpret_cast<const f32x4*>(a.res2 + o);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) stg[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r32] = acc[t][i];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(b2s + 32 * t + pc);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t row = rb + pr + 8 * m;
+      f32x4 v = *reinterpret_cast<const f32x4*>(stg + (pr + 8 * m) * 32 + pc);
+      v += bias + rv[m];
+      if (row < lim) *reinterpret_cast<f32x4*>(a.out + row * D + 32 * t + pc) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+template <int D, int KS>
+__device__ __forceinline__ void mlp_load_x(const bf16_t* X, int64_t row, bool ok, int h, bf16x8m (&xf)[KS]) {
+  const bf16_t* p = X + (ok ? row : 0) * D + 8 * h;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    xf[s] = __builtin_bit_cast(bf16x8m, ok ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0u, 0u, 0u, 0u});
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
+  constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave epilogue strips
+  extern __shared__ float b1s[];                                         // [HID] b1, then [D] b2
+  float* b2s = b1s + a.HID;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  for (int i = tid; i < D; i += NTH) b2s[i] = a.b2 ? a.b2[i] : 0.f;
+  float* stg = stg_all[wave];
+  retire_loads();
+  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
+  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  __syncthreads();  // b1s / b2s
+  int g = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform: a wave past the tile's rows only streams weights
+    bf16x8m xf[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    const bool more_tiles = t0 + TR < re;
+    for (int j = 0; j < NC; ++j, ++g) {
+      wait_vm<0>();
+      __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
+      asm volatile("" ::: "memory");
+      if (j + 1 < NC || more_tiles) {
+        const int jn = j + 1 < NC ? j + 1 : 0;
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      }
+      if (!active) continue;
+      const unsigned char* w1 = img[g & 1][0];
+      const unsigned char* w2 = img[g & 1][1];
+      // LDS reads one step ahead of their MFMA; the compiler fences keep the unrolled loops
+      // from hoisting every read (register pressure: 2 waves per SIMD)
+      f32x16 S = f32x16{};
+      bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const bf16x8m fn = mlp_row_frag<D>(w1, lane, k + 1 < KS ? k + 1 : k);
+        S = mfma32(fa, xf[k], S);
+        fa = fn;
+        asm volatile("" ::: "memory");
+      }
+      float hv[16];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[4 * m + e] = gelu_tanh(S[4 * m + e] + bb[e]);
+      }
+      const bf16x8m hf0 = mlp_pack(hv), hf1 = mlp_pack(hv + 8);
+      bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int tn = t + 1 < NT ? t + 1 : t;
+        const bf16x8m n0 = mlp_tr_frag<D>(w2, lane, 0, tn), n1 = mlp_tr_frag<D>(w2, lane, 1, tn);
+        acc[t] = mfma32(hf0, b0, acc[t]);
+        acc[t] = mfma32(hf1, b1, acc[t]);
+        b0 = n0;
+        b1 = n1;
+        asm volatile("" ::: "memory");
+      }
+    }
+    if (active) {
+      if (a.res1 && a.res2) mlp_fwd_epi<D, NT, 2>(a, acc, b2s, stg, rb, lim, lane);
+      else if (a.res1) mlp_fwd_epi<D, NT, 1>(a, acc, b2s, stg, rb, lim, lane);
+      else mlp_fwd_epi<D, NT, 0>(a, acc, b2s, stg, rb, lim, lane);
+    }
+  }
+}
+
+}  // namespace lthm
+
+using namespace lthm;
+
+static int mlp_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// waves per forward workgroup: 8 (one workgroup per CU, 256-row tiles) or 4 (two per CU);
+// LTHM_MLP_NW overrides (measurement)
+static int mlp_fwd_waves() {
+  static int nw = 0;
+  if (nw == 0) {
+    const char* e = getenv("LTHM_MLP_NW");
+    nw = (e && e[0] == '4') ? 4 : 8;
+  }
+  return nw;
+}
+
+extern "C" int lthm_mlp_supported(int32_t D, int32_t HID) {
+  return (D == 128 || D == 256) && HID >= 32 && HID % 32 == 0 && HID <= 8192;
+}
+
+extern "C" int lthm_mlp_fwd(const void* X, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
+                            const void* W2T, const float* b2, const float* res1, const float* res2, float* out,
+                            void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && M >= 0);
+  LTHM_REQUIRE(X && W1 && W2T && out);
+  LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)W1 % 16) == 0 && ((uintptr_t)W2T % 16) == 0 &&
+               ((uintptr_t)b1 % 16) == 0);
+  if (M == 0) return 0;
+  MlpArgs a;
+  a.X = (const bf16_t*)X; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1; a.b2 = b2; a.res1 = res1; a.res2 = res2; a.out = out;
+  a.M = M; a.HID = HID;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t dyn = (size_t)(HID + D) * 4;
+  const int nw = mlp_fwd_waves();
+  a.ntiles = (int)((M + 32 * nw - 1) / (32 * nw));
+  const int per_cu = 1;
+  int grid = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count() * per_cu);
+#define LTHM_MLPF(D_, NW_) hipLaunchKernelGGL((mlp_fwd_k<D_, NW_>), dim3(grid), dim3(64 * NW_), dyn, s, a)
+  if (D == 256) { if (nw == 8) LTHM_MLPF(256, 8); else LTHM_MLPF(256, 4); }
+  else { if (nw == 8) LTHM_MLPF(128, 8); else LTHM_MLPF(128, 4); }
+#undef LTHM_MLPF
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -402,6 +402,36 @@ def linear_wgrad(dy2d, x2d, out=None, accumulate=False):
                 out_dtype=torch.float32, res1=res, splits=s)
 
 
+# ----------------------------------------------------------------- fused MLP
+def mlp_supported(D: int, HID: int) -> bool:
+    """Shapes the fused MLP kernels take (include/lthm.h lthm_mlp_supported)."""
+    from ._lib import load
+    return bool(load().lthm_mlp_supported(D, HID))
+
+
+def mlp_fwd(x2d, w1_b, b1, w2t_b, b2, res1=None, res2=None):
+    """res1 [+ res2] + c_proj(GELU(c_fc(x))) in one kernel, hidden on chip (lthm_mlp_fwd).
+    x2d [M, D] bf16, w1_b [HID, D] bf16 (c_fc.weight), w2t_b [HID, D] bf16 (c_proj.weight^T)."""
+    require_gpu(x2d, w1_b, w2t_b)
+    M, D = x2d.shape
+    HID = w1_b.shape[0]
+    _check(x2d.dtype == torch.bfloat16 and w1_b.dtype == torch.bfloat16 and w2t_b.dtype == torch.bfloat16,
+           "mlp_fwd takes bf16 x / weights")
+    _check(mlp_supported(D, HID), f"fused MLP does not take D={D} HID={HID}")
+    _check(tuple(w1_b.shape) == (HID, D) and tuple(w2t_b.shape) == (HID, D), "mlp_fwd: weight shapes")
+    for t in (x2d, w1_b, w2t_b, b1, b2, res1, res2):
+        _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_fwd: contiguous 16-B aligned operands")
+    for t, n in ((b1, HID), (b2, D)):
+        _check(t is None or (t.dtype == torch.float32 and t.numel() == n), "mlp_fwd: f32 biases")
+    for t in (res1, res2):
+        _check(t is None or (t.dtype == torch.float32 and t.numel() == M * D), "mlp_fwd: f32 [M, D] residuals")
+    out = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
+    call("lthm_mlp_fwd", ptr(x2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(b2), ptr(res1), ptr(res2),
+         ptr(out), stream(), _key=(_GEMM_TAG[-1] + ":mlp_fwd") if _GEMM_TAG else "mlp_fwd",
+         _work=4.0 * M * D * HID, _unit="flop")
+    return out
+
+
 # ----------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
     require_gpu(x2d, w)
