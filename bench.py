@@ -260,6 +260,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-hbm-gather", action="store_true", help="skip the 1 GB-table embedding roofline")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="form the process group, print the world size it reports and exit (launcher test)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -275,6 +277,16 @@ def main():
     reported = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     if world != args.gpus or reported != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} and the process group has {reported} ranks")
+    if args.check_launch:
+        if world > 1:
+            t = torch.ones(1)
+            torch.distributed.all_reduce(t)  # every rank joined the group
+            if rank == 0:
+                print(json.dumps({"world": reported, "backend": torch.distributed.get_backend(), "sum": float(t)}))
+            torch.distributed.destroy_process_group()
+        else:
+            print(json.dumps({"world": 1, "backend": None, "sum": 1.0}))
+        return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cfgd = dict(CONFIGS[args.config])
@@ -287,7 +299,9 @@ def main():
         if ranker:
             model._model.cat_tables.replicated_dp = True
         elif model._model.user_context is not None:
-            model._model.user_context.tables.replicated_dp = True
+            # table-wise sharding of the categorical tables (all_to_all routing, no xworld
+            # growth of the sparse backward / optimizer); before the optimizers are built
+            model._model.user_context.shard_tables(rank, world)
     opts = model.optimizers_for_param_groups(model.param_groups())
     dense_params = [p for n, p in model.named_parameters() if p.requires_grad and not model.is_sparse(n)]
     allreduce = GradBucketAllReduce(dense_params)
@@ -371,9 +385,11 @@ def main():
                                 + (f", {cfgd['mbs']}-sequence loss mini-batches" if cfgd.get("mbs") else "")),
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
                    "parallelism": f"dp{world}" + (
-                       (" (item table row-sharded, all_to_all row exchange; categorical tables replicated, "
-                        "gathered row updates)" if cfgd.get("item_table_sharded") else
-                        " (replicated KShift tables, gathered row updates)") if world > 1 else "")},
+                       (" (item table row-sharded, all_to_all row exchange; categorical tables table-wise "
+                        "sharded, all_to_all id / row / gradient routing; dense grads bucketed all-reduce "
+                        "overlapped with the backward)" if cfgd.get("item_table_sharded") else
+                        " (categorical tables table-wise sharded, all_to_all id / row / gradient routing; dense "
+                        "grads bucketed all-reduce overlapped with the backward)") if world > 1 else "")},
         "final_loss": round(float(loss), 5),
     }
     if timer is not None:

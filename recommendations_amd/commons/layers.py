@@ -168,6 +168,33 @@ class _ZeroRowGrad(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------ sparse (row-wise) KShift
+def _kshift_fwd_local(mod, ids, gather_w):
+    """The row-wise-trained tables' forward kernel (lthm_kshift_fwd_multi): ids [..., F]
+    over mod's F tables -> (out [..., F, D], norms or None)."""
+    from .._lib import call, dcode, ptr, require_gpu, stream
+    require_gpu(ids, gather_w)
+    F_, P, Kk, mode = mod._F, mod._num_embeddings, mod._num_shifts, mod._mode
+    D = gather_w.shape[1]
+    K._check_kshift(ids, P, Kk, F_, D, table_rows=gather_w.shape[0])
+    out_dtype = mod._out_dtype or torch.float32
+    out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
+    norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if mode == K.KSHIFT_NORMALIZE else None
+    call("lthm_kshift_fwd_multi", ptr(ids), ids.numel() // F_, F_, ptr(gather_w), dcode(gather_w), P, D, Kk, mode,
+         ptr(out), dcode(out), ptr(norms), stream(), _key="kshift_fwd_k",
+         _work=ids.numel() * (8 + Kk * D * gather_w.element_size() + D * out.element_size()), _unit="byte")
+    return out, norms
+
+
+def _kshift_bwd_local(mod, ids, gy, out, norms):
+    """Accumulate the pooled gradient gy of ids into mod's persistent row gradient and
+    touched-row list (lthm_kshift_bwd_sparse)."""
+    mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
+    K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
+                        mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,
+                        pending=mod.sparse_pending)
+    mod.sparse_pending += ids.numel() * mod._num_shifts
+
+
 class _SparseKShiftFn(torch.autograd.Function):
     """Forward as K.KShiftFn; backward accumulates into the module's persistent
     dense f32 gradient and appends the touched rows for the row-wise optimizer
@@ -175,19 +202,9 @@ class _SparseKShiftFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ids, weight, mod, gather_w):
-        from .._lib import call, dcode, ptr, require_gpu, stream
-        require_gpu(ids, weight)
-        F_, P, Kk, mode = mod._F, mod._num_embeddings, mod._num_shifts, mod._mode
-        D = weight.shape[1]
-        K._check_kshift(ids, P, Kk, F_, D, table_rows=gather_w.shape[0])
-        out_dtype = mod._out_dtype or torch.float32
-        out = torch.empty(ids.shape + (D,), dtype=out_dtype, device=ids.device)
-        norms = torch.empty(ids.shape, dtype=torch.float32, device=ids.device) if mode == K.KSHIFT_NORMALIZE else None
-        call("lthm_kshift_fwd_multi", ptr(ids), ids.numel() // F_, F_, ptr(gather_w), dcode(gather_w), P, D, Kk, mode,
-             ptr(out), dcode(out), ptr(norms), stream(), _key="kshift_fwd_k",
-             _work=ids.numel() * (8 + Kk * D * gather_w.element_size() + D * out.element_size()), _unit="byte")
+        out, norms = _kshift_fwd_local(mod, ids, gather_w)
         ctx.mod = mod
-        ctx.save_for_backward(ids, out if mode == K.KSHIFT_NORMALIZE else None, norms)
+        ctx.save_for_backward(ids, out if mod._mode == K.KSHIFT_NORMALIZE else None, norms)
         return out
 
     @staticmethod
@@ -200,11 +217,49 @@ class _SparseKShiftFn(torch.autograd.Function):
             # (1/world-scaled) updates, so the replicas stay identical
             from ..distributed import gather_sparse_grads
             ids, gy, out, norms = gather_sparse_grads(ids, gy, out, norms)
-        mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
-        K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
-                            mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,
-                            pending=mod.sparse_pending)
-        mod.sparse_pending += ids.numel() * mod._num_shifts
+        _kshift_bwd_local(mod, ids, gy, out, norms)
+        return None, None, None, None
+
+
+class _TableShardedFn(torch.autograd.Function):
+    """Routing of TableShardedKShiftEmbedding: ids to the tables' owners, pooled rows
+    back (forward); pooled gradients to the owners (backward).  Every split size is a
+    function of (B, F, world) alone, so no count exchange and no host sync."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, mod, gather_w):
+        import torch.distributed as dist
+        B, F = ids.shape
+        W, fl = mod._world, mod._F
+        Fo = mod._owned  # tables per owner
+        ids_t = ids.t().contiguous()  # [F, B]: owner r's tables are rows [bounds[r], bounds[r+1])
+        recv = torch.empty(W * fl * B, dtype=torch.int64, device=ids.device)
+        dist.all_to_all_single(recv, ids_t.view(-1), [fl * B] * W, [n * B for n in Fo])
+        local_ids = recv.view(W, fl, B).permute(0, 2, 1).reshape(W * B, fl).contiguous()  # [W*B, F_loc]
+        out_local, norms = _kshift_fwd_local(mod, local_ids, gather_w)                      # [W*B, F_loc, D]
+        D = out_local.shape[-1]
+        back = torch.empty(B * F * D, dtype=out_local.dtype, device=ids.device)
+        dist.all_to_all_single(back, out_local.view(-1), [n * B * D for n in Fo], [fl * B * D] * W)
+        blocks = torch.split(back, [n * B * D for n in Fo])
+        out = torch.cat([b.view(B, n, D) for b, n in zip(blocks, Fo)], dim=1)  # [B, F, D]
+        ctx.mod = mod
+        ctx.shape = (B, F, D)
+        ctx.save_for_backward(local_ids, out_local if mod._mode == K.KSHIFT_NORMALIZE else None, norms)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        import torch.distributed as dist
+        local_ids, out_local, norms = ctx.saved_tensors
+        mod = ctx.mod
+        B, F, D = ctx.shape
+        W, fl, Fo, bnd = mod._world, mod._F, mod._owned, mod._bounds
+        send = torch.cat([gy[:, bnd[r]:bnd[r + 1], :].reshape(-1) for r in range(W)])
+        recv = torch.empty(W * B * fl * D, dtype=gy.dtype, device=gy.device)
+        dist.all_to_all_single(recv, send, [fl * B * D] * W, [n * B * D for n in Fo])
+        g_local = recv.view(W * B, fl, D)
+        g_local = g_local * (1.0 / W) if g_local.dtype == torch.float32 else (g_local.float() * (1.0 / W)).to(gy.dtype)
+        _kshift_bwd_local(mod, local_ids, g_local.contiguous(), out_local, norms)
         return None, None, None, None
 
 
@@ -234,6 +289,41 @@ class TableBatchedKShiftEmbedding(_SparseRowsMixin, nn.Module):
             return _SparseKShiftFn.apply(ids, self.weight, self, self.gather_weight())
         return K.kshift(ids, self.weight, self._num_embeddings, self._num_shifts, self._mode, F=self._F,
                         out_dtype=self._out_dtype or self.weight.dtype)
+
+
+class TableShardedKShiftEmbedding(TableBatchedKShiftEmbedding):
+    """Table-wise model parallelism for the F table-batched, row-wise-trained KShift
+    tables under data parallelism (the TorchRec/DLRM "table-wise" plan):
+    rank r owns tables [F r / W, F (r + 1) / W) -- their fp32 master, gradient and
+    optimizer state.  Forward: all_to_all of every rank's ids to the owners, the owner
+    pools its tables for all W x B ids (one table-batched lookup), all_to_all of the
+    pooled rows back.  Backward: all_to_all of the pooled gradients to the owners, which
+    apply them at 1/W (the rank-averaged loss, as GradBucketAllReduce averages the
+    dense gradients).  A rank computes and stores F/W tables for W B ids -- the same
+    F B lookups one replica does at world 1 -- where replication (``replicated_dp``)
+    grows the sparse backward and optimizer by W.  Every rank must call forward with
+    the same batch size."""
+
+    def __init__(self, full: TableBatchedKShiftEmbedding, rank: int, world: int):
+        nn.Module.__init__(self)
+        F, P = full._F, full._num_embeddings
+        self._bounds = [F * r // world for r in range(world + 1)]
+        self._owned = [self._bounds[r + 1] - self._bounds[r] for r in range(world)]
+        self._rank, self._world, self._F_total = rank, world, F
+        self._F = self._owned[rank]
+        if self._F == 0:
+            raise ValueError(f"{F} tables over {world} ranks leave rank {rank} without a table")
+        self._num_embeddings, self._num_shifts, self._mode = P, full._num_shifts, full._mode
+        self._out_dtype, self._gather_dtype = full._out_dtype, full._gather_dtype
+        f0, f1 = self._bounds[rank], self._bounds[rank + 1]
+        self.weight = nn.Parameter(full.weight.detach()[f0 * P:f1 * P].clone(), requires_grad=full.weight.requires_grad)
+        self.sparse = True
+        self._init_sparse_state()
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        if ids.dim() != 2 or ids.shape[1] != self._F_total:
+            raise ValueError(f"ids must be [B, {self._F_total}]")
+        return _TableShardedFn.apply(ids.contiguous(), self.weight, self, self.gather_weight())
 
 
 class RowShardedKShiftEmbedding(nn.Module):

@@ -42,35 +42,69 @@ def world_size() -> int:
 
 
 class GradBucketAllReduce:
-    """Average dense gradients across ranks with a few large flat all-reduces."""
+    """Average dense gradients across ranks with a few large flat all-reduces,
+    overlapped with the backward.
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 64 << 20):
+    Parameters are dealt into ~``bucket_bytes`` buckets in reverse registration order
+    (roughly the order the backward produces their gradients).  A post-accumulate-grad
+    hook counts each bucket's ready gradients; the moment the last one lands, the bucket
+    is flattened into its persistent buffer and its all-reduce is launched asynchronously
+    (RCCL runs it on its own stream while the backward's kernels continue).  ``__call__``
+    (after ``loss.backward()``) launches any bucket whose parameters received no gradient
+    this step, waits for every all-reduce and writes the averages back."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 64 << 20, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.bucket_bytes = bucket_bytes
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur: List[torch.nn.Parameter] = []
+        size = 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self._bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self._ready = [0] * len(self.buckets)
+        self._work: List[Optional[tuple]] = [None] * len(self.buckets)
+        self._hooks = []
+        if overlap and world_size() > 1 and hasattr(torch.Tensor, "register_post_accumulate_grad_hook"):
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p: torch.Tensor) -> None:
+        i = self._bucket_of[id(p)]
+        self._ready[i] += 1
+        if self._ready[i] == len(self.buckets[i]) and self._work[i] is None:
+            self._launch(i)
+
+    def _launch(self, i: int) -> None:
+        grads = [p.grad for p in self.buckets[i] if p.grad is not None]
+        if not grads:
+            self._work[i] = ()
+            return
+        flat = torch._utils._flatten_dense_tensors(grads)
+        self._work[i] = (flat, grads, dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True))
 
     def __call__(self):
         ws = world_size()
         if ws == 1:
             return
-        grads = [p.grad for p in self.params if p.grad is not None]
-        bucket: List[torch.Tensor] = []
-        size = 0
-        for g in grads:
-            bucket.append(g)
-            size += g.numel() * g.element_size()
-            if size >= self.bucket_bytes:
-                self._flush(bucket, ws)
-                bucket, size = [], 0
-        if bucket:
-            self._flush(bucket, ws)
-
-    @staticmethod
-    def _flush(bucket: List[torch.Tensor], ws: int):
-        flat = torch._utils._flatten_dense_tensors(bucket)
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-        flat.div_(ws)
-        for g, f in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
-            g.copy_(f)
+        for i in range(len(self.buckets)):
+            if self._work[i] is None:  # no hook fired for the whole bucket this step
+                self._launch(i)
+        for i, w in enumerate(self._work):
+            if w:
+                flat, grads, work = w
+                work.wait()
+                flat.div_(ws)
+                for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                    g.copy_(f)
+        self._ready = [0] * len(self.buckets)
+        self._work = [None] * len(self.buckets)
 
 
 def all_gather_rows(t: torch.Tensor) -> torch.Tensor:

@@ -16,7 +16,8 @@ import torch.nn as nn
 
 from .... import kernels as K
 from ....commons.functional import cap_gradients
-from ....commons.layers import KShiftEmbedding, MLP, RowShardedKShiftEmbedding, TableBatchedKShiftEmbedding
+from ....commons.layers import (KShiftEmbedding, MLP, RowShardedKShiftEmbedding, TableBatchedKShiftEmbedding,
+                                TableShardedKShiftEmbedding)
 from .item_artifact import load_item_artifact
 from .product_tower import ProductTower
 from .query_tower import QueryTower
@@ -32,6 +33,13 @@ class UserContext(nn.Module):
         with torch.no_grad():
             self.tables.weight.normal_(0.0, 1.0)
         self.mlp = MLP(cfg.n_features * cfg.emb_dim, d_model, cfg.gate_sizes)
+
+    def shard_tables(self, rank: int, world: int) -> None:
+        """Data-parallel training over ``world`` ranks: keep only this rank's tables
+        (table-wise sharding, commons.layers.TableShardedKShiftEmbedding).  Call before
+        the optimizers are built; the replicas must hold identical tables on entry."""
+        if world > 1 and not isinstance(self.tables, TableShardedKShiftEmbedding):
+            self.tables = TableShardedKShiftEmbedding(self.tables, rank, world)
 
     def forward(self, cat_ids: torch.Tensor) -> torch.Tensor:
         B = cat_ids.shape[0]

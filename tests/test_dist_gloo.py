@@ -5,6 +5,7 @@ themselves are covered by the -m gpu tests; here the row update is applied with
 the C oracle (oracle/kshift_ref.c), so the test checks that every replica ends
 with the same table and that it equals the single-process update of the
 rank-averaged loss."""
+import math
 import os
 import socket
 
@@ -78,6 +79,39 @@ def test_grad_bucket_allreduce_averages():
     for i, (a, b) in enumerate(zip(*out)):
         assert torch.equal(a, b)
         assert torch.allclose(a, torch.full(a.shape, 1.5 * (i + 1)))
+
+
+def _bucket_allreduce_overlapped(rank, world):
+    """Real backward: the post-accumulate hooks launch each bucket's all-reduce during
+    the backward; the result equals the rank-averaged gradient."""
+    from recommendations_amd.distributed import GradBucketAllReduce
+    torch.manual_seed(0)  # identical replicas
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 32), torch.nn.Tanh(),
+                              torch.nn.Linear(32, 4))
+    ar = GradBucketAllReduce(net.parameters(), bucket_bytes=1024)  # several buckets
+    launched = []
+    for step in range(2):
+        x = torch.randn(8, 16, generator=torch.Generator().manual_seed(10 * step + rank))
+        net.zero_grad(set_to_none=True)
+        net(x).square().mean().backward()
+        launched.append(sum(w is not None for w in ar._work))
+        ar()
+    grads = [p.grad.clone() for p in net.parameters()]
+    # single-process reference of the last step: mean over both ranks' losses
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 32), torch.nn.Tanh(),
+                              torch.nn.Linear(32, 4))
+    ref.load_state_dict(net.state_dict())
+    loss = sum(ref(torch.randn(8, 16, generator=torch.Generator().manual_seed(10 + r))).square().mean()
+               for r in range(world)) / world
+    loss.backward()
+    return grads, [p.grad for p in ref.parameters()], launched, len(ar.buckets)
+
+
+def test_grad_bucket_allreduce_overlaps_backward():
+    for grads, ref, launched, nb in spawn(_bucket_allreduce_overlapped):
+        assert nb > 1 and launched == [nb, nb]  # every bucket launched from the backward's hooks
+        for g, r in zip(grads, ref):
+            torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
 
 
 def _gather_sparse(rank, world):
@@ -157,4 +191,93 @@ def _sharded_lookup(rank, world):
 def test_row_sharded_exchange():
     for exact, err in spawn(_sharded_lookup):
         assert exact
+        assert err < 1e-5
+
+
+def _oracle_local_kernels(record):
+    """CPU stand-ins for the two HIP calls of the table-sharded module (the routing is
+    what the gloo tests check; the kernels have their own -m gpu parity tests)."""
+    from oracle.ref import kshift_bwd_c, kshift_fwd_c
+
+    def fwd(mod, ids, gather_w):
+        P, Kk, Fl = mod._num_embeddings, mod._num_shifts, mod._F
+        Wn = gather_w.detach().float().numpy()
+        outs = [kshift_fwd_c(ids[:, f].numpy(), Wn[f * P:(f + 1) * P], Kk, mod._mode) for f in range(Fl)]
+        return torch.from_numpy(np.stack(outs, axis=1)), None
+
+    def bwd(mod, ids, gy, out, norms):
+        P, Kk, Fl = mod._num_embeddings, mod._num_shifts, mod._F
+        g = np.concatenate([kshift_bwd_c(ids[:, f].numpy(), gy[:, f].float().numpy(), P, Kk, mod._mode)
+                            for f in range(Fl)])
+        record.append(g)
+
+    return fwd, bwd
+
+
+def _table_sharded(rank, world):
+    """TableShardedKShiftEmbedding at world 2: every rank's forward equals the unsharded
+    lookup of its own ids, and each owner receives exactly the rank-averaged gradient
+    of its tables."""
+    import recommendations_amd.commons.layers as L
+    from oracle.ref import kshift_fwd_c
+    F, P, D, Kk, B = 5, 40, 8, 4, 6  # 5 tables over 2 ranks: owners hold 2 and 3
+    Wfull = torch.from_numpy(np.random.default_rng(3).standard_normal((F * P, D)).astype(np.float32))
+    full = L.TableBatchedKShiftEmbedding(F, P, D, Kk, sparse=True, out_dtype=torch.float32)
+    with torch.no_grad():
+        full.weight.copy_(Wfull)
+    record = []
+    L._kshift_fwd_local, L._kshift_bwd_local = _oracle_local_kernels(record)
+    mod = L.TableShardedKShiftEmbedding(full, rank, world)
+    g = np.random.default_rng(50 + rank)
+    ids = torch.from_numpy(g.integers(-2**63, 2**63 - 1, size=(B, F), dtype=np.int64))
+    gy = torch.from_numpy(g.standard_normal((B, F, D)).astype(np.float32))
+    out = mod(ids)
+    exp = np.stack([kshift_fwd_c(ids[:, f].numpy(), Wfull[f * P:(f + 1) * P].numpy(), Kk, 0) for f in range(F)], 1)
+    out.backward(gy)
+    return (float(np.abs(out.detach().numpy() - exp).max()), ids, gy, record[0], mod._bounds,
+            torch.equal(mod.weight.detach(), Wfull[mod._bounds[rank] * P:mod._bounds[rank + 1] * P]))
+
+
+def test_table_sharded_routing_world2():
+    from oracle.ref import kshift_bwd_c
+    res = spawn(_table_sharded)
+    F, P, Kk = 5, 40, 4
+    ids_all = [r[1] for r in res]
+    gy_all = [r[2] for r in res]
+    for rank, (err, _, _, grad, bounds, own_ok) in enumerate(res):
+        assert err == 0.0 and own_ok
+        f0, f1 = bounds[rank], bounds[rank + 1]
+        exp = np.concatenate([sum(kshift_bwd_c(i[:, f].numpy(), g[:, f].numpy(), P, Kk, 0) for i, g in
+                                  zip(ids_all, gy_all)) / 2 for f in range(f0, f1)])
+        np.testing.assert_allclose(grad, exp, rtol=1e-5, atol=1e-6)
+
+
+def _row_sharded_module(rank, world):
+    """RowShardedKShiftEmbedding (C3 item table) itself at world 2, its two kernels
+    replaced by the oracle: bit-identical to the unsharded gather of the same ids."""
+    import recommendations_amd.kernels as K_
+    import recommendations_amd.commons.layers as L
+    from oracle.ref import kshift_fwd_c, kshift_rows
+    P, D, Kk = 1000, 8, 16
+    K_.kshift_rows = lambda ids, P_, K2: torch.from_numpy(kshift_rows(ids.numpy(), P_, K2)).view(ids.shape + (K2,))
+
+    def pool(rows, vals, mode, out_dtype=torch.float32):
+        acc = torch.zeros(rows.shape[0], vals.shape[1], dtype=torch.float32)
+        for c in range(rows.shape[1]):  # in-order f32 sum, as lthm_gather_pool
+            acc += vals[rows[:, c]].float()
+        return acc / math.sqrt(rows.shape[1]) if mode == K_.KSHIFT_SCALE else acc
+
+    K_.gather_pool = pool
+    Wfull = torch.from_numpy(np.random.default_rng(9).standard_normal((P, D)).astype(np.float32))
+    mod = L.RowShardedKShiftEmbedding(P, D, num_shifts=Kk, rank=rank, world=world, dtype=torch.float32)
+    mod.load_full_weight(Wfull)
+    ids = torch.from_numpy(np.random.default_rng(70 + rank).integers(-2**63, 2**63 - 1, size=(50 + 7 * rank, 3),
+                                                                     dtype=np.int64))
+    out = mod(ids)
+    exp = kshift_fwd_c(ids.numpy(), Wfull.numpy(), Kk, 0).reshape(out.shape)
+    return float(np.abs(out.numpy() - exp).max())
+
+
+def test_row_sharded_module_world2():
+    for err in spawn(_row_sharded_module):
         assert err < 1e-5

@@ -67,3 +67,21 @@ def test_item_artifact_file_round_trip(tmp_path):
     save_file({"x": torch.zeros(2)}, str(tmp_path / "bad.safetensors"))
     with pytest.raises(ValueError):
         load_item_artifact(str(tmp_path / "bad.safetensors"))
+
+
+def test_bench_launches_n_ranks_by_itself():
+    """`python bench.py --gpus 2` with no torchrun env spawns 2 ranks itself (gloo here,
+    RCCL on the GPU box) and the process group reports world size 2."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--check-launch"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["world"] == 2 and out["sum"] == 2.0
