@@ -512,8 +512,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
   }
 }
 
-// Backward, blockIdx.y == 0: query tiles -> dQ and the bias gradient.
-//           blockIdx.y == 1: key tiles   -> dK and dV.
+// Backward, one block per (head, pass): pass 0 = query tiles -> dQ and the bias
+// gradient; pass 1 = key tiles -> dK and dV.
 // P = exp(S - lse) is recomputed from the forward's LSE; delta = rowsum(dO * O).
 template <int E>
 __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
@@ -527,8 +527,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
   float* lse = dbias + 2 * T + 2;                             // [Tk]
   float* delta = lse + Tk;                                    // [Tk]
   float* scr_all = delta + Tk;                                // [4][16][SCR_LD]
-  const int b = blockIdx.x / a.H, h = blockIdx.x - (blockIdx.x / a.H) * a.H;
-  const bool rows_pass = blockIdx.y == 0;
+  // both passes of a head are adjacent logical blocks on one XCD, dispatched together:
+  // the second pass's reads of q / k / v / o / dO hit that XCD's L2
+  const int lid = xcd_remap(blockIdx.x, gridDim.x), bh = lid >> 1;
+  const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const bool rows_pass = (lid & 1) == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
   const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
@@ -1100,7 +1103,7 @@ template <int E>
 static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   const size_t sh = bwd ? bwd_mfma_lds(a.T, E) : fwd_mfma_lds(a.T, E);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
-  if (bwd) hipLaunchKernelGGL((attn_bwd_mfma_k<E>), dim3(B * a.H, 2), dim3(256), sh, s, a);
+  if (bwd) hipLaunchKernelGGL((attn_bwd_mfma_k<E>), dim3(B * a.H * 2), dim3(256), sh, s, a);
   else hipLaunchKernelGGL((attn_fwd_mfma_k<E>), dim3(B * a.H), dim3(256), sh, s, a);
   LTHM_CHECK_LAUNCH();
   return 0;
