@@ -239,13 +239,15 @@ def cpu_cores() -> int:
 
 def timed_median(step) -> float:
     """BASELINE.md CPU plan: 2 warm-ups, then the median of 5 timed steps (seconds)."""
-    for _ in range(CPU_WARMUP):
+    for i in range(CPU_WARMUP):
         step()
+        print(f"[cpu_baseline] warm-up {i + 1}/{CPU_WARMUP}", file=sys.stderr, flush=True)
     ts = []
-    for _ in range(CPU_TIMED):
+    for i in range(CPU_TIMED):
         t0 = time.perf_counter()
         step()
         ts.append(time.perf_counter() - t0)
+        print(f"[cpu_baseline] step {i + 1}/{CPU_TIMED}: {ts[-1]:.2f} s", file=sys.stderr, flush=True)
     return float(np.median(ts))
 
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 19 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 20 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -451,6 +451,10 @@ typedef struct lthm_contrastive_desc {
                              of every input token (wrapper.py:131-135, 204-208; zero on the positive) */
   int64_t logq_stride;
   float* logq_col;        /* with logq: [n_mb, n_max] scratch written by the forward, read by the backward */
+  const void* y_raw;      /* backward, optional: bf16 [B, T+1, n_heads, De] next_token_emb before F.normalize */
+  const float* y_norm;    /* with y_raw: f32 [B, T+1, n_heads] its row norms (lthm_rownorm) */
+  void* dy;               /* with y_raw: bf16 [B, T+1, n_heads, De] written INSTEAD of d_out: the gradient through
+                             F.normalize (wrapper.py:118-119), every row of this head written */
 } lthm_contrastive_desc;
 
 /* Forward for one head over all mini-batches.  stats [n_mb, nstat] f32:

@@ -232,6 +232,10 @@ struct ClArgs {
   const float* lq;
   int64_t lq_stride;
   float* lqcol;
+  // ROWS epilogue through F.normalize: dy = (g - y (y . g)) / |x| with y = x / |x|
+  const bf16_t* y_raw;  // [B, Tp, NH, DE] or null
+  const float* y_norm;  // [B, Tp, NH]
+  bf16_t* dy;           // [B, Tp, NH, DE], written instead of d_out
 };
 
 struct Geo {
@@ -325,8 +329,9 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
     const int b = (int)(i / per_seq), rem = (int)(i - (int64_t)b * per_seq);
     const int t = tl0 + rem / (DE / 4), c4 = rem % (DE / 4);
-    float* dst = a.d_out + (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
-    *reinterpret_cast<float4*>(dst) = float4{0.f, 0.f, 0.f, 0.f};
+    const int64_t o = (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
+    if (a.dy) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
+    else *reinterpret_cast<float4*>(a.d_out + o) = float4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -927,6 +932,36 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   // write: dacc[mi][nd][j] = d[x = x0 + 32 w + 16 mi + rg + j][e = nd*16 + col]
   // (COLS: pad `in` rows get no gradient; their dacc is not written)
   const float gs = (a.gscale ? *a.gscale : 1.f) * it;
+  if (ROWS && a.dy) {
+    // through F.normalize (the separate lthm_rownorm_bwd pass and the f32 d_out round trip
+    // disappear): the 16 lanes of a lane group hold one row's 128 columns (col + 16 nd)
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int x = x0 + 32 * w + 16 * mi + rg + j;
+        const int xc = min(x, g.n - 1);  // every lane takes part in the row reduction
+        const int b = xc / g.L, t = xc - (xc / g.L) * g.L;
+        const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
+        const float nrm = a.y_norm[ro], den = fmaxf(nrm, 1e-12f);
+        float yv[8], dot = 0.f;
+#pragma unroll
+        for (int nd = 0; nd < 8; ++nd) {
+          yv[nd] = bf2f(a.y_raw[ro * DE + nd * 16 + col]) / den;
+          dot += yv[nd] * (gs * dacc[mi][nd][j]);
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) dot += __shfl_xor(dot, o, 64);
+        if (x < g.n) {
+#pragma unroll
+          for (int nd = 0; nd < 8; ++nd) {
+            const float gv = gs * dacc[mi][nd][j];
+            a.dy[ro * DE + nd * 16 + col] = f2bf(nrm > 1e-12f ? (gv - yv[nd] * dot) / nrm : gv / 1e-12f);
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -960,6 +995,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.d_out = d->d_out; a.d_in = d->d_in;
   a.colb = nullptr;
   a.lq = d->logq; a.lq_stride = d->logq_stride; a.lqcol = d->logq_col;
+  a.y_raw = (const bf16_t*)d->y_raw; a.y_norm = d->y_norm; a.dy = (bf16_t*)d->dy;
   return a;
 }
 
@@ -1050,7 +1086,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
 }
 
 extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream) {
-  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->diag && d->d_out && d->d_in);
+  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->diag && (d->d_out || d->dy) && d->d_in);
+  LTHM_REQUIRE(!d->dy || (d->y_raw && d->y_norm));
   ClArgs a = cl_args(d);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb), dim3(256), 0, s, a, d->diag);

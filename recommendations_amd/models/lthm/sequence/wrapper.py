@@ -100,20 +100,26 @@ class ContrastiveLossFn(torch.autograd.Function):
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         dev = yc.device
         g = dloss.contiguous().float()
-        # every element is written by lthm_contrastive_bwd (kept rows by the ROWS kernel,
-        # the t >= L tail of each head by its prologue), so no fill
-        d_out = torch.empty((B, T + 1, NH, De), dtype=torch.float32, device=dev)
+        # dy (bf16, the gradient through F.normalize) comes straight out of the ROWS kernel:
+        # every element is written (kept rows by the kernel, the t >= L tail of each head
+        # by its prologue), so no fill and no f32 d_out round trip
+        fuse = yc.dtype == torch.bfloat16
+        dy = torch.empty_like(yc) if fuse else None
+        d_out = None if fuse else torch.empty((B, T + 1, NH, De), dtype=torch.float32, device=dev)
         d_in = K.zeros((B, T, De), torch.float32, dev)
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
                                         lse[h], None, None, None, diag[h], w[h],  # diag: shift scratch
                                         logq, None if lqc is None else lqc[h])
             d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
+            if fuse:
+                d.y_raw, d.y_norm, d.dy = ptr(yc), ptr(ynorm), ptr(dy)
             # algorithmic work 3 x 2 n^2 De per head (one S recompute, dS . in, dS^T . out);
             # the ROWS and COLS kernels each recompute S, so they execute 4 x
             call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
                  _work=3.0 * ctx.flops[h], _unit="flop")
-        dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
+        if not fuse:
+            dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
         dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
         return dy.view(yc.shape), dt.view(tc.shape), None, None, None, None
 

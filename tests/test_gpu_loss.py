@@ -27,14 +27,20 @@ def bf16_unit(x):
 
 
 
-@pytest.mark.parametrize("B,T,NH,mbs,tau", [(8, 40, 2, 3, 0.05), (5, 130, 1, 4, 0.05), (6, 33, 3, 6, 0.01),
-                                            (3, 9, 2, 2, 0.05), (4, 9, 2, 2, 0.05), (33, 128, 1, 32, 0.05)])
+@pytest.mark.parametrize("B,T,NH,mbs,tau,ydt", [
+    (8, 40, 2, 3, 0.05, "f32"), (5, 130, 1, 4, 0.05, "f32"), (6, 33, 3, 6, 0.01, "f32"), (3, 9, 2, 2, 0.05, "f32"),
+    (4, 9, 2, 2, 0.05, "f32"), (33, 128, 1, 32, 0.05, "f32"),
+    # bf16 next_token_emb (the encoder's emb_heads output): the ROWS kernel writes the gradient
+    # through F.normalize itself (lthm_contrastive_desc.dy), no f32 d_out
+    (8, 40, 2, 3, 0.05, "bf16"), (33, 128, 3, 32, 0.05, "bf16"), (6, 33, 3, 6, 0.01, "bf16")])
 @pytest.mark.parametrize("beta", [0.0, 0.5])
-def test_contrastive_loss_vs_oracle(dev, B, T, NH, mbs, tau, beta):
+def test_contrastive_loss_vs_oracle(dev, B, T, NH, mbs, tau, ydt, beta):
     from recommendations_amd.models.lthm.sequence.wrapper import ContrastiveLossFn
     De, ks = 128, [1, 5, 10]
     g = torch.Generator().manual_seed(B * T + NH)
     y = torch.randn((B, T + 1, NH, De), generator=g)
+    if ydt == "bf16":
+        y = y.to(torch.bfloat16)
     tgt = torch.randn((B, T, De), generator=g)
     mask = torch.zeros((B, T), dtype=torch.bool)
     for b in range(B):  # left padding of random length; one fully padded sequence
@@ -54,17 +60,17 @@ def test_contrastive_loss_vs_oracle(dev, B, T, NH, mbs, tau, beta):
     loss.backward()
     torch.cuda.synchronize()
 
-    yc = y.clone().requires_grad_(True)
+    yc = y.float().clone().requires_grad_(True)
     tc = tgt.clone().requires_grad_(True)
     ref, stats = contrastive_loss(bf16_unit(yc), bf16_unit(tc), mask, offsets.numpy(), mbs, tau, ks, normalize=False,
                                   logq=logq)
     check(f"loss beta={beta}", abs(float(loss) - float(ref)) / max(abs(float(ref)), 1e-6), 1e-4)
     if ref.requires_grad:
         ref.backward()
-        check(f"d next_token_emb beta={beta}", relerr(yd.grad, yc.grad), 1e-2)
+        check(f"d next_token_emb beta={beta}", relerr(yd.grad.float(), yc.grad), 1e-2)
         check(f"d current_token_emb beta={beta}", relerr(td.grad, tc.grad), 1e-2)
     else:  # no usable row anywhere: the loss is a constant
-        assert float(yd.grad.abs().max()) == 0.0 and float(td.grad.abs().max()) == 0.0
+        assert float(yd.grad.float().abs().max()) == 0.0 and float(td.grad.abs().max()) == 0.0
     if True:  # per (mini-batch, head) statistics
         for mb in range(n_mb):
             for h in range(NH):
