@@ -30,7 +30,7 @@ FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md 
 
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
 PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
     "cl_bwd_k": ["cl_bwd_k<", "cl_shift_k"],
     "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_stats_k"],

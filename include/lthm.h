@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 20 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 21 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -342,6 +342,33 @@ int lthm_table_bwd_mfma(const uint16_t* rows, int32_t nidx, int32_t R, const voi
  * out = bucketize(x[:, f], q_f) / (nq + 1) - 0.5; quantiles [shared ? 1 : F, nq]. */
 int lthm_quantile_map(const float* x, int64_t B, int32_t F, const float* quantiles, int32_t nq, int32_t shared,
                       float* out, void* stream);
+
+/* Vector-feature layers (commons/transformers/layers.py), f32, all device pointers.
+ * rowproj_fwd: z[r, j] = s_r sum_k x[r, k] W[j, k] with W[j, k] at w[j*ldj + k*ldk], x [rows, dim].
+ *   mode 0 SimhashVectorIndexer (:426-437): out int64 [rows] = sum_j (z[r, j] > 0) << j, P <= 64;
+ *   mode 1 CosineLinear (:517-525) forward with w = normalize(W) [P, dim]:
+ *          out f32 [rows, P] = z / max(|x_r|, 1e-12). */
+int lthm_rowproj_fwd(const float* x, int64_t rows, int32_t dim, const float* w, int64_t ldj, int64_t ldk, int32_t P,
+                     int32_t mode, void* out, void* stream);
+/* F.normalize(x, dim=-1) over f32 rows */
+int lthm_l2norm_rows(const float* x, int64_t rows, int32_t dim, float* y, void* stream);
+/* its backward dx = (g - y (y . g)) / |x| (g / eps when |x| <= eps); exactly one of
+ * g [rows, dim] or dz [rows, P] (then g = dz @ w_hat, w_hat [P, dim]: CosineLinear's x
+ * side) is given; rinv [rows] (may be NULL) receives 1 / max(|x|, eps). */
+int lthm_l2norm_rows_bwd(const float* x, int64_t rows, int32_t dim, const float* g, const float* dz,
+                         const float* w_hat, int32_t P, float* dx, float* rinv, void* stream);
+/* CosineLinear weight side: dw_hat[j, k] += sum_r dz[r, j] x[r, k] rinv[r] (accumulates). */
+int lthm_cosine_wgrad(const float* dz, const float* x, const float* rinv, int64_t rows, int32_t P, int32_t dim,
+                      float* dw_hat, void* stream);
+/* Gaussian bins of LearnableCosineVectorEmbedding / ProbabilityVectorEmbedding
+ * (:558-569, :588-595): z [n] f32 with n = rows * P, element i at projection p = i % P,
+ * mean [P, nb] (nb <= 64): out[i, b] = normalize_b(topk_b(exp(-0.5 (z_i - mean[p, b])^2 / sigma2)));
+ * top_k 0 = no top-k.  out_dtype LTHM_F32 or LTHM_BF16.  bwd: dz [n] (may be NULL) and
+ * dmean [P, nb] (accumulated) from gout [n, nb] (g_dtype F32 / BF16). */
+int lthm_gauss_bins_fwd(const float* z, int64_t n, int32_t P, const float* mean, int32_t nb, float sigma2,
+                        int32_t top_k, void* out, int32_t out_dtype, void* stream);
+int lthm_gauss_bins_bwd(const float* z, int64_t n, int32_t P, const float* mean, int32_t nb, float sigma2,
+                        int32_t top_k, const void* gout, int32_t g_dtype, float* dz, float* dmean, void* stream);
 
 /* MoELinear (commons/transformers/layers.py:101-136), the parts around its GEMMs.
  * gate: probs[m, :] = softmax(g) with g = scale * logits[m, :] and, when top_k > 0,

@@ -319,6 +319,35 @@ def quantile_mapper(x, quantiles):
     return torch.bucketize(x, quantiles).to(torch.float32) / float(quantiles.numel() + 1) - 0.5
 
 
+def cosine_linear(x, weight):
+    """commons/transformers/layers.py:524-525."""
+    return F.linear(F.normalize(x, p=2.0, dim=-1), F.normalize(weight, p=2.0, dim=-1))
+
+
+def gaussian_bins(z, mean, sigma2, top_k=None):
+    """commons/transformers/layers.py:558-569 / 588-595: z [..., P], mean broadcast to
+    [..., P, nb]; the top-k threshold is the k-th largest activation."""
+    diff = z.unsqueeze(-1) - mean
+    act = torch.exp(-0.5 * diff * diff / float(sigma2))
+    out = act
+    if top_k is not None:
+        thresh = torch.topk(act, k=top_k, dim=-1, largest=True, sorted=True)[0][..., -1:]
+        out = torch.where(act < thresh, torch.zeros_like(act), act)
+    return F.normalize(out, p=2.0, dim=-1)
+
+
+def learnable_cve(x, proj_weight, mean, emb_weight, sigma2, top_k=None):
+    """commons/transformers/layers.py:553-556."""
+    bs, T, _ = x.shape
+    z = gaussian_bins(cosine_linear(x, proj_weight), mean, sigma2, top_k)
+    return F.linear(z.reshape(bs, T, -1), emb_weight)
+
+
+def probability_ve(x, mean, emb_weight, sigma2, top_k=None):
+    """commons/transformers/layers.py:581-586."""
+    return F.linear(gaussian_bins(x, mean, sigma2, top_k).reshape(x.shape[0], -1), emb_weight)
+
+
 def simhash(x, projection_mat):
     """commons/transformers/layers.py:431-437."""
     z = (x @ projection_mat) > 0

@@ -643,6 +643,97 @@ class CosineVectorEmbedding(nn.Module):
         return CVEFn.apply(x, [self], self.emb.weight)
 
 
+class SimhashVectorIndexer(nn.Module):
+    """commons/transformers/layers.py:426-437: int64 codes of the sign bits of
+    x @ projection_mat (buffer [inp_dim, n_proj], n_proj <= 64), one HIP kernel."""
+
+    def __init__(self, inp_dim: int, n_proj: int = 16):
+        super().__init__()
+        self.register_buffer("projection_mat", torch.randn((inp_dim, n_proj)) / math.sqrt(float(inp_dim)),
+                             persistent=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        codes = K.simhash(x.reshape(-1, x.shape[-1]), self.projection_mat)
+        return codes.view(x.shape[:-1])
+
+
+class CosineLinear(nn.Module):
+    """commons/transformers/layers.py:517-525: F.linear(normalize(x), normalize(W)) in f32
+    (K.CosineLinearFn)."""
+
+    def __init__(self, inp_dim: int, out_dim: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.randn((out_dim, inp_dim)) / math.sqrt(float(inp_dim)))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return K.CosineLinearFn.apply(x, self.weight)
+
+
+def _gauss_linear(z: torch.Tensor, mean: torch.Tensor, sigma2: float, top_k: Optional[int], emb: nn.Linear,
+                  rows_shape) -> torch.Tensor:
+    """gaussian_kernel -> view -> emb: the bins come out of the HIP kernel as the bf16
+    operand of the MFMA GEMM (K.mlp_chain with one Linear, f32 output)."""
+    bins = K.GaussBinsFn.apply(z, mean, sigma2, 0 if top_k is None else top_k, torch.bfloat16)
+    return K.mlp_chain(bins.view(*rows_shape, -1), [emb], [K.ACT_NONE], out_f32=True)
+
+
+def _check_top_k(top_k: Optional[int], num_bins: int) -> Optional[int]:
+    if top_k is None:
+        return None
+    if top_k < 1:
+        raise ValueError(f"top_k must be >= 1, got {top_k}")
+    return min(top_k, num_bins)
+
+
+class LearnableCosineVectorEmbedding(nn.Module):
+    """commons/transformers/layers.py:531-569: CosineLinear projection, gaussian bins around a
+    learnable mean (1, 1, n_proj, num_bins), optional top-k, Linear(n_proj * num_bins, emb_dim)."""
+
+    def __init__(self, inp_dim: int, emb_dim: int, n_proj: int = 16, num_bins: int = 20,
+                 sigma_inflation_factor: float = 1.0, top_k: Optional[int] = None):
+        super().__init__()
+        self.emb_dim, self.n_proj, self.num_bins = emb_dim, n_proj, num_bins
+        self.top_k = _check_top_k(top_k, num_bins)
+        self.sigma2 = (sigma_inflation_factor * 2.0 / num_bins) ** 2
+        self.proj = CosineLinear(inp_dim, n_proj)
+        self.mean = nn.Parameter(2 * torch.rand((1, 1, n_proj, num_bins)) - 1)
+        self.emb = nn.Linear(n_proj * num_bins, emb_dim, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        bs, seq_len, _ = x.shape
+        return _gauss_linear(self.proj(x), self.mean, self.sigma2, self.top_k, self.emb, (bs, seq_len))
+
+    def gaussian_kernel(self, z: torch.Tensor) -> torch.Tensor:
+        """:558-569 on its own (f32 out): [bs, seq_len, n_proj] -> [bs, seq_len, n_proj, num_bins]."""
+        out = K.GaussBinsFn.apply(z, self.mean, self.sigma2, self.top_k or 0, torch.float32)
+        return out.view(*z.shape, self.num_bins)
+
+
+class ProbabilityVectorEmbedding(nn.Module):
+    """commons/transformers/layers.py:575-595: gaussian bins of a probability x [bs, 1]
+    around a learnable mean (1, 1, num_bins), optional top-k, Linear(num_bins, emb_dim)."""
+
+    def __init__(self, emb_dim: int, num_bins: int = 10, sigma_inflation_factor: float = 1.0,
+                 top_k: Optional[int] = None):
+        super().__init__()
+        self.emb_dim, self.num_bins = emb_dim, num_bins
+        self.top_k = _check_top_k(top_k, num_bins)
+        self.sigma2 = (sigma_inflation_factor * 1.0 / num_bins) ** 2
+        self.mean = nn.Parameter(torch.rand((1, 1, num_bins)))
+        self.emb = nn.Linear(num_bins, emb_dim, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        bs, d = x.shape
+        if d != 1:
+            raise RuntimeError("ProbabilityVectorEmbedding expects input dim 1")
+        return _gauss_linear(x, self.mean, self.sigma2, self.top_k, self.emb, (bs,))
+
+    def gaussian_kernel(self, x: torch.Tensor) -> torch.Tensor:
+        """:588-595 on its own (f32 out): [bs, 1] -> [bs, 1, num_bins]."""
+        out = K.GaussBinsFn.apply(x, self.mean, self.sigma2, self.top_k or 0, torch.float32)
+        return out.view(*x.shape, self.num_bins)
+
+
 class QuantileMapper(nn.Module):
     """commons/transformers/layers.py:477-487: bucketize(x, q) / (len(q) + 1) - 0.5."""
 

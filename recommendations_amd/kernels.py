@@ -841,6 +841,111 @@ def quantile_map(x, quantiles, shared):
     return out
 
 
+def _aligned16(t):
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def simhash(x2d, proj):
+    """SimhashVectorIndexer (commons/transformers/layers.py:431-437): int64 [rows] of the
+    sign bits of x2d [rows, dim] @ proj [dim, P] (f32 dot products, P <= 64)."""
+    require_gpu(x2d, proj)
+    rows, dim = x2d.shape
+    P = proj.shape[1]
+    _check(proj.shape[0] == dim and 0 < P <= 64, f"simhash takes proj [{dim}, P <= 64], got {tuple(proj.shape)}")
+    x2d, proj = _aligned16(x2d.contiguous().float()), proj.contiguous().float()
+    out = torch.empty(rows, dtype=torch.int64, device=x2d.device)
+    call("lthm_rowproj_fwd", ptr(x2d), rows, dim, ptr(proj), 1, P, P, 0, ptr(out), stream(),
+         _key="rowproj_fwd_k", _work=4.0 * rows * dim + 8.0 * rows, _unit="B")
+    return out
+
+
+def l2norm_rows(x2d):
+    """F.normalize(x, dim=-1) over f32 rows (lthm_l2norm_rows)."""
+    rows, dim = x2d.shape
+    y = torch.empty_like(x2d)
+    call("lthm_l2norm_rows", ptr(x2d), rows, dim, ptr(y), stream())
+    return y
+
+
+def l2norm_rows_bwd(x2d, g=None, dz=None, w_hat=None, rinv=None):
+    rows, dim = x2d.shape
+    dx = torch.empty_like(x2d)
+    call("lthm_l2norm_rows_bwd", ptr(x2d), rows, dim, ptr(g), ptr(dz), ptr(w_hat),
+         0 if w_hat is None else w_hat.shape[0], ptr(dx), ptr(rinv), stream())
+    return dx
+
+
+class CosineLinearFn(torch.autograd.Function):
+    """CosineLinear (commons/transformers/layers.py:517-525): normalize(x) @ normalize(W)^T
+    in f32.  fwd: lthm_l2norm_rows(W) + lthm_rowproj_fwd(mode 1).  bwd: lthm_l2norm_rows_bwd
+    (x side, dz @ W_hat fused), lthm_cosine_wgrad + lthm_l2norm_rows_bwd (W side)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        require_gpu(x, w)
+        shp = x.shape
+        x2 = _aligned16(x.detach().contiguous().view(-1, shp[-1]).float())
+        wf = w.detach().contiguous().float()
+        P, dim = wf.shape
+        _check(dim == x2.shape[1], f"CosineLinear: x dim {x2.shape[1]} != weight dim {dim}")
+        w_hat = l2norm_rows(wf)
+        out = torch.empty((x2.shape[0], P), dtype=torch.float32, device=x.device)
+        call("lthm_rowproj_fwd", ptr(x2), x2.shape[0], dim, ptr(w_hat), dim, 1, P, 1, ptr(out), stream(),
+             _key="rowproj_fwd_k", _work=4.0 * x2.shape[0] * (dim + P), _unit="B")
+        ctx.save_for_backward(x2, wf, w_hat)
+        ctx.shp, ctx.dts = shp, (x.dtype, w.dtype)
+        return out.view(*shp[:-1], P)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wf, w_hat = ctx.saved_tensors
+        P, dim = wf.shape
+        dz = dy.contiguous().view(-1, P).float()
+        rows = x2.shape[0]
+        rinv = torch.empty(rows, dtype=torch.float32, device=x2.device)
+        dx = l2norm_rows_bwd(x2, dz=dz, w_hat=w_hat, rinv=rinv)
+        dwh = zeros((P, dim), torch.float32, x2.device)
+        call("lthm_cosine_wgrad", ptr(dz), ptr(x2), ptr(rinv), rows, P, dim, ptr(dwh), stream())
+        dw = l2norm_rows_bwd(wf, g=dwh)
+        return dx.view(ctx.shp).to(ctx.dts[0]), dw.to(ctx.dts[1])
+
+
+class GaussBinsFn(torch.autograd.Function):
+    """The gaussian_kernel of LearnableCosineVectorEmbedding / ProbabilityVectorEmbedding
+    (commons/transformers/layers.py:558-569, 588-595): z [..., P] f32, mean [P, nb]
+    -> [..., P * nb] (bf16 when it feeds the bf16 GEMM, else f32)."""
+
+    @staticmethod
+    def forward(ctx, z, mean, sigma2, top_k, out_dtype):
+        require_gpu(z, mean)
+        zf = z.detach().contiguous().float()
+        P = zf.shape[-1]
+        mf = mean.detach().contiguous().float().view(P, -1)
+        nb = mf.shape[1]
+        _check(0 < nb <= 64, f"gaussian bins take 1..64 bins, got {nb}")
+        out = torch.empty((*zf.shape[:-1], P * nb), dtype=out_dtype, device=z.device)
+        n = zf.numel()
+        call("lthm_gauss_bins_fwd", ptr(zf), n, P, ptr(mf), nb, float(sigma2), int(top_k), ptr(out), dcode(out),
+             stream(), _key="gauss_bins_fwd_k", _work=4.0 * n + out.element_size() * n * nb, _unit="B")
+        ctx.save_for_backward(zf, mf)
+        ctx.meta = (float(sigma2), int(top_k), mean.shape, z.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        zf, mf = ctx.saved_tensors
+        sigma2, top_k, mshape, zdt = ctx.meta
+        P, nb = mf.shape
+        g = g.contiguous()
+        if g.dtype not in (torch.float32, torch.bfloat16):
+            g = g.float()
+        dz = torch.empty_like(zf) if ctx.needs_input_grad[0] else None
+        dmean = zeros((P, nb), torch.float32, zf.device)
+        call("lthm_gauss_bins_bwd", ptr(zf), zf.numel(), P, ptr(mf), nb, sigma2, top_k, ptr(g), dcode(g), ptr(dz),
+             ptr(dmean), stream(), _key="gauss_bins_bwd_k")
+        return (None if dz is None else dz.to(zdt)), dmean.view(mshape), None, None, None
+
+
 def cve_table_bwd(rows, dY, R, modules, out=None):
     """MFMA one-hot gradient of CVE-structured tables (include/lthm.h lthm_cve_table_bwd).
     modules: [(slot0, nslot, row0, rows_per_slot)]; dY bf16 or f32 [n, D], D in {16..256} pow2."""

@@ -260,6 +260,47 @@ def gen_transformer_mask():
              **{f"g_{n}": p.grad for n, p in blk.named_parameters()})
 
 
+def gen_vecemb():
+    """CosineLinear, LearnableCosineVectorEmbedding, ProbabilityVectorEmbedding and a
+    wider SimhashVectorIndexer (commons/transformers/layers.py:426-595), forward + backward."""
+    from commons.transformers.layers import (CosineLinear, LearnableCosineVectorEmbedding,
+                                             ProbabilityVectorEmbedding, SimhashVectorIndexer)
+    torch.manual_seed(600)
+    cl = CosineLinear(24, 7)
+    x = torch.randn(5, 6, 24)
+    x[0, 0] = 0.0
+    x.requires_grad_(True)
+    y = cl(x)
+    dy = torch.randn(y.shape)
+    (y * dy).sum().backward()
+    save("cosine_linear", x=x.detach(), weight=cl.weight.detach(), out=y.detach(), dy=dy, dx=x.grad,
+         dweight=cl.weight.grad)
+    for tag, nb, tk in (("lcve", 20, None), ("lcve_top5", 20, 5), ("lcve_nb7", 7, 3)):
+        torch.manual_seed(610 + nb + (tk or 0))
+        m = LearnableCosineVectorEmbedding(24, 32, n_proj=8, num_bins=nb, sigma_inflation_factor=1.5, top_k=tk)
+        x = torch.randn(3, 9, 24, requires_grad=True)
+        y = m(x)
+        dy = torch.randn(y.shape)
+        (y * dy).sum().backward()
+        save(tag, x=x.detach(), proj_weight=m.proj.weight.detach(), mean=m.mean.detach(), emb_weight=m.emb.weight.detach(),
+             sigma2=np.float64(m.sigma2), top_k=np.int64(tk or 0), out=y.detach(), dy=dy, dx=x.grad,
+             dproj_weight=m.proj.weight.grad, dmean=m.mean.grad, demb_weight=m.emb.weight.grad)
+    for tag, nb, tk in (("pve", 10, None), ("pve_top3", 10, 3)):
+        torch.manual_seed(620 + (tk or 0))
+        m = ProbabilityVectorEmbedding(16, num_bins=nb, top_k=tk)
+        x = torch.rand(40, 1, requires_grad=True)
+        y = m(x)
+        dy = torch.randn(y.shape)
+        (y * dy).sum().backward()
+        save(tag, x=x.detach(), mean=m.mean.detach(), emb_weight=m.emb.weight.detach(), sigma2=np.float64(m.sigma2),
+             top_k=np.int64(tk or 0), out=y.detach(), dy=dy, dx=x.grad, dmean=m.mean.grad,
+             demb_weight=m.emb.weight.grad)
+    torch.manual_seed(630)
+    sv = SimhashVectorIndexer(40, 63)
+    x = torch.randn(4, 25, 40)
+    save("simhash63", x=x, projection_mat=sv.projection_mat, out=sv(x))
+
+
 if __name__ == "__main__":
     if not any("reference" in p for p in sys.path + os.environ.get("PYTHONPATH", "").split(":")):
         sys.exit("run with PYTHONPATH=/root/reference (build container only)")

@@ -22,6 +22,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class _Tensor:
+    """A result tensor sent back as a plain array: torch's fd-sharing of tensors through
+    a Queue needs the sending child alive until the parent has received, which it is not."""
+
+    def __init__(self, t):
+        self.a = t.detach().cpu().numpy().copy()
+
+
+def _pack(v):
+    if isinstance(v, torch.Tensor):
+        return _Tensor(v)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_pack(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _pack(x) for k, x in v.items()}
+    return v
+
+
+def _unpack(v):
+    if isinstance(v, _Tensor):
+        return torch.from_numpy(v.a)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_unpack(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _unpack(x) for k, x in v.items()}
+    return v
+
+
 def _run(rank, world, port, fn, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -29,7 +57,7 @@ def _run(rank, world, port, fn, q):
         from recommendations_amd.distributed import init_from_env
         r, _, w = init_from_env(backend="gloo")
         assert (r, w) == (rank, world)
-        q.put((rank, fn(rank, world)))
+        q.put((rank, _pack(fn(rank, world))))
     except Exception as e:  # surfaced by the parent
         q.put((rank, e))
     finally:
@@ -44,7 +72,7 @@ def _spawn_once(fn, world):
     procs = [ctx.Process(target=_run, args=(r, world, port, fn, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    res = {r: _unpack(v) for r, v in (q.get(timeout=120) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
     return res

@@ -131,3 +131,41 @@ def test_cve(name):
 def test_simhash():
     g = golden("simhash")
     assert (ref.simhash(T(g["x"]), T(g["projection_mat"])).numpy() == g["out"]).all()
+
+
+def test_simhash63():
+    g = golden("simhash63")
+    assert (ref.simhash(T(g["x"]), T(g["projection_mat"])).numpy() == g["out"]).all()
+
+
+def test_cosine_linear():
+    g = golden("cosine_linear")
+    x, w = T(g["x"]).clone().requires_grad_(True), T(g["weight"]).clone().requires_grad_(True)
+    y = ref.cosine_linear(x, w)
+    close(y, g["out"], 1e-5)
+    y.backward(T(g["dy"]))
+    close(x.grad, g["dx"], 1e-5)
+    close(w.grad, g["dweight"], 1e-5)
+
+
+@pytest.mark.parametrize("tag", ["lcve", "lcve_top5", "lcve_nb7"])
+def test_learnable_cve(tag):
+    g = golden(tag)
+    x, pw, mean, ew = (T(g[k]).clone().requires_grad_(True) for k in ("x", "proj_weight", "mean", "emb_weight"))
+    tk = int(g["top_k"]) or None
+    y = ref.learnable_cve(x, pw, mean, ew, float(g["sigma2"]), tk)
+    close(y, g["out"], 1e-5)
+    y.backward(T(g["dy"]))
+    for t, k in ((x, "dx"), (pw, "dproj_weight"), (mean, "dmean"), (ew, "demb_weight")):
+        close(t.grad, g[k], 1e-4)
+
+
+@pytest.mark.parametrize("tag", ["pve", "pve_top3"])
+def test_probability_ve(tag):
+    g = golden(tag)
+    x, mean, ew = (T(g[k]).clone().requires_grad_(True) for k in ("x", "mean", "emb_weight"))
+    y = ref.probability_ve(x, mean, ew, float(g["sigma2"]), int(g["top_k"]) or None)
+    close(y, g["out"], 1e-5)
+    y.backward(T(g["dy"]))
+    for t, k in ((x, "dx"), (mean, "dmean"), (ew, "demb_weight")):
+        close(t.grad, g[k], 1e-4)
