@@ -485,10 +485,13 @@ constexpr int CL_ROWS = 128;
 constexpr int CL_NBUF = 3;
 constexpr float LOG2E = 1.4426950408889634f;
 
+// M1: whether the second per-column vector is used (the fixed-shift forward has none,
+// which brings its LDS under 160 KiB / 3 for three blocks, i.e. three waves per SIMD)
+template <bool M1 = true, int NB = CL_NBUF>
 struct ClTile {
-  unsigned char img[CL_NBUF][64 * 256];
-  float m0[CL_NBUF][4][64];  // per-wave copies of a per-column vector (fwd: diag; bwd COLS: shift)
-  float m1[CL_NBUF][4][64];  // bwd COLS: row weights of the image rows
+  unsigned char img[NB][64 * 256];
+  float m0[NB][4][64];             // per-wave copies of a per-column vector (fwd: diag; bwd COLS: shift)
+  float m1[NB][4][M1 ? 64 : 1];    // bwd COLS: row weights of the image rows; fwd: logQ of the columns
 };
 
 __device__ __attribute__((aligned(16))) unsigned char cl_zero_row[256];
@@ -613,9 +616,11 @@ __device__ __forceinline__ float rank_threshold(float dg, float it, float tau) {
   return t;
 }
 
-template <bool FIXED>
-__global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
-  __shared__ __attribute__((aligned(16))) ClTile sh;
+// NB: LDS ring depth (3: two tiles of loads in flight behind the math; 2: one), OCC:
+// blocks per CU the registers and LDS are sized for
+template <bool FIXED, int NB, int OCC>
+__global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a) {
+  __shared__ __attribute__((aligned(16))) ClTile<!FIXED, NB> sh;
   const int bid = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
   const int mb = bid / gridDim.x;
   const Geo g = geo(a, mb);
@@ -649,20 +654,20 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
   RowCursor cur_in;
   cur_in.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
   auto stage = [&](int t) {
-    const int buf = t % CL_NBUF;
+    const int buf = t % NB;
     cur_in.stage(sh.img[buf], g.n, w, lane);
     glds4(t * 64 + lane < a.n_max ? a.colb + base + t * 64 + lane : &cl_ninf, sh.m0[buf][w]);
     if (!FIXED) glds4(a.lq && t * 64 + lane < a.n_max ? a.lqcol + base + t * 64 + lane : &cl_zero_f, sh.m1[buf][w]);
   };
   retire_loads();
   stage(0);
-  if (ntile > 1) stage(1);
+  if (NB > 2 && ntile > 1) stage(1);
   for (int tI = 0; tI < ntile; ++tI) {
-    const int cur = tI % CL_NBUF, c0 = tI * 64;
-    if (tI + 1 < ntile) wait_vm<FIXED ? 5 : 6>();
+    const int cur = tI % NB, c0 = tI * 64;
+    if (NB > 2 && tI + 1 < ntile) wait_vm<FIXED ? 5 : 6>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    if (tI + 2 < ntile) stage(tI + 2);
+    if (tI + NB - 1 < ntile) stage(tI + NB - 1);
     f32x4 acc[2][4];
     st_tile(acc, qf, sh.img[cur], lane);
     const float* cdg = sh.m0[cur][w];  // column exp2 bias: cs, or -inf for a pad column / beyond n
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(256, 2) void cl_fwd_k(ClArgs a) {
 // so it stays finite).
 template <bool ROWS, bool FIXED>
 __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
-  __shared__ __attribute__((aligned(16))) ClTile sh;
+  __shared__ __attribute__((aligned(16))) ClTile<> sh;
   const int bid = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
   const int mb = bid / gridDim.x;
   const Geo g = geo(a, mb);
@@ -1076,8 +1081,11 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   LTHM_CHECK_LAUNCH();
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
   // the fixed softmax shift 1/tau bounds the plain logits only: logQ takes the online max
-  if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((cl_fwd_k<false>), grid, dim3(256), 0, s, a);
+  // fixed shift: 3 blocks per CU (3 waves per SIMD hide more of the exp / count VALU
+  // latency: 0.91 -> 0.78-0.82 ms per C2 head; a 2-deep ring at 3 blocks measured the
+  // same, 4 blocks spill); running shift: 2
+  if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb), dim3(256), 0, s, a, stats, nstat, (const int*)ks, nk, loss_scale,
                      (float*)d->w);
