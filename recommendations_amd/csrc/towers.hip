@@ -306,7 +306,13 @@ constexpr int PE_MAXR = 4096;  // table rows
 
 __host__ __device__ constexpr int pe_rbw(int R32) { return R32 / 32 + 1; }  // odd dword stride: no bank repeats
 
-template <typename TX, int NF>
+// DMA (D = 128 / 256): the slabs stream by LDS-DMA through a 4-deep ring instead of the
+// register-staged double buffer: ring slots 0-1 sit where the double buffer was, slots
+// 2-3 reuse the mapper's wN / xs staging once the mapper products are done, so up to
+// three slabs are in flight behind the MFMAs (counted vmcnt + raw barrier per slab).
+__device__ __attribute__((aligned(16))) unsigned char pt_zero16[16];
+
+template <typename TX, int NF, bool DMA = false>
 __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int total, int R) {
   constexpr int D = 16 * NF;
   constexpr int CH = (NF % 2 == 0) ? 2 : 1;  // column halves
@@ -340,11 +346,38 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   }
   for (int i = tid; i < PE_TOK * RBW; i += 512) bits[i] = 0u;
   __syncthreads();
-  for (int i = tid; i < PE_TOK * total; i += 512) {
-    const int tt = i / total;
-    if (t0 + tt < d.n) {
-      const int k = d.rows_out[t0 * total + i];
-      if (k < R) atomicOr(bits + tt * RBW + (k >> 5), 1u << (k & 31));
+  {
+    // the block's rows are one contiguous run of nv uint16: 16-B loads, all of a thread's
+    // chunks in flight before the first LDS OR (was one dependent 2-byte load per OR)
+    const int64_t nt = min((int64_t)PE_TOK, d.n - t0);
+    const int nv = (int)nt * total;
+    const uint16_t* src = d.rows_out + t0 * total;
+    if (((uintptr_t)src & 15) == 0) {
+      constexpr int PASS = 9;  // 9 x 512 x 8 = 36864 >= PE_TOK * total for total <= 257 (nproj <= 256)
+      u32x4 v[PASS];
+#pragma unroll
+      for (int q = 0; q < PASS; ++q) {
+        const int c = tid + 512 * q;
+        v[q] = c * 8 < nv ? *reinterpret_cast<const u32x4*>(src + c * 8) : u32x4{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+      }
+#pragma unroll
+      for (int q = 0; q < PASS; ++q) {
+        const int c = tid + 512 * q;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = c * 8 + e;
+          const int k = (int)((v[q][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+          if (i < nv && k < R) {
+            const int tt = i / total;
+            atomicOr(bits + tt * RBW + (k >> 5), 1u << (k & 31));
+          }
+        }
+      }
+    } else {
+      for (int i = tid; i < nv; i += 512) {
+        const int k = src[i];
+        if (k < R) atomicOr(bits + (i / total) * RBW + (k >> 5), 1u << (k & 31));
+      }
     }
   }
   {
@@ -389,9 +422,35 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
       if (idx < 32 * D / 8) *reinterpret_cast<u32x4*>(slab + buf * SLAB + ct_off<D>(r, c)) = pf[q];
     }
   };
-  fetch(0);
-  store(0);
-  __syncthreads();
+  // DMA slab k0 / 32 into ring slot `slot`: piece p = 1 KiB = 512 / D rows; lane l lands at
+  // row p (512 / D) + l / NC, slot l % NC, so it loads chunk slot ^ (row & (NC - 1)) (ct_off)
+  constexpr int NC = D / 8;
+  constexpr int DPW = DMA ? D / 128 : 1;  // DMAs per wave and slab (16 or 8 pieces over 8 waves)
+  auto ring = [&](int slot) -> unsigned char* {
+    return slot < 2 ? slab + slot * SLAB : reinterpret_cast<unsigned char*>(wN) + (slot - 2) * SLAB;
+  };
+  auto issue = [&](int sl) {
+    const int k0 = sl * 32;
+    unsigned char* img = ring(sl & 3);
+#pragma unroll
+    for (int q = 0; q < DPW; ++q) {
+      const int pc = w + 8 * q;
+      const int row = pc * (512 / D) + lane / NC;
+      const int ch = (lane % NC) ^ (row & (NC - 1));
+      const void* src = k0 + row < R ? (const void*)(tab + (int64_t)(k0 + row) * ldt + ch * 8) : (const void*)pt_zero16;
+      glds16(src, img + pc * 1024);
+    }
+  };
+  const int nslab = R32 / 32;
+  if constexpr (DMA) {
+    issue(0);
+    if (nslab > 1) issue(1);
+    __syncthreads();  // (drains the two slab DMAs with the staging loads)
+  } else {
+    fetch(0);
+    store(0);
+    __syncthreads();
+  }
   const int tg = w % TG, chh = w / TG;
   const int nb0 = chh * NFW * 16;  // first column of this wave
   f32x4 acc[MT][NFW];
@@ -436,12 +495,29 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
     mb[mt] = reinterpret_cast<const unsigned char*>(bits + (tg * 16 * MT + mt * 16 + (lane & 15)) * RBW) + (lane >> 4);
-  const int nslab = R32 / 32;
+  if constexpr (DMA) {
+    __syncthreads();  // every wave is done with wN / xs: ring slots 2-3 take them over
+    if (nslab > 2) issue(2);
+    if (nslab > 3) issue(3);
+  }
   for (int sI = 0; sI < nslab; ++sI) {
     const int cur = sI & 1, k0 = sI * 32;
     const bool more = sI + 1 < nslab;
-    if (more) fetch(k0 + 32);
-    const unsigned char* img = slab + cur * SLAB;
+    const unsigned char* img;
+    if constexpr (DMA) {
+      // slabs issued: 0 .. min(nslab - 1, sI + 2) (sI = 0: .. 3); slab sI must have landed
+      const int pend = min(nslab - 1, sI == 0 ? 3 : sI + 2) - sI;
+      if (pend >= 3) wait_vm<3 * DPW>();
+      else if (pend == 2) wait_vm<2 * DPW>();
+      else if (pend == 1) wait_vm<DPW>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();  // also: every wave is done with slot (sI - 1) & 3
+      if (sI >= 1 && sI + 3 < nslab) issue(sI + 3);
+      img = ring(sI & 3);
+    } else {
+      if (more) fetch(k0 + 32);
+      img = slab + cur * SLAB;
+    }
     bf16x8v af[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) af[mt] = __builtin_bit_cast(bf16x8v, lut[mb[mt][k0 >> 3]]);
@@ -452,8 +528,10 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
       for (int mt = 0; mt < MT; ++mt)
         acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bf, acc[mt][f], 0, 0, 0);
     }
-    if (more) store(cur ^ 1);
-    __syncthreads();
+    if constexpr (!DMA) {
+      if (more) store(cur ^ 1);
+      __syncthreads();
+    }
   }
   // ---- epilogue: + bias, mask fill, bf16 store
   bf16_t* eo = reinterpret_cast<bf16_t*>(d.emb_out);
@@ -570,6 +648,9 @@ __global__ __launch_bounds__(256) void seg_tab_reduce_k(const float* __restrict_
 constexpr int CT_MAXTILE = 64;
 constexpr int CT_ROWS = 128;   // rows per tile (8 waves x 16)
 constexpr int CT_KT = 32;      // tokens per k-step
+// bucket-id tile row pitch (uint16): 40 instead of 32 puts the 16 slots a wave's
+// transposed 2-byte stores hit at once on 16 distinct banks (32: 4 banks, 16-way)
+constexpr int CT_RTLD = CT_KT + 8;
 constexpr int CT_MAXSL = 128;  // slots covering one tile
 struct CveTiles {
   int ntile;
@@ -591,7 +672,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
   constexpr int EPC = F32 ? 4 : 8;              // dY elements per 16-byte chunk
   constexpr int NCH = D / EPC;                  // 16-byte chunks per dY row
   constexpr int IMG = CT_KT * D * 2;            // one bf16 dY image
-  constexpr int RTB = CT_MAXSL * CT_KT * 2;     // bucket-id tile bytes
+  constexpr int RTB = CT_MAXSL * CT_RTLD * 2;   // bucket-id tile bytes
   constexpr int BUF = (F32 ? 2 : 1) * IMG + RTB;
   constexpr int PD = (CT_KT * NCH + 511) / 512;
   constexpr int PR = (CT_KT * CT_MAXSL + 511) / 512;
@@ -676,7 +757,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
     for (int k = 0; k < PR; ++k) {
       const int idx = tid + 512 * k;
       const int r = idx / nsl, s = idx - r * nsl;
-      if (idx < CT_KT * nsl) rt[s * CT_KT + r] = pr[k];
+      if (idx < CT_KT * nsl) rt[s * CT_RTLD + r] = pr[k];
     }
   };
   const int64_t nsteps = (t1 - t0 + CT_KT - 1) / CT_KT;
@@ -699,7 +780,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
 #pragma unroll
         for (int sl = 0; sl < CT_GENMAX; ++sl) {
           if (sl < nsl) {
-            const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + sl * CT_KT + 8 * (lane >> 4));
+            const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + sl * CT_RTLD + 8 * (lane >> 4));
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
@@ -710,7 +791,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = mvalid[mt] ? (short)f2bf((float)cnt[i]) : (short)0;
       } else {
-        const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls[mt] * CT_KT + 8 * (lane >> 4));
+        const u32x4 rv = *reinterpret_cast<const u32x4*>(rt + ls[mt] * CT_RTLD + 8 * (lane >> 4));
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const uint32_t rr = (i & 1) ? (rv[i >> 1] >> 16) : (rv[i >> 1] & 0xffffu);
@@ -893,13 +974,22 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
     }
     LTHM_CHECK_LAUNCH();
     const dim3 g2((unsigned)((d->n + PE_TOK - 1) / PE_TOK), (unsigned)nsl);
+    // the 4-deep DMA ring needs the mapper staging (wN + xs) to hold two 32-row slabs
+    const bool dma = (Ds == 128 || Ds == 256) &&
+                     (size_t)d->Din * Ds * 4 + (size_t)PE_TOK * d->Din * 4 >= (size_t)2 * 32 * Ds * 2;
 #define LTHM_PT_EMB(TX)                                                                                     \
   switch (Ds) {                                                                                             \
     case 16: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 1>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
     case 32: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 2>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
     case 64: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 4>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \
-    case 128: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 8>), g2, dim3(512), sh_mfma, s, *d, total, R); break; \
-    default: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 16>), g2, dim3(512), sh_mfma, s, *d, total, R); break; \
+    case 128:                                                                                               \
+      if (dma) hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 8, true>), g2, dim3(512), sh_mfma, s, *d, total, R);   \
+      else hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 8>), g2, dim3(512), sh_mfma, s, *d, total, R);             \
+      break;                                                                                                \
+    default:                                                                                                \
+      if (dma) hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 16, true>), g2, dim3(512), sh_mfma, s, *d, total, R);  \
+      else hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 16>), g2, dim3(512), sh_mfma, s, *d, total, R);            \
+      break;                                                                                                \
   }
     if (d->x_dtype == LTHM_BF16) { LTHM_PT_EMB(bf16_t) } else { LTHM_PT_EMB(float) }
 #undef LTHM_PT_EMB
@@ -989,7 +1079,7 @@ static int launch_table_mfma(const uint16_t* rows, int32_t nidx, CveTiles& ct, S
   const int direct = gz == 1;
   float* dst = direct ? dW : (float*)workspace;
   const bool f32 = dy_dtype == LTHM_F32;
-  const size_t sh = 2 * ((f32 ? 2 : 1) * (size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_KT * 2);
+  const size_t sh = 2 * ((f32 ? 2 : 1) * (size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_RTLD * 2);
   dim3 grid(nt, 1, (unsigned)gz);
   const int64_t zs = zbytes / 4;
 #define LTHM_TAB_CASE(DD)                                                                                            \
