@@ -445,11 +445,18 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_k(AttnArgs a) {
   const float rs = rsqrtf((float)E);
   const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
   const int col = lane & 15, rg = (lane >> 4) * 4;
-  const uint32_t mine = lpt_tiles(Tq / 16, Tk, a.causal, false, wave);
-  for (int q0 = 0; q0 < Tq; q0 += 16) {
-    if (!((mine >> (q0 >> 4)) & 1u)) continue;
+  // the wave's tiles in ascending order; the next tile's Q fragments are loaded while
+  // the current one computes
+  uint32_t mine = lpt_tiles(Tq / 16, Tk, a.causal, false, wave);
+  bf16x8v qn[NS];
+  if (mine) glob_row_frags<E>(qn, qg, a.q_ts, 16 * __builtin_ctz(mine), T, lane);
+  while (mine) {
+    const int q0 = 16 * __builtin_ctz(mine);
+    mine &= mine - 1;
     bf16x8v qf[NS];
-    glob_row_frags<E>(qf, qg, a.q_ts, q0, T, lane);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = qn[s];
+    if (mine) glob_row_frags<E>(qn, qg, a.q_ts, 16 * __builtin_ctz(mine), T, lane);
     f32x4 o[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) o[e] = f32x4{0.f, 0.f, 0.f, 0.f};
