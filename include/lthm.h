@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 21 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 22 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -392,6 +392,12 @@ int lthm_moe_hidden_bwd(const float* dGH, const void* H, const void* pre, const 
 int lthm_bce_logits_fwd(const float* z, const float* y, int64_t n, float inv_n, float* loss_sum, void* stream);
 int lthm_bce_logits_bwd(const float* z, const float* y, int64_t n, const float* gscale, float inv_n, float* dz,
                         void* stream);
+
+/* nn.MSELoss (embedding_module_gen.py:139-150): loss_sum += inv_n * sum (y - x)^2 (zero it
+ * first); bwd dy = 2 (y - x) * (*gscale) * inv_n.  y F32 or BF16 (dy the same), x f32. */
+int lthm_mse_fwd(const void* y, int32_t y_dtype, const float* x, int64_t n, float inv_n, float* loss_sum, void* stream);
+int lthm_mse_bwd(const void* y, int32_t y_dtype, const float* x, int64_t n, const float* gscale, float inv_n, void* dy,
+                 void* stream);
 
 /* QueryTower input assembly (query_tower.py:89-111): action + time embeddings,
  * pad substitution, zero/CLS token, reversed position embedding. */

@@ -448,6 +448,60 @@ __global__ __launch_bounds__(256) void bce_bwd_k(const float* __restrict__ z, co
 }
 }  // namespace lthm
 
+// ---------------------------------------------------------------- mean squared error
+// nn.MSELoss (embedding_module_gen.py:139, the reconstruction model): mean((y - x)^2),
+// backward dy = 2 (y - x) g / n.  y f32 or bf16 (KShift output), x f32.
+namespace lthm {
+template <typename TY>
+__global__ __launch_bounds__(256) void mse_fwd_k(const TY* __restrict__ y, const float* __restrict__ x, int64_t n,
+                                                 float inv_n, float* __restrict__ loss_sum) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = Elem<TY>::ld(y + i) - x[i];
+    acc = fmaf(d, d, acc);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss_sum, ((red[0] + red[1]) + (red[2] + red[3])) * inv_n);
+}
+template <typename TY>
+__global__ __launch_bounds__(256) void mse_bwd_k(const TY* __restrict__ y, const float* __restrict__ x, int64_t n,
+                                                 const float* __restrict__ gscale, float inv_n, TY* __restrict__ dy) {
+  const float g = (gscale ? *gscale : 1.f) * 2.f * inv_n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    Elem<TY>::st(dy + i, (Elem<TY>::ld(y + i) - x[i]) * g);
+}
+}  // namespace lthm
+
+extern "C" int lthm_mse_fwd(const void* y, int32_t y_dtype, const float* x, int64_t n, float inv_n, float* loss_sum,
+                            void* stream) {
+  LTHM_REQUIRE(n >= 0 && loss_sum != nullptr && (y_dtype == LTHM_F32 || y_dtype == LTHM_BF16));
+  if (n == 0) return 0;
+  const dim3 g(grid_for(n, 256, 1024)), b(256);
+  if (y_dtype == LTHM_F32)
+    hipLaunchKernelGGL(mse_fwd_k<float>, g, b, 0, (hipStream_t)stream, (const float*)y, x, n, inv_n, loss_sum);
+  else
+    hipLaunchKernelGGL(mse_fwd_k<bf16_t>, g, b, 0, (hipStream_t)stream, (const bf16_t*)y, x, n, inv_n, loss_sum);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_mse_bwd(const void* y, int32_t y_dtype, const float* x, int64_t n, const float* gscale, float inv_n,
+                            void* dy, void* stream) {
+  LTHM_REQUIRE(n >= 0 && dy != nullptr && (y_dtype == LTHM_F32 || y_dtype == LTHM_BF16));
+  if (n == 0) return 0;
+  const dim3 g(grid_for(n, 256, 4096)), b(256);
+  if (y_dtype == LTHM_F32)
+    hipLaunchKernelGGL(mse_bwd_k<float>, g, b, 0, (hipStream_t)stream, (const float*)y, x, n, gscale, inv_n, (float*)dy);
+  else
+    hipLaunchKernelGGL(mse_bwd_k<bf16_t>, g, b, 0, (hipStream_t)stream, (const bf16_t*)y, x, n, gscale, inv_n,
+                       (bf16_t*)dy);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int lthm_bce_logits_fwd(const float* z, const float* y, int64_t n, float inv_n, float* loss_sum,
                                    void* stream) {
   LTHM_REQUIRE(n >= 0 && loss_sum != nullptr);

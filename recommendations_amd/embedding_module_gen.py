@@ -24,9 +24,9 @@ from typing import Callable, Optional
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import ingest
+from . import kernels as K
 from .commons.layers import MLP, KShiftEmbedding
 from .optim import FusedAdagrad, SparseRowAdagrad
 
@@ -61,34 +61,60 @@ def _batches(n: int, batch_size: int, rng: np.random.Generator):
         yield idx[b:b + batch_size]
 
 
+class _LossLog:
+    """Per-batch losses stay on the device and reach ``log`` in groups (one host sync per
+    flush instead of one per batch as the reference's ``loss.item()`` print):
+    ``log_every`` batches per flush, 0 = once per epoch."""
+
+    def __init__(self, log: Optional[Callable], tag: str, num_epochs: int, log_every: int):
+        self.log, self.tag, self.num_epochs, self.every = log, tag, num_epochs, log_every
+        self.pending = []
+
+    def add(self, epoch: int, b: int, loss: torch.Tensor) -> None:
+        if self.log is None:
+            return
+        self.pending.append((epoch, b, loss.detach().reshape(1)))
+        if self.every > 0 and len(self.pending) >= self.every:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.pending:
+            return
+        vals = torch.cat([p[2] for p in self.pending]).tolist()
+        for (epoch, b, _), v in zip(self.pending, vals):
+            self.log(self.tag, epoch, self.num_epochs, b, v)
+        self.pending = []
+
+
 def train_model(df, expansion_factor: float, k_shift: int, *, num_epochs: int = 500, batch_size: int = 2 ** 18,
                 device: Optional[torch.device] = None, seed: int = 0, lr: float = 5e-1,
-                log: Optional[Callable] = print) -> KShiftEmbedding:
-    """embedding_module_gen.py:122-156 (reconstruction model)."""
+                log: Optional[Callable] = print, log_every: int = 0) -> KShiftEmbedding:
+    """embedding_module_gen.py:122-156 (reconstruction model); nn.MSELoss on lthm_mse_*."""
     device = device or torch.device("cuda")
     hashed_idx = torch.from_numpy(np.asarray(df["product_id"].values, dtype=np.int64)).to(device)
     x = torch.from_numpy(np.stack(df["embedding"].values).astype(np.float32)).to(device)
-    x = F.normalize(x, p=2.0, dim=-1)
+    x = K.l2norm_rows(x.contiguous())  # F.normalize(x, p=2.0, dim=-1)
     model = KShiftEmbedding(int(expansion_factor * x.size(0)), x.size(1), num_shifts=k_shift,
                             normalize_output=True, sparse=True).to(device)
     optim = SparseRowAdagrad([model], lr=lr)
     rng = np.random.default_rng(seed)
+    losses = _LossLog(log, "Model", num_epochs, log_every)
     for epoch in range(num_epochs):
         for b, idx in enumerate(_batches(x.size(0), batch_size, rng)):
             it = torch.from_numpy(idx).to(device)
             y = model(hashed_idx[it])
-            loss = F.mse_loss(y, x[it])
+            loss = K.mse_loss(y, x[it])
             loss.backward()
             optim.step()
-            if log is not None:
-                log("Model", epoch, num_epochs, b, float(loss.detach()))
+            losses.add(epoch, b, loss)
+        losses.flush()
     return model
 
 
 def train_mask_model(df, expansion_factor: float, k_shift: int, mask_emb_dim: int, *, num_epochs: int = 100,
                      batch_size: int = 2 ** 17, device: Optional[torch.device] = None, seed: int = 0,
                      lr: float = 5e-1, log: Optional[Callable] = print,
-                     negatives: Optional[Callable[[int], torch.Tensor]] = None) -> nn.Module:
+                     negatives: Optional[Callable[[int], torch.Tensor]] = None, log_every: int = 0) -> nn.Module:
     """embedding_module_gen.py:70-118 (catalogue-membership mask model).
     ``negatives(k)`` (default: uniform int64 on the device) supplies the k random
     non-catalogue ids of a batch."""
@@ -102,6 +128,7 @@ def train_mask_model(df, expansion_factor: float, k_shift: int, mask_emb_dim: in
     opt_mlp = FusedAdagrad(model[1].parameters(), lr=lr)
     rng = np.random.default_rng(seed)
     g = torch.Generator(device=device).manual_seed(seed)
+    losses = _LossLog(log, "MASK", num_epochs, log_every)
     for epoch in range(num_epochs):
         for b, idx in enumerate(_batches(n, batch_size, rng)):
             pos = product_id[torch.from_numpy(idx).to(device)]
@@ -113,11 +140,11 @@ def train_mask_model(df, expansion_factor: float, k_shift: int, mask_emb_dim: in
             ids = torch.cat([pos, neg])
             target = torch.cat([torch.ones(pos.size(0), device=device), torch.zeros(neg.size(0), device=device)])
             pred = model(ids).squeeze(1)
-            loss = F.binary_cross_entropy_with_logits(pred, target)
+            loss = K.bce_with_logits(pred.float().contiguous(), target)
             loss.backward()
             opt_tab.step()
             opt_mlp.step()
             opt_mlp.zero_grad(set_to_none=True)
-            if log is not None:
-                log("MASK", epoch, num_epochs, b, float(loss.detach()))
+            losses.add(epoch, b, loss)
+        losses.flush()
     return model

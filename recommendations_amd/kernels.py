@@ -1044,3 +1044,31 @@ class BCEWithLogitsFn(torch.autograd.Function):
 
 def bce_with_logits(z, y):
     return BCEWithLogitsFn.apply(z, y)
+
+
+class MSELossFn(torch.autograd.Function):
+    """nn.MSELoss() (mean) of y (f32 / bf16) against an f32 target, on lthm_mse_*."""
+
+    @staticmethod
+    def forward(ctx, y, x):
+        require_gpu(y, x)
+        _check(y.numel() == x.numel() and y.dtype in (torch.float32, torch.bfloat16) and x.dtype == torch.float32,
+               "mse takes f32 / bf16 predictions and an f32 target of the same size")
+        y, x = y.contiguous(), x.contiguous()
+        n = y.numel()
+        out = zeros((1,), torch.float32, y.device)
+        call("lthm_mse_fwd", ptr(y), dcode(y), ptr(x), n, 1.0 / max(n, 1), ptr(out), stream())
+        ctx.save_for_backward(y, x)
+        return out.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        y, x = ctx.saved_tensors
+        dy = torch.empty_like(y)
+        g = g.contiguous().float()
+        call("lthm_mse_bwd", ptr(y), dcode(y), ptr(x), y.numel(), ptr(g), 1.0 / max(y.numel(), 1), ptr(dy), stream())
+        return dy, None
+
+
+def mse_loss(y, x):
+    return MSELossFn.apply(y, x)

@@ -183,3 +183,22 @@ def test_item_artifact_round_trip_and_encoder(dev, tmp_path):
     out = model(batch)
     loss, _ = model.train_step(batch, out)
     assert torch.isfinite(loss).all()
+
+
+@pytest.mark.parametrize("n,ydt", [(1, torch.float32), (1000, torch.float32), (262_144 * 4 + 3, torch.float32),
+                                   (70_001, torch.bfloat16)])
+def test_mse_loss_kernel(dev, n, ydt):
+    """lthm_mse_fwd / _bwd (nn.MSELoss of the reconstruction model) against torch fp64."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(n)
+    y = torch.randn(n, generator=g).to(ydt)
+    x = torch.randn(n, generator=g)
+    yd = y.to(dev).requires_grad_(True)
+    loss = K.mse_loss(yd, x.to(dev))
+    loss.backward(torch.tensor(0.5, device=dev))
+    yr = y.double().requires_grad_(True)
+    lr = F.mse_loss(yr, x.double())
+    (0.5 * lr).backward()
+    check("mse loss vs fp64", abs(float(loss) - float(lr)) / max(abs(float(lr)), 1e-30), 1e-5)
+    tol = 1e-6 if ydt == torch.float32 else 8e-3  # the bf16 gradient's own rounding
+    check("mse grad vs fp64", relerr(yd.grad.float(), yr.grad), tol)

@@ -85,3 +85,24 @@ def test_bench_launches_n_ranks_by_itself():
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     out = json.loads(line)
     assert out["world"] == 2 and out["sum"] == 2.0
+
+
+def test_loss_log_batches_host_syncs():
+    """embedding_module_gen._LossLog: per-batch device losses reach the logger in order,
+    in groups of log_every (0 = at flush / epoch end)."""
+    import torch
+    from recommendations_amd.embedding_module_gen import _LossLog
+    seen = []
+    ll = _LossLog(lambda *a: seen.append(a), "Model", 3, 2)
+    for b in range(5):
+        ll.add(0, b, torch.tensor(float(b)))
+        assert len(seen) == (b + 1) // 2 * 2
+    ll.flush()
+    assert seen == [("Model", 0, 3, b, float(b)) for b in range(5)]
+    seen.clear()
+    ll = _LossLog(lambda *a: seen.append(a), "MASK", 1, 0)
+    ll.add(0, 0, torch.tensor(1.5))
+    assert seen == []
+    ll.flush()
+    assert seen == [("MASK", 0, 1, 0, 1.5)]
+    _LossLog(None, "x", 1, 1).add(0, 0, torch.tensor(0.0))  # no logger: nothing kept
