@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 22 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 23 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -488,9 +488,12 @@ typedef struct lthm_contrastive_desc {
   const float* y_norm;    /* with y_raw: f32 [B, T+1, n_heads] its row norms (lthm_rownorm) */
   void* dy;               /* with y_raw: bf16 [B, T+1, n_heads, De] written INSTEAD of d_out: the gradient through
                              F.normalize (wrapper.py:118-119), every row of this head written */
+  int32_t heads_run;      /* forward: heads head .. head + heads_run - 1 in one set of launches (0 or 1: one) */
+  int64_t head_stride;    /* with heads_run > 1: elements between consecutive heads' lse / pos / cnt / rank /
+                             diag / w / logq_col buffers; stats rows advance by n_mb * nstat */
 } lthm_contrastive_desc;
 
-/* Forward for one head over all mini-batches.  stats [n_mb, nstat] f32:
+/* Forward for one head (or heads_run consecutive heads) over all mini-batches.  stats [n_mb, nstat] f32 per head:
  * {mean CE, used rows, mean negatives, min negatives, mean rank, median rank,
  *  offset, hit@ks[0..nk)}; loss_scale multiplies the row weights (1 / n_mb). */
 int lthm_contrastive_fwd(const lthm_contrastive_desc* desc, float* stats, int32_t nstat, const int32_t* ks,

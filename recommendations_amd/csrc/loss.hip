@@ -236,7 +236,22 @@ struct ClArgs {
   const bf16_t* y_raw;  // [B, Tp, NH, DE] or null
   const float* y_norm;  // [B, Tp, NH]
   bf16_t* dy;           // [B, Tp, NH, DE], written instead of d_out
+  int64_t head_stride;  // forward over several heads: per-head buffer stride (blockIdx.z = head - head0)
 };
+
+// the per-head view of a multi-head forward launch: head head0 + z, buffers advanced by z strides
+__device__ __forceinline__ ClArgs head_args(const ClArgs& a0, int z) {
+  ClArgs a = a0;
+  if (z) {
+    const int64_t o = (int64_t)z * a0.head_stride;
+    a.head += z;
+    a.lse += o; a.pos += o; a.cnt += o; a.rank += o; a.diag += o;
+    a.w += o;
+    if (a.colb) a.colb += o;
+    if (a.lqcol) a.lqcol += o;
+  }
+  return a;
+}
 
 struct Geo {
   int L, off, Bm, n;
@@ -284,7 +299,8 @@ __device__ __forceinline__ void reg_frags(bf16x8v (&f)[4], int lane, int cnt, in
 // diag[r] = out_r . in_r / tau (fp32 dot of the bf16 operands), per (mb, row);
 // -inf for pad rows and for the rows n <= r < n_max (the forward reads the
 // diag of its columns as their pad flag)
-__global__ __launch_bounds__(256) void cl_diag_k(ClArgs a) {
+__global__ __launch_bounds__(256) void cl_diag_k(ClArgs a0) {
+  const ClArgs a = head_args(a0, blockIdx.z);
   const int mb = blockIdx.y;
   const Geo g = geo(a, mb);
   const int lane = threadIdx.x & 63;
@@ -338,8 +354,11 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
 // ---------------------------------------------------------------- stats (one block per mini-batch)
 // per (mb): used rows, mean CE, weights w_r = used / (U * n_mb_total); metrics.
 // stats[mb][*] = {loss, used, sum_negatives, min_negatives, sum_rank, median_rank, hits@k...}
-__global__ __launch_bounds__(256) void cl_stats_k(ClArgs a, float* __restrict__ stats, int nstat, const int* __restrict__ ks,
+__global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, float* __restrict__ stats, int nstat, const int* __restrict__ ks,
                                                   int nk, float loss_scale, float* __restrict__ wout) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  stats += (int64_t)blockIdx.z * a0.n_mb * nstat;
+  wout += (int64_t)blockIdx.z * a0.head_stride;
   constexpr int RPT = 4096 / 256;  // rows per thread (n <= 4096)
   __shared__ int hist[4096];       // histogram of the used rows' ranks (rank < n <= 4096)
   __shared__ float red[256];
@@ -619,9 +638,14 @@ __device__ __forceinline__ float rank_threshold(float dg, float it, float tau) {
 // NB: LDS ring depth (3: two tiles of loads in flight behind the math; 2: one), OCC:
 // blocks per CU the registers and LDS are sized for
 template <bool FIXED, int NB, int OCC>
-__global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a) {
+__global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a0) {
   __shared__ __attribute__((aligned(16))) ClTile<!FIXED, NB> sh;
-  const int bid = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  // (row block, mini-batch, head) from one XCD-remapped linear id: each XCD walks a
+  // contiguous run of (head, mini-batch) pairs
+  const int per_head = gridDim.x * gridDim.y;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), per_head * gridDim.z);
+  const int z = lin / per_head, bid = lin - z * per_head;
+  const ClArgs a = head_args(a0, z);
   const int mb = bid / gridDim.x;
   const Geo g = geo(a, mb);
   const int r0 = (bid - mb * gridDim.x) * CL_ROWS;
@@ -1001,6 +1025,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.colb = nullptr;
   a.lq = d->logq; a.lq_stride = d->logq_stride; a.lqcol = d->logq_col;
   a.y_raw = (const bf16_t*)d->y_raw; a.y_norm = d->y_norm; a.dy = (bf16_t*)d->dy;
+  a.head_stride = d->head_stride;
   return a;
 }
 
@@ -1074,12 +1099,17 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
                                     int32_t nk, float loss_scale, void* stream) {
   LTHM_REQUIRE(cl_check(d) == 0 && stats && d->lse && d->pos && d->cnt && d->rank && d->diag && d->w);
   LTHM_REQUIRE(nstat >= 7 + nk);
+  // several heads per launch: no tail round per head (C2: 4096 blocks a head at 3 per CU
+  // is 5.33 rounds of the 768 slots; six heads together are 32)
+  const int nrun = d->heads_run > 1 ? d->heads_run : 1;
+  LTHM_REQUIRE(d->head + nrun <= d->n_heads);
+  LTHM_REQUIRE(nrun == 1 || d->head_stride >= (int64_t)d->n_mb * d->n_max);
   ClArgs a = cl_args(d);
   a.colb = d->w;  // scratch until cl_stats_k writes the row weights
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb, nrun), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
-  const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
+  const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
   // the fixed softmax shift 1/tau bounds the plain logits only: logQ takes the online max
   // fixed shift: 3 blocks per CU (3 waves per SIMD hide more of the exp / count VALU
   // latency: 0.91 -> 0.78-0.82 ms per C2 head; a 2-deep ring at 3 blocks measured the
@@ -1087,8 +1117,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb), dim3(256), 0, s, a, stats, nstat, (const int*)ks, nk, loss_scale,
-                     (float*)d->w);
+  hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb, 1, nrun), dim3(256), 0, s, a, stats, nstat, (const int*)ks, nk,
+                     loss_scale, (float*)d->w);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

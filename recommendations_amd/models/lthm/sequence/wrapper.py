@@ -63,14 +63,13 @@ class ContrastiveLossFn(torch.autograd.Function):
         stats = torch.empty((NH, n_mb, nstat), **f32)
         ks_dev = torch.tensor(ks, dtype=torch.int32).to(dev, non_blocking=True)
         lqc = torch.empty((NH, n_mb, n_max), **f32) if logq is not None else None
-        descs = []
-        for h in range(NH):
-            d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
-                                        lse[h], pos[h], cnt[h], rank[h], diag[h], w[h], logq,
-                                        None if lqc is None else lqc[h])
-            call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats[h]), nstat, ptr(ks_dev), len(ks),
-                 1.0 / n_mb, stream(), _key="cl_fwd_k", _work=cfg["flops"][h], _unit="flop")
-            descs.append(d)
+        # every head in one set of launches (head h's buffers at h * n_mb * n_max)
+        d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, 0, De, mbs, n_mb, n_max, tau, offsets_dev,
+                                    lse[0], pos[0], cnt[0], rank[0], diag[0], w[0], logq,
+                                    None if lqc is None else lqc[0])
+        d.heads_run, d.head_stride = NH, n_mb * n_max
+        call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
+             1.0 / n_mb, stream(), _key="cl_fwd_k", _work=float(sum(cfg["flops"])), _unit="flop")
         # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
         loss = torch.empty(1, **f32)
         call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
