@@ -583,6 +583,160 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
   float* stg = sh.stg[wave];
   const float alpha = F8 ? g.alpha * *g.sa * *g.sb : g.alpha;
 
+  // Forward forms (K-contiguous B) defer their epilogue; the dgrad forms and the
+  // two-residual epilogue keep the in-line one (the deferred accumulator spills them).
+  constexpr bool DEFER = KB && EPI != EPI_RES2 && !F8;
+  if constexpr (DEFER) {
+  // Deferred epilogue: a finished tile's accumulator moves to eacc and its four 16-row
+  // slices are finished one per K-stage of the next tile (after that stage's MFMAs are
+  // issued), so the epilogue's VALU / LDS / stores overlap this wave's own MFMAs instead
+  // of following them.  Slices still pending when a tile ends are finished first.
+  f32x4 eacc[4][4];
+  int64_t erb = 0;  // row base of the deferred tile
+  PsIn<EPI> ein, enx;
+  // slice i of the deferred tile (i a compile-time constant: eacc stays in registers)
+  auto epi_slice = [&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    if (i + 1 < 4) ps_epi_load<EPI>(g, enx, erb + 16 * (i + 1), colc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) stg[((lane >> 4) * 4 + rr) * PS_LD + j * 16 + (lane & 15)] = eacc[i][j][rr];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int lr = (lane >> 3) + 8 * u;
+      const int64_t row = erb + 16 * i + 8 * u;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + lr * PS_LD + (lane & 7) * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + lr * PS_LD + (lane & 7) * 8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      const PsIn<EPI>& q = ein;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = alpha * v[e] + bias[e];
+      const bool ok = row < g.M && col0 < g.N;
+      if constexpr (EPI == EPI_ACT) {
+        if (g.act == LTHM_ACT_GELU_D) {
+          float dv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_tanh_and_grad(v[e], dv[e]);
+          if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, dv);
+        } else {
+          if (g.aux_out && ok) store_vec<bf16_t, 8>(g.aux_out + row * g.ldaux + col0, v);
+          if (g.act == LTHM_ACT_GELU) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = qgelu(v[e]);
+          }
+        }
+      }
+      if constexpr (EPI == EPI_GRAD) {
+        if (g.act == LTHM_ACT_MUL_AUX) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= q.x[u][e];
+        } else if (g.act == LTHM_ACT_GELU_GRAD) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(q.x[u][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(q.x[u][e]);
+        }
+      }
+      if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += q.x[u][e];
+      }
+      if constexpr (EPI == EPI_RES2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += q.y[u][e];
+      }
+      if (ok) {
+        if (g.out_dt == LTHM_F32) {
+          float* o = reinterpret_cast<float*>(g.C) + row * g.ldc + col0;
+          *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          store_vec<bf16_t, 8>(reinterpret_cast<bf16_t*>(g.C) + row * g.ldc + col0, v);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    ein = enx;
+  };
+  auto epi_all = [&]() __attribute__((always_inline)) {
+    epi_slice(std::integral_constant<int, 0>{});
+    epi_slice(std::integral_constant<int, 1>{});
+    epi_slice(std::integral_constant<int, 2>{});
+    epi_slice(std::integral_constant<int, 3>{});
+  };
+  int s = 0;  // ring stage counter (one per K-step, across tiles)
+  auto kstep = [&](int kk) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the stage the loaders refill next are done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const unsigned char* sa = sh.ring[s % PS_NST];
+    const unsigned char* sb = BRES ? sh.bslab[kk] : sa + TILE_BYTES;
+    ++s;
+    if constexpr (F8) {
+      i32x8v af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag8(sa, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag8(sb, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8v af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = read_frag<true>(sa, wm * 64 + i * 16, s2, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = read_frag<KB>(sb, wn * 64 + j * 16, s2, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+  for (int ti = 0; ti < ntile; ++ti) {
+    if (NK >= 4 && ti > 0) {
+      // the previous tile's four slices beside the first four K-steps' MFMAs
+      kstep(0);
+      epi_slice(std::integral_constant<int, 0>{});
+      kstep(1);
+      epi_slice(std::integral_constant<int, 1>{});
+      kstep(2);
+      epi_slice(std::integral_constant<int, 2>{});
+      kstep(3);
+      epi_slice(std::integral_constant<int, 3>{});
+      for (int kk = 4; kk < NK; ++kk) kstep(kk);
+    } else {
+      if (ti > 0) epi_all();
+      for (int kk = 0; kk < NK; ++kk) kstep(kk);
+    }
+    // ---- tile done: defer its epilogue
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        eacc[i][j] = acc[i][j];
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    erb = (int64_t)(first + 8 * R * ti) * BM + wm * 64 + (lane >> 3);  // + 16 i + 8 u
+    ps_epi_load<EPI>(g, ein, erb, colc);
+  }
+  if (ntile > 0) epi_all();
+  } else {
   int kk = 0, ti = 0;
   for (int s = 0; s < S; ++s) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the stage the loaders refill next are done
@@ -696,6 +850,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
     }
+  }
   }
 }
 
