@@ -474,15 +474,22 @@ __device__ __forceinline__ void ps_dma_ks(unsigned char* img, const bf16_t* P, i
 // epilogue inputs of one 16-row slice (the lane's 2 chunks of 8 columns)
 template <int EPI>
 struct PsIn {
-  float x[EPI == EPI_GRAD || EPI == EPI_RES1 || EPI == EPI_RES2 ? 2 : 1][8];
+  float x[EPI == EPI_RES1 || EPI == EPI_RES2 ? 2 : 1][8];
   float y[EPI == EPI_RES2 ? 2 : 1][8];
+  u32x4 xb[EPI == EPI_GRAD ? 2 : 1];  // GRAD: the aux chunks kept as packed bf16 until used
 };
+// element e of the GRAD aux chunk u
+template <int EPI>
+__device__ __forceinline__ float ps_aux(const PsIn<EPI>& q, int u, int e) {
+  const uint32_t w = q.xb[u][e >> 1];
+  return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+}
 template <int EPI>
 __device__ __forceinline__ void ps_epi_load(const GemmArgs& g, PsIn<EPI>& in, int64_t r0, int64_t col0) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t row = min(r0 + 8 * u, g.M - 1);  // clamped: the store is predicated
-    if constexpr (EPI == EPI_GRAD) load_vec<bf16_t, 16>(g.aux + row * g.ldaux + col0, in.x[u]);
+    if constexpr (EPI == EPI_GRAD) in.xb[u] = *reinterpret_cast<const u32x4*>(g.aux + row * g.ldaux + col0);
     if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
       const float* p = reinterpret_cast<const float*>(g.res1) + row * g.ldr1 + col0;
       load_vec<float, 16>(p, in.x[u]);
@@ -636,13 +643,13 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
       if constexpr (EPI == EPI_GRAD) {
         if (g.act == LTHM_ACT_MUL_AUX) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= q.x[u][e];
+          for (int e = 0; e < 8; ++e) v[e] *= ps_aux(q, u, e);
         } else if (g.act == LTHM_ACT_GELU_GRAD) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(q.x[u][e]);
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(ps_aux(q, u, e));
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(q.x[u][e]);
+          for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(ps_aux(q, u, e));
         }
       }
       if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
@@ -820,13 +827,13 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
         if constexpr (EPI == EPI_GRAD) {
           if (g.act == LTHM_ACT_MUL_AUX) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= q.x[u][e];
+            for (int e = 0; e < 8; ++e) v[e] *= ps_aux(q, u, e);
           } else if (g.act == LTHM_ACT_GELU_GRAD) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(q.x[u][e]);
+            for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(ps_aux(q, u, e));
           } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(q.x[u][e]);
+            for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(ps_aux(q, u, e));
           }
         }
         if constexpr (EPI == EPI_RES1 || EPI == EPI_RES2) {
