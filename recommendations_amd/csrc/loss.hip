@@ -256,7 +256,12 @@ __device__ __forceinline__ ClArgs head_args(const ClArgs& a0, int z) {
 struct Geo {
   int L, off, Bm, n;
   int64_t b0;
+  uint64_t Lm;  // ceil(2^32 / L): seq(c) = c / L by one 32 x 64 multiply (exact for c < 2^32 / L)
 };
+// sequence index c / L of a row / column c < n <= 4096
+__device__ __forceinline__ int seq_of(const Geo& g, int c) {
+  return (int)(((uint64_t)(uint32_t)c * g.Lm) >> 32);
+}
 
 __device__ __forceinline__ Geo geo(const ClArgs& a, int mb) {
   Geo g;
@@ -265,6 +270,7 @@ __device__ __forceinline__ Geo geo(const ClArgs& a, int mb) {
   g.b0 = (int64_t)mb * a.mbs;
   g.Bm = (int)min((int64_t)a.mbs, a.B - g.b0);
   g.n = g.L > 0 ? g.Bm * g.L : 0;
+  g.Lm = g.L > 0 ? ((1ull << 32) + (uint64_t)g.L - 1) / (uint64_t)g.L : 0;
   return g;
 }
 __device__ __forceinline__ const bf16_t* out_row(const ClArgs& a, const Geo& g, int r) {
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a0) {
     l[mi] = 0.f; pv[mi] = -INFINITY; cn[mi] = 0; rk[mi] = 0;
     dg[mi] = (r < g.n) ? a.diag[base + r] : 0.f;
     thr[mi] = rank_threshold(dg[mi], it, a.tau);
-    rsq[mi] = (r < g.n) ? r / g.L : -2;
+    rsq[mi] = (r < g.n) ? seq_of(g, r) : -2;
   }
   const int ntile = (g.n + 63) / 64;
   // 5 DMAs per wave and tile: 4 image pieces + the diag (pad flag) of the tile's columns
@@ -727,7 +733,7 @@ __global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a0) {
         for (int j = 0; j < 4; ++j) {
           const int cl = yb * 16 + rg + j;
           cok[yb][j] = cdg[cl] != -INFINITY;
-          csq[yb][j] = (c0 + cl) / g.L;
+          csq[yb][j] = seq_of(g, c0 + cl);
         }
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
@@ -840,7 +846,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     xsh[mi] = (ROWS && in) ? shift[base + x] : -INFINITY;
     xcap[mi] = xw[mi] != 0.f ? __log2f(xw[mi]) : -INFINITY;
     xpad[mi] = in ? (ROWS ? false : pad_of(a, g, x)) : true;
-    xsq[mi] = in ? x / g.L : -2;
+    xsq[mi] = in ? seq_of(g, x) : -2;
     // COLS: the logQ correction of this register row's column (log2 units)
     xq[mi] = (!FIXED && !ROWS && a.lq && in) ? a.lqcol[base + x] * LOG2E : 0.f;
   }
@@ -912,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int yl = yb * 16 + rg + j, y = y0 + yl;
-          const int ysq = y < g.n ? y / g.L : -1;
+          const int ysq = y < g.n ? seq_of(g, y) : -1;
           const float ysh = ROWS ? 0.f : sh.m0[cur][w][yl], yw = ROWS ? 0.f : sh.m1[cur][w][yl];
           const float yq = (ROWS && !FIXED) ? sh.m0[cur][w][yl] * LOG2E : 0.f;
 #pragma unroll
