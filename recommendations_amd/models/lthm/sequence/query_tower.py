@@ -169,22 +169,60 @@ class QueryTower(nn.Module):
         d.div_dow, d.mod_dow = te.dow.div, te.dow.mod
         return d
 
+    def _trim_stats(self, mask: torch.Tensor) -> torch.Tensor:
+        B, T = mask.shape
+        work = torch.empty(T + 2, dtype=torch.int32, device=mask.device)
+        call("lthm_trim_stats", ptr(mask), B, T, ptr(work), stream())
+        return work
+
     def compute_trim(self, mask: torch.Tensor) -> int:
         """query_tower.py:73-86: if the all-pad columns outnumber T - export_span the
         trim is T - export_span, else the first column with a real token.  The
         reference slices ``x[:, trim:]`` and re-reads seq_len from the result, so a
         negative trim (export_span > T) keeps the last |trim| columns."""
         B, T = mask.shape
-        work = torch.empty(T + 2, dtype=torch.int32, device=mask.device)
-        call("lthm_trim_stats", ptr(mask), B, T, ptr(work), stream())
-        first, n_all_pad = work[:2].tolist()  # one 8-byte device->host read per step (the reference syncs here too)
+        first, n_all_pad = self._trim_stats(mask)[:2].tolist()  # one 8-byte device->host read
         return effective_trim(T, self.export_span, first, n_all_pad)
 
     def forward(self, input, target, mask_inp, labels, timestamp, ids, ctx: Optional[torch.Tensor] = None,
                 future_outcome: int = 0):
+        """The trim (a host int that sets every shape below) needs the device mask.  Read
+        synchronously, the whole previous step drains first and the GPU then idles while the
+        host issues this step's first kernels.  Instead the tower is enqueued for the trim of
+        the previous call (production batches keep one full history, so it rarely changes)
+        while the trim statistics travel to pinned host memory on a side stream; the host
+        waits for that copy only, and re-runs the tower with the true trim on a miss (the
+        speculative outputs, which nothing else has read, are dropped)."""
         require_gpu(input)
+        B, T_full, _ = input.shape
+        guess = getattr(self, "_trim_guess", None)
+        if guess is None or guess[0] != T_full or torch.cuda.is_current_stream_capturing():
+            trim = self.compute_trim(mask_inp)
+            self._trim_guess = (T_full, trim)
+            return self._forward_trimmed(trim, input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome)
+        work = self._trim_stats(mask_inp)
+        if getattr(self, "_trim_host", None) is None:
+            self._trim_host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+            self._trim_stream = torch.cuda.Stream(device=input.device)
+        main = torch.cuda.current_stream(input.device)
+        side = self._trim_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._trim_host.copy_(work[:2], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        work.record_stream(side)
+        out = self._forward_trimmed(guess[1], input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome)
+        done.synchronize()
+        first, n_all_pad = self._trim_host.tolist()
+        trim = effective_trim(T_full, self.export_span, first, n_all_pad)
+        self._trim_guess = (T_full, trim)
+        if trim != guess[1]:
+            out = self._forward_trimmed(trim, input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome)
+        return out
+
+    def _forward_trimmed(self, trim: int, input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome):
         B, T_full, Dout = input.shape
-        trim = self.compute_trim(mask_inp)
         inp = input[:, trim:].contiguous() if trim else input
         T = T_full - trim
         P = LinearFn.apply(inp.view(B * T, Dout), self.inp_proj.weight, self.inp_proj.bias).view(B, T, self.emb_dim)

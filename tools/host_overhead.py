@@ -1,0 +1,75 @@
+"""Host-side issue time of the C2 training step vs its GPU time: times how long the
+Python loop takes to enqueue K steps (no sync inside) and the wall time until the GPU
+has finished them.  Issue time close to the GPU time means a host-bound step.
+python tools/host_overhead.py [--config c2] [--steps 10]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--find-sync", action="store_true",
+                    help="run one step under torch.cuda.set_sync_debug_mode('error') and print where it syncs")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    cfgd = dict(bench.CONFIGS[args.config])
+    cfg, model = bench.build(cfgd, dev)
+    opts = model.optimizers_for_param_groups(model.param_groups())
+    from recommendations_amd.data import synthetic_lthm_batch
+    batch = synthetic_lthm_batch(cfgd["B"], cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=0, device=dev)
+
+    def step():
+        out = model(batch)
+        loss, _ = model.train_step(batch, out)
+        loss.backward()
+        for o in opts:
+            o.step()
+            o.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    if args.find_sync:
+        import traceback
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            step()
+            print("no synchronizing torch call in the step")
+        except RuntimeError:
+            traceback.print_exc(limit=12)
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t_issue = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    # the issue time of one step on its own, GPU idle at the start (a lower bound on the host cost)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    step()
+    t_one = time.perf_counter() - t1
+    torch.cuda.synchronize()
+    print(json.dumps({"config": args.config, "steps": args.steps,
+                      "issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
+                      "wall_ms_per_step": round(1e3 * t_all / args.steps, 3),
+                      "issue_ms_single_step": round(1e3 * t_one, 3),
+                      "host_cpus": os.cpu_count()}))
+
+
+if __name__ == "__main__":
+    main()
