@@ -52,9 +52,25 @@ def main():
         finally:
             torch.cuda.set_sync_debug_mode("default")
         torch.cuda.synchronize()
+    # host time per phase in steady state (a phase that blocks on the GPU shows up here)
+    phases = {"forward": 0.0, "train_step": 0.0, "backward": 0.0, "optimizer": 0.0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        ta = time.perf_counter()
+        out = model(batch)
+        tb = time.perf_counter()
+        loss, _ = model.train_step(batch, out)
+        tc = time.perf_counter()
+        loss.backward()
+        td = time.perf_counter()
+        for o in opts:
+            o.step()
+            o.zero_grad(set_to_none=True)
+        te = time.perf_counter()
+        phases["forward"] += tb - ta
+        phases["train_step"] += tc - tb
+        phases["backward"] += td - tc
+        phases["optimizer"] += te - td
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
@@ -68,6 +84,7 @@ def main():
                       "issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
                       "wall_ms_per_step": round(1e3 * t_all / args.steps, 3),
                       "issue_ms_single_step": round(1e3 * t_one, 3),
+                      "phase_ms_per_step": {k: round(1e3 * v / args.steps, 3) for k, v in phases.items()},
                       "host_cpus": os.cpu_count()}))
 
 
