@@ -26,8 +26,11 @@ def main():
     cfgd = dict(bench.CONFIGS[args.config])
     cfg, model = bench.build(cfgd, dev)
     opts = model.optimizers_for_param_groups(model.param_groups())
-    from recommendations_amd.data import synthetic_lthm_batch
-    batch = synthetic_lthm_batch(cfgd["B"], cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=0, device=dev)
+    from recommendations_amd.data import synthetic_lthm_batch, synthetic_ranker_batch
+    if cfgd.get("kind") == "ranker":
+        batch = synthetic_ranker_batch(cfgd["B"], cfgd["n_dense"], cfgd["n_cat"], seed=1234, rank=0, device=dev)
+    else:
+        batch = synthetic_lthm_batch(cfgd["B"], cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=0, device=dev)
 
     def step():
         out = model(batch)
