@@ -837,50 +837,105 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
 // x0[b, t+1] = (mask ? pad : P[b,t] + act[lab] + hod[.] + how[.] + dow[.]) + wpe[T-1-t]
 template <typename TP>
 __global__ __launch_bounds__(256) void tokens_fwd_k(lthm_tokens_desc d) {
+  // A wave takes 64 rows at a time: lane l first derives the table indices of row r0 + l
+  // (the label / timestamp loads and the 64-bit floor-div / mod chains of all 64 rows in
+  // parallel), then the wave assembles the rows one after the other with those indices
+  // read back by lane broadcast, 64 columns per instruction.
   const int T = d.T_full - d.trim, Tp = T + 1, D = d.d;
   const int64_t rows = d.B * Tp;
   const int lane = threadIdx.x & 63;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
-    const int64_t b = r / Tp;
-    const int tp = (int)(r - b * Tp);
-    uint16_t ri[5] = {0xffff, 0xffff, 0xffff, 0xffff, 0xffff};
-    const int wrow = T - tp;  // pos = seq_len - arange(0, seq_len + 1)
-    ri[4] = (uint16_t)(d.off_wpe + wrow);
-    bool masked = false;
-    int64_t ia = 0, ih = 0, iw = 0, idw = 0;
-    int64_t src = -1;
-    if (tp > 0) {
-      const int64_t g = b * d.T_full + d.trim + (tp - 1);
-      masked = d.mask[g] != 0;
-      if (!masked) {
-        ia = pymod64(d.labels[g], 4);
-        const int64_t ts = d.ts[g];
-        ih = pymod64(floordiv64(ts, d.div_hod), d.mod_hod);
-        iw = pymod64(floordiv64(ts, d.div_how), d.mod_how);
-        idw = pymod64(floordiv64(ts, d.div_dow), d.mod_dow);
-        ri[0] = (uint16_t)(d.off_act + ia);
-        ri[1] = (uint16_t)(d.off_hod + ih);
-        ri[2] = (uint16_t)(d.off_how + iw);
-        ri[3] = (uint16_t)(d.off_dow + idw);
-        src = b * T + (tp - 1);
-      } else {
-        ri[0] = (uint16_t)d.off_pad;
+  const int64_t wstride = (int64_t)gridDim.x * 4 * 64;
+  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; r0 < rows; r0 += wstride) {
+    const int64_t r = r0 + lane;
+    int kind = 0;  // 0: context token (tp == 0), 1: pad, 2: item token
+    int ia = 0, ih = 0, iw = 0, idw = 0, wrow = 0;
+    int64_t b = 0, src = 0;
+    if (r < rows) {
+      b = r / Tp;
+      const int tp = (int)(r - b * Tp);
+      uint16_t ri[5] = {0xffff, 0xffff, 0xffff, 0xffff, 0xffff};
+      wrow = T - tp;  // pos = seq_len - arange(0, seq_len + 1)
+      ri[4] = (uint16_t)(d.off_wpe + wrow);
+      if (tp > 0) {
+        const int64_t g = b * d.T_full + d.trim + (tp - 1);
+        if (d.mask[g] != 0) {
+          kind = 1;
+          ri[0] = (uint16_t)d.off_pad;
+        } else {
+          kind = 2;
+          ia = (int)pymod64(d.labels[g], 4);
+          const int64_t ts = d.ts[g];
+          ih = (int)pymod64(floordiv64(ts, d.div_hod), d.mod_hod);
+          iw = (int)pymod64(floordiv64(ts, d.div_how), d.mod_how);
+          idw = (int)pymod64(floordiv64(ts, d.div_dow), d.mod_dow);
+          ri[0] = (uint16_t)(d.off_act + ia);
+          ri[1] = (uint16_t)(d.off_hod + ih);
+          ri[2] = (uint16_t)(d.off_how + iw);
+          ri[3] = (uint16_t)(d.off_dow + idw);
+          src = b * T + (tp - 1);
+        }
+      }
+      if (d.rows_out) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) d.rows_out[r * 5 + i] = ri[i];
       }
     }
-    for (int c = lane; c < D; c += 64) {
-      float v;
-      if (tp == 0) {
-        v = d.ctx ? d.ctx[b * D + c] : 0.f;
-      } else if (masked) {
-        v = d.pad[c];
-      } else {
-        v = Elem<TP>::ld(reinterpret_cast<const TP*>(d.P) + src * D + c);
-        v = v + d.act[ia * D + c] + d.hod[ih * D + c] + d.how[iw * D + c] + d.dow[idw * D + c];
+    const int nr = (int)min((int64_t)64, rows - r0);
+    if (D == 256) {
+      // 4 rows per step, every load of the 4 rows issued before the first store
+      for (int k0 = 0; k0 < nr; k0 += 4) {
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = min(k0 + u, nr - 1);
+          const int kk = __shfl(kind, k, 64), wr = __shfl(wrow, k, 64);
+          const int a0 = __shfl(ia, k, 64), a1 = __shfl(ih, k, 64), a2 = __shfl(iw, k, 64), a3 = __shfl(idw, k, 64);
+          const int64_t bk = (int64_t)__shfl((int)b, k, 64);
+          const int64_t sk = ((int64_t)__shfl((int)(src >> 32), k, 64) << 32) | (uint32_t)__shfl((int)src, k, 64);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = lane + 64 * q;
+            float x;
+            if (kk == 0) {
+              x = d.ctx ? d.ctx[bk * 256 + c] : 0.f;
+            } else if (kk == 1) {
+              x = d.pad[c];
+            } else {
+              x = Elem<TP>::ld(reinterpret_cast<const TP*>(d.P) + sk * 256 + c);
+              x = x + d.act[a0 * 256 + c] + d.hod[a1 * 256 + c] + d.how[a2 * 256 + c] + d.dow[a3 * 256 + c];
+            }
+            v[u][q] = x + d.wpe[(int64_t)wr * 256 + c];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + u < nr) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d.x0[(r0 + k0 + u) * 256 + lane + 64 * q] = v[u][q];
+          }
       }
-      v = v + d.wpe[(int64_t)wrow * D + c];
-      d.x0[r * D + c] = v;
+      continue;
     }
-    if (d.rows_out && lane < 5) d.rows_out[r * 5 + lane] = ri[lane];
+    for (int k = 0; k < nr; ++k) {
+      const int kk = __shfl(kind, k, 64), wr = __shfl(wrow, k, 64);
+      const int a0 = __shfl(ia, k, 64), a1 = __shfl(ih, k, 64), a2 = __shfl(iw, k, 64), a3 = __shfl(idw, k, 64);
+      const int64_t bk = (int64_t)__shfl((int)b, k, 64);
+      const int64_t sk = ((int64_t)__shfl((int)(src >> 32), k, 64) << 32) | (uint32_t)__shfl((int)src, k, 64);
+      const int64_t rk = r0 + k;
+      for (int c = lane; c < D; c += 64) {
+        float v;
+        if (kk == 0) {
+          v = d.ctx ? d.ctx[bk * D + c] : 0.f;
+        } else if (kk == 1) {
+          v = d.pad[c];
+        } else {
+          v = Elem<TP>::ld(reinterpret_cast<const TP*>(d.P) + sk * D + c);
+          v = v + d.act[a0 * D + c] + d.hod[a1 * D + c] + d.how[a2 * D + c] + d.dow[a3 * D + c];
+        }
+        v = v + d.wpe[(int64_t)wr * D + c];
+        d.x0[rk * D + c] = v;
+      }
+    }
   }
 }
 
@@ -1195,9 +1250,9 @@ extern "C" int lthm_tokens_fwd(const lthm_tokens_desc* d, void* stream) {
   const int64_t rows = d->B * (d->T_full - d->trim + 1);
   hipStream_t s = (hipStream_t)stream;
   if (d->p_dtype == LTHM_BF16)
-    hipLaunchKernelGGL((tokens_fwd_k<bf16_t>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, *d);
+    hipLaunchKernelGGL((tokens_fwd_k<bf16_t>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
   else
-    hipLaunchKernelGGL((tokens_fwd_k<float>), dim3(grid_for(rows, 4, 256 * 8)), dim3(256), 0, s, *d);
+    hipLaunchKernelGGL((tokens_fwd_k<float>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
   LTHM_CHECK_LAUNCH();
   return 0;
 }
