@@ -1119,12 +1119,55 @@ extern "C" int lthm_segmented_table_bwd(const uint16_t* rows, int32_t nidx, int3
   return 0;
 }
 
+static int lthm_tower_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// resident 512-thread blocks per CU of one cve_tab_bwd_k form (registers and LDS), cached
+template <int DD>
+static int cve_tab_bpc_d(bool f32, bool gen, size_t sh) {
+  static int cache[4] = {0, 0, 0, 0};
+  int& c = cache[(f32 ? 2 : 0) + (gen ? 1 : 0)];
+  if (c == 0) {
+    int b = 0;
+    hipError_t e;
+    if (f32 && gen) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, cve_tab_bwd_k<DD, true, true>, 512, sh);
+    else if (f32) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, cve_tab_bwd_k<DD, true, false>, 512, sh);
+    else if (gen) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, cve_tab_bwd_k<DD, false, true>, 512, sh);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, cve_tab_bwd_k<DD, false, false>, 512, sh);
+    c = (e == hipSuccess && b > 0) ? b : 1;
+  }
+  return c;
+}
+static int cve_tab_blocks_per_cu(int D, bool f32, bool gen, size_t sh) {
+  switch (D) {
+    case 16: return cve_tab_bpc_d<16>(f32, gen, sh);
+    case 32: return cve_tab_bpc_d<32>(f32, gen, sh);
+    case 64: return cve_tab_bpc_d<64>(f32, gen, sh);
+    case 128: return cve_tab_bpc_d<128>(f32, gen, sh);
+    default: return cve_tab_bpc_d<256>(f32, gen, sh);
+  }
+}
+
 static int launch_table_mfma(const uint16_t* rows, int32_t nidx, CveTiles& ct, SegTab& st, int rtot, bool gen,
                              const void* dY, int32_t dy_dtype, int64_t ldy, int64_t n, int32_t D, float* dW,
                              void* workspace, int64_t workspace_bytes, hipStream_t s) {
   const int nt = ct.ntile;
   const int64_t zbytes = (int64_t)rtot * D * 4;
-  int64_t gz = (512 + nt - 1) / nt;  // ~2 blocks of 512 threads per CU
+  const bool f32 = dy_dtype == LTHM_F32;
+  const size_t sh = 2 * ((f32 ? 2 : 1) * (size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_RTLD * 2);
+  // one round of blocks: ntile x gz <= CUs x resident blocks per CU (the D = 256 forms hold
+  // ~200 VGPRs, i.e. one 512-thread block per CU).  522 blocks for 256 slots ran three
+  // rounds, the last with ten blocks.
+  const int bpc = cve_tab_blocks_per_cu(D, f32, gen, sh);
+  int64_t gz = std::max<int64_t>(1, (int64_t)lthm_tower_cus() * bpc / nt);
   gz = std::min<int64_t>(gz, (n + 1023) / 1024);
   gz = std::min<int64_t>(gz, workspace ? workspace_bytes / zbytes : (int64_t)1);
   if (gz < 2) gz = 1;
@@ -1133,8 +1176,6 @@ static int launch_table_mfma(const uint16_t* rows, int32_t nidx, CveTiles& ct, S
   gz = (n + tpb - 1) / tpb;
   const int direct = gz == 1;
   float* dst = direct ? dW : (float*)workspace;
-  const bool f32 = dy_dtype == LTHM_F32;
-  const size_t sh = 2 * ((f32 ? 2 : 1) * (size_t)CT_KT * D * 2 + (size_t)CT_MAXSL * CT_RTLD * 2);
   dim3 grid(nt, 1, (unsigned)gz);
   const int64_t zs = zbytes / 4;
 #define LTHM_TAB_CASE(DD)                                                                                            \
