@@ -309,16 +309,26 @@ __global__ __launch_bounds__(256) void cl_diag_k(ClArgs a0) {
   const ClArgs a = head_args(a0, blockIdx.z);
   const int mb = blockIdx.y;
   const Geo g = geo(a, mb);
-  const int lane = threadIdx.x & 63;
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < a.n_max; r += gridDim.x * 4) {
+  const int lane = threadIdx.x & 63, sub = lane & 15;
+  // 16 lanes per row (one 16-B chunk of each operand per lane), 4 rows per wave
+  for (int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4); r - (lane >> 4) < a.n_max;
+       r += gridDim.x * 16) {
     float s = -INFINITY;
-    if (r < g.n && !pad_of(a, g, r)) {
-      const bf16_t* o = out_row(a, g, r);
-      const bf16_t* i = in_row(a, g, r);
-      s = bf2f(o[lane]) * bf2f(i[lane]) + bf2f(o[lane + 64]) * bf2f(i[lane + 64]);
-      s = wave_sum(s) / a.tau;
+    const bool live = r < g.n && !pad_of(a, g, min(r, g.n - 1));
+    float acc = 0.f;
+    if (live) {
+      const u32x4 ov = *reinterpret_cast<const u32x4*>(out_row(a, g, r) + sub * 8);
+      const u32x4 iv = *reinterpret_cast<const u32x4*>(in_row(a, g, r) + sub * 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = fmaf(__uint_as_float(ov[k] << 16), __uint_as_float(iv[k] << 16), acc);
+        acc = fmaf(__uint_as_float(ov[k] & 0xffff0000u), __uint_as_float(iv[k] & 0xffff0000u), acc);
+      }
     }
-    if (lane == 0) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (live) s = acc / a.tau;
+    if (sub == 0 && r < a.n_max) {
       a.diag[(int64_t)mb * a.n_max + r] = s;
       if (a.colb) a.colb[(int64_t)mb * a.n_max + r] = s == -INFINITY ? -INFINITY : -(1.f / a.tau) * 1.4426950408889634f;
       if (a.lq) {
