@@ -1,22 +1,28 @@
-"""Per-dispatch GEMM durations of one C2 training step from a rocprofv3 kernel trace
-(python3 tools/gemm_shapes.py gpurun_out/<dir>/run_kernel_trace.csv): grid size ->
-(tiles, batch, splits) and duration, grouped by kernel and grid."""
-import collections
-import csv
-import sys
-
-rows = list(csv.DictReader(open(sys.argv[1])))
-agg = collections.defaultdict(list)
-for r in rows:
-    k = r["Kernel_Name"]
-    if "gemm_" not in k and "splitk" not in k:
-        continue
-    key = (k.split("(")[0].replace("void lthm::", ""), r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"],
-           r.get("LDS_Block_Size", ""))
-    agg[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-tot = 0.0
-for key, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-    tot += sum(v)
-    print(f"{key[0]:28s} grid=({key[1]},{key[2]},{key[3]}) n={len(v):4d} avg={sum(v) / len(v):8.1f} us "
-          f"total={sum(v) / 1e3:8.2f} ms")
-print(f"total {tot / 1e3:.2f} ms")
+import os, sys, collections
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
+import torch
+import bench
+from recommendations_amd import kernels as K
+seen = collections.Counter()
+orig = K.gemm
+def spy(A, B, M, N, Kd, **kw):
+    seen[(K._GEMM_TAG[-1] if K._GEMM_TAG else "", M, N, Kd, kw.get("a_kcontig", True), kw.get("b_kcontig", True),
+          str(kw.get("out_dtype")), kw.get("act", 0), kw.get("bias") is not None, kw.get("res1") is not None,
+          kw.get("ldc"), kw.get("splits", 1))] += 1
+    return orig(A, B, M, N, Kd, **kw)
+K.gemm = spy
+dev = torch.device("cuda:0")
+cfgd = dict(bench.CONFIGS["c2"])
+cfg, model = bench.build(cfgd, dev)
+opts = model.optimizers_for_param_groups(model.param_groups())
+from recommendations_amd.data import synthetic_lthm_batch
+batch = synthetic_lthm_batch(cfgd["B"], cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=0, device=dev)
+for _ in range(2):
+    seen.clear()
+    out = model(batch); loss, _ = model.train_step(batch, out); loss.backward()
+    for o in opts:
+        o.step(); o.zero_grad(set_to_none=True)
+torch.cuda.synchronize()
+for k, v in sorted(seen.items(), key=lambda x: str(x[0])):
+    if k[0] != "enc":
+        print(v, k)
