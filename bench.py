@@ -402,6 +402,12 @@ def main():
             avg_ms = s["ms"] / s["calls"]
             e = {"calls_per_step": s["calls"] / PROF_STEPS, "avg_ms": round(avg_ms, 4),
                  "share": round(s["ms"] / prof_ms, 4)}
+            if s.get("bytes"):
+                # roofline of the form: the larger of its MFMA time and its compulsory-HBM time
+                pk = FP8_PEAK_TFLOPS if "fp8" in k else BF16_PEAK_TFLOPS
+                t_roof = max(s["work"] / (pk * 1e12), s["bytes"] / (HBM_PEAK_GBS * 1e9))
+                e["flop_per_byte"] = round(s["work"] / s["bytes"], 1)
+                e["frac_roofline"] = round(t_roof / (s["ms"] / 1000.0), 4)
             if s["work"]:
                 rate = s["work"] / (s["ms"] / 1000.0)
                 if s["unit"] == "byte":
@@ -421,14 +427,20 @@ def main():
                           for k, v in enc.items())
             t = sum(v["ms"] for v in enc.values()) / 1000.0
             fl = sum(v["work"] for v in enc.values())
+            roof = sum(max(v["work"] / ((FP8_PEAK_TFLOPS if "fp8" in k else BF16_PEAK_TFLOPS) * 1e12),
+                           v.get("bytes", 0.0) / (HBM_PEAK_GBS * 1e9)) for k, v in enc.items())
             res["encoder_gemm"] = {"bound": "mfma", "achieved": round(fl / t / 1e12, 1), "unit": "TFLOP/s",
                                    "frac": round(at_peak / t, 4),
                                    "peak": FP8_PEAK_TFLOPS if all("fp8" in k for k in enc) else BF16_PEAK_TFLOPS,
+                                   "frac_roofline": round(roof / t, 4),
                                    "flop_per_step": round(fl / PROF_STEPS / 1e12, 3),
                                    "ms_per_step": round(1000 * t / PROF_STEPS, 3),
                                    "forms": sorted(enc),
                                    "note": "all TransformerBlock GEMMs (c_attn, c_proj, c_fc, mlp.c_proj; forward, "
-                                           "dgrad, wgrad), algorithmic 2MNK flop over HIP-event kernel time"}
+                                           "dgrad, wgrad), algorithmic 2MNK flop over HIP-event kernel time; "
+                                           "frac_roofline: per form max(flop / MFMA peak, compulsory HBM bytes / "
+                                           "HBM peak) summed, over the time taken (K = 528k-row weight gradients "
+                                           "sit below the ridge point)"}
         live = timer.summary()
         dom = max(live, key=lambda k: live[k]["ms"])
         s = live[dom]

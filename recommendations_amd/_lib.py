@@ -151,24 +151,25 @@ class KernelTimer:
     ``work`` is the algorithmic bytes / flops the wrapper declares per call."""
 
     def __init__(self, only=None):
-        self.records = []  # (key, ev0, ev1, work, unit)
+        self.records = []  # (key, ev0, ev1, work, unit, bytes)
         self.only = None if only is None else set(only)  # time just these keys (others run untouched)
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for key, e0, e1, work, unit in self.records:
-            s = out.setdefault(key, {"calls": 0, "ms": 0.0, "work": 0.0, "unit": unit})
+        for key, e0, e1, work, unit, nbytes in self.records:
+            s = out.setdefault(key, {"calls": 0, "ms": 0.0, "work": 0.0, "unit": unit, "bytes": 0.0})
             s["calls"] += 1
             s["ms"] += e0.elapsed_time(e1)
             s["work"] += work or 0.0
+            s["bytes"] += nbytes or 0.0
         return out
 
 
 TIMER = None  # type: KernelTimer
 
 
-def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = None) -> None:
+def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = None, _bytes: float = None) -> None:
     lib = load()
     t = TIMER
     if t is not None and (t.only is None or (_key or name) in t.only):
@@ -177,7 +178,7 @@ def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = N
         e0.record()
         rc = getattr(lib, name)(*args)
         e1.record()
-        t.records.append((_key or name, e0, e1, _work, _unit))
+        t.records.append((_key or name, e0, e1, _work, _unit, _bytes))
     else:
         rc = getattr(lib, name)(*args)
     if rc != 0:

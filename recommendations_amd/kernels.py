@@ -315,8 +315,14 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
         d.ab_dtype, d.a_scale, d.b_scale = FP8_E4M3, ptr(a_scale), ptr(b_scale)
     import ctypes
     key = "gemm_fp8" if fp8 else f"gemm_k<{int(a_kcontig)},{int(b_kcontig)}>"
+    # compulsory HBM bytes (each operand read once, C written once, epilogue tensors):
+    # with the flops this places the call on the roofline (bench.py encoder_gemm)
+    nbytes = batch * (M * K * A.element_size() + N * K * B.element_size() + M * N * out.element_size())
+    for t in (aux, aux_out, res1, res2):
+        if t is not None:
+            nbytes += M * N * batch * t.element_size()
     call("lthm_gemm", ctypes.addressof(d), stream(), _key=(_GEMM_TAG[-1] + ":" + key) if _GEMM_TAG else key,
-         _work=2.0 * M * N * K * batch, _unit="flop")
+         _work=2.0 * M * N * K * batch, _unit="flop", _bytes=float(nbytes))
     return out
 
 
