@@ -9,7 +9,7 @@ table-batched KShift lookups -> cap_gradients -> MLP(QuickGELU) -> CLS token.
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 import torch.nn as nn
@@ -79,12 +79,62 @@ class Encoder(nn.Module):
         self.user_context = UserContext(model_config.categorical, model_config.emb_dim) \
             if model_config.categorical.n_features > 0 else None
 
-    def forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        ids = K.flip_tokens(batch["product_ids"].contiguous())
-        labels = K.flip_tokens(batch["labels"].contiguous())
-        ts = K.flip_tokens(batch["timestamp"].contiguous())
+    @torch.no_grad()
+    def prefetch(self, batch: Dict[str, torch.Tensor], ready: Optional["torch.cuda.Event"] = None) -> None:
+        """Pipelined item lookup for a later ``forward(batch)`` (the same
+        ``batch["product_ids"]`` tensor, unmodified): the item table is frozen
+        (product_tower.py:47), so the whole lookup -- for the row-sharded table
+        (C3) the id dedup, the count exchange the host reads and both all_to_alls --
+        can run ahead of the step that consumes it, on a side stream of the device.
+        ``ready`` marks when the ids are valid (default: everything issued so far
+        on the current stream).  Call it where every rank issues it at the same
+        point and no backward is in flight (e.g. after the optimizer step), so the
+        collectives keep one order on all ranks."""
+        raw = batch["product_ids"]
+        K.require_gpu(raw)
+        side = _side_stream(raw.device)
+        if ready is None:
+            ready = torch.cuda.Event()
+            ready.record()
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            ids = K.flip_tokens(raw.contiguous())
+            embs = self.product_emb_module(ids)
+            done = torch.cuda.Event()
+            done.record(side)
+        self._prefetched = (raw, raw._version, ids, embs, done)
+
+    def _item_lookup(self, raw: torch.Tensor):
+        p = getattr(self, "_prefetched", None)
+        if p is not None and p[0] is raw and p[1] == raw._version:
+            self._prefetched = None
+            _, _, ids, embs, done = p
+            cur = torch.cuda.current_stream(raw.device)
+            cur.wait_event(done)
+            ids.record_stream(cur)
+            embs.record_stream(cur)
+            return ids, embs
+        ids = K.flip_tokens(raw.contiguous())
         with torch.no_grad():
             embs = self.product_emb_module(ids)
+        return ids, embs
+
+    def forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        ids, embs = self._item_lookup(batch["product_ids"])
+        labels = K.flip_tokens(batch["labels"].contiguous())
+        ts = K.flip_tokens(batch["timestamp"].contiguous())
         inp, target, mask = self.product_tower(ids, embs)
         ctx = self.user_context(batch["categorical_ids"]) if self.user_context is not None else None
         return self.query_tower(inp, target, mask, labels, ts, ids, ctx)
+
+
+_SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _SIDE_STREAMS[dev] = s
+    return s
+

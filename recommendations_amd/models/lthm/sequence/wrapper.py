@@ -153,6 +153,11 @@ class LTHMModelWrapper(BaseModelWrapper):
     def forward(self, batch: Dict[str, torch.Tensor]):
         return self._model(self.format_inputs(batch))
 
+    def prefetch(self, batch: Dict[str, torch.Tensor], ready=None) -> None:
+        """Run the frozen item-table lookup of a later ``forward(batch)`` now, on a side
+        stream (``Encoder.prefetch``; build-defined, the reference has no pipelining)."""
+        self._model.prefetch(self.format_inputs(batch), ready)
+
     def draw_offsets(self, n_mb: int) -> np.ndarray:
         """wrapper.py:147-153, once per mini-batch: head 0 uses lookahead[0], head i
         draws randint(previous + 1, lookahead[i])."""

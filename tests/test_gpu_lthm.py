@@ -291,3 +291,36 @@ def test_speculative_trim_matches_synchronous(dev):
             for k in ("next_token_emb", "current_token_emb", "current_token_mask"):
                 assert torch.equal(out[k], exp[k]), k
     assert trims[0] == 0 and trims[2] > 0 and trims[4] == 0, trims
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_item_prefetch_matches_inline(dev, sharded):
+    """Encoder.prefetch runs the frozen item-table lookup of a later forward on a side
+    stream (C3: the row-sharded table's dedup / exchange).  The prefetched forward and
+    the training step behind it equal the inline lookup bit for bit; a prefetch made
+    for another ids tensor, or for ids modified since, is not used."""
+    import copy
+    from recommendations_amd.data import synthetic_lthm_batch
+    cfg, m = _model(dev, item_table_sharded=sharded)
+    ref_m = copy.deepcopy(m)
+    a = synthetic_lthm_batch(64, 32, n_cat=2, seed=21, device=dev)
+    b = synthetic_lthm_batch(64, 32, n_cat=2, seed=22, device=dev)
+    with torch.no_grad():
+        m(a), ref_m(a)                                          # first-use table init on both
+        m.prefetch(a)
+        out, exp = m(a), ref_m(a)
+        assert m._model._prefetched is None                     # consumed
+        for k in ("next_token_emb", "current_token_emb", "current_token_mask"):
+            assert torch.equal(out[k], exp[k]), k
+        m.prefetch(a)
+        out, exp = m(b), ref_m(b)                               # different ids tensor: inline lookup
+        assert torch.equal(out["next_token_emb"], exp["next_token_emb"])
+        m.prefetch(b)
+        b["product_ids"][:, -1] = 0                             # modified after the prefetch
+        out, exp = m(b), ref_m(b)
+        assert torch.equal(out["next_token_emb"], exp["next_token_emb"])
+    m.prefetch(a)
+    out, exp = m(a), ref_m(a)
+    la, _ = m.train_step(a, out)
+    lb, _ = ref_m.train_step(a, exp)
+    assert torch.equal(la.detach(), lb.detach())
