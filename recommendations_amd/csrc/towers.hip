@@ -200,9 +200,10 @@ __device__ __forceinline__ bf16x8v ct_tr_frag(const unsigned char* img, int nb, 
 constexpr int PR_TOK = 256;
 constexpr int PR_DMAX = 64;  // Din <= 64 (registers sized by the DM = 32 / 64 instance)
 constexpr int PR_NBMAX = 32;
+constexpr int PR_UNROLL = 2;  // tokens per phase-2 step (4 spills at 3 waves per SIMD)
 
 template <typename TX, int DM>
-__global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int total) {
+__global__ __launch_bounds__(256, 3) void ptower_rows_k(lthm_ptower_desc d, int total) {
   constexpr int LD = DM + 4;
   __shared__ __attribute__((aligned(16))) float xs2[PR_TOK * LD];
   __shared__ uint8_t msk[PR_TOK];
@@ -229,7 +230,15 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
     }
   }
   const TX* x = reinterpret_cast<const TX*>(d.x);
+  const bool full = Din == DM;  // the chunk's x rows stage through LDS with lane-linear loads
   for (int64_t t0 = (int64_t)blockIdx.x * PR_TOK; t0 < d.n; t0 += (int64_t)gridDim.x * PR_TOK) {
+    const int cnt = (int)min((int64_t)PR_TOK, d.n - t0);
+    if (full) {
+      // [cnt, DM] contiguous elements: consecutive lanes read consecutive elements
+      const TX* xc = x + t0 * DM;
+      for (int e = tid; e < cnt * DM; e += 256) xs2[(e / DM) * LD + (e % DM)] = Elem<TX>::ld(xc + e);
+      __syncthreads();
+    }
     {
       const int64_t t = t0 + tid;
       if (t < d.n) {
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
         float ss = 0.f;
 #pragma unroll
         for (int i = 0; i < DM; ++i) {
-          v[i] = (i < Din) ? Elem<TX>::ld(x + t * Din + i) : 0.f;
+          v[i] = (i < Din) ? (full ? xs2[tid * LD + i] : Elem<TX>::ld(x + t * Din + i)) : 0.f;
           ss += v[i] * v[i];
         }
         const float nrm = sqrtf(ss);
@@ -248,7 +257,17 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
         for (int i = 0; i < DM; ++i) {
           v[i] = v[i] / den;
           ss2 += v[i] * v[i];
-          if (i < Din && d.xn_out) reinterpret_cast<bf16_t*>(d.xn_out)[t * Din + i] = f2bf(v[i]);
+        }
+        if (d.xn_out) {
+          bf16_t* xo = reinterpret_cast<bf16_t*>(d.xn_out) + t * Din;
+          if (full) {
+#pragma unroll
+            for (int i = 0; i < DM; i += 8) store_vec<bf16_t, 8>(xo + i, v + i);
+          } else {
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+              if (i < Din) xo[i] = f2bf(v[i]);
+          }
         }
         const float den2 = fmaxf(sqrtf(ss2), 1e-12f);
 #pragma unroll
@@ -265,8 +284,36 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
     }
     __syncthreads();
     if (mine) {
-      const int cnt = (int)min((int64_t)PR_TOK, d.n - t0);
-      for (int tt = 0; tt < cnt; ++tt) {
+      // PU tokens per step: independent FMA chains (each in the sequential i order
+      // of the one-token form) keep the broadcast LDS reads in flight
+      constexpr int PU = PR_UNROLL;
+      int tt = 0;
+      for (; tt + PU <= cnt; tt += PU) {
+        float z[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) z[u] = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; i += 4) {
+          if (i < Din) {
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+              const f32x4 q = *reinterpret_cast<const f32x4*>(xs2 + (tt + u) * LD + i);
+              z[u] = fmaf(q[0], Rc[i], z[u]);
+              z[u] = fmaf(q[1], Rc[i + 1], z[u]);
+              z[u] = fmaf(q[2], Rc[i + 2], z[u]);
+              z[u] = fmaf(q[3], Rc[i + 3], z[u]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+          int bk = 0;
+#pragma unroll
+          for (int q = 0; q < PR_NBMAX; ++q) bk += (gr[q] < z[u]) ? 1 : 0;  // bucketize(right=False)
+          d.rows_out[(t0 + tt + u) * total + tid] = msk[tt + u] ? (uint16_t)0xffff : (uint16_t)(rbase + bk);
+        }
+      }
+      for (; tt < cnt; ++tt) {
         const float* xr = xs2 + tt * LD;
         float z = 0.f;
 #pragma unroll
@@ -274,9 +321,9 @@ __global__ __launch_bounds__(256) void ptower_rows_k(lthm_ptower_desc d, int tot
           if (i < Din) {
             const f32x4 q = *reinterpret_cast<const f32x4*>(xr + i);
             z = fmaf(q[0], Rc[i], z);
-            if (i + 1 < Din) z = fmaf(q[1], Rc[i + 1], z);
-            if (i + 2 < Din) z = fmaf(q[2], Rc[i + 2], z);
-            if (i + 3 < Din) z = fmaf(q[3], Rc[i + 3], z);
+            z = fmaf(q[1], Rc[i + 1], z);
+            z = fmaf(q[2], Rc[i + 2], z);
+            z = fmaf(q[3], Rc[i + 3], z);
           }
         }
         int bk = 0;
