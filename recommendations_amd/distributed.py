@@ -163,7 +163,11 @@ def exchange_rows(uniq: torch.Tensor, shard: torch.Tensor) -> torch.Tensor:
 
 def step_flags(stop: bool, loss: torch.Tensor) -> torch.Tensor:
     """[stop, non-finite loss] MAX-reduced over ranks in one collective (no host sync here)."""
-    f = torch.stack([torch.tensor(float(stop), device=loss.device), (~torch.isfinite(loss.detach())).float().reshape(())])
+    # no host->device copy: torch.tensor(x, device=gpu) is a pageable upload that blocks
+    # the host until the stream reaches it, i.e. until the whole backward has run, after
+    # which the GPU idled ~1.2 ms per C2 step while the host issued the optimizer
+    nf = (~torch.isfinite(loss.detach().reshape(1))).float()
+    f = torch.cat([nf.new_full((1,), float(stop)), nf])
     if world_size() > 1:
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
     return f

@@ -599,12 +599,28 @@ def adamw_multi_(ps, gs, ms, vs, lr, betas, eps, wd, step, grad_scale=1.0):
             _need(t, p.numel(), nm)
         _check(all(t.dtype == torch.float32 and t.is_contiguous() for t in (p, g, m, v)),
                "adamw_multi_ takes contiguous fp32 tensors")
+    plan = adamw_multi_plan(ps, gs, ms, vs)
+    adamw_multi_run(plan, lr, betas, eps, wd, step, grad_scale)
+
+
+def adamw_multi_plan(ps, gs, ms, vs):
+    """The pointer / count arrays of one lthm_adamw_multi call (checked by the caller),
+    kept by FusedAdamW across steps while the tensors stay where they are."""
+    import ctypes
+    n = len(ps)
     arr = lambda ts: (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in ts])  # noqa: E731
-    cnt = (ctypes.c_int64 * max(n, 1))(*[p.numel() for p in ps])
-    call("lthm_adamw_multi", n, ctypes.cast(arr(ps), ctypes.c_void_p), ctypes.cast(arr(gs), ctypes.c_void_p),
-         ctypes.cast(arr(ms), ctypes.c_void_p), ctypes.cast(arr(vs), ctypes.c_void_p),
-         ctypes.cast(cnt, ctypes.c_void_p), lr, betas[0], betas[1], eps, wd, step, grad_scale, stream(),
-         _key="lthm_adamw", _work=28.0 * sum(p.numel() for p in ps), _unit="byte")
+    arrs = (arr(ps), arr(gs), arr(ms), arr(vs), (ctypes.c_int64 * max(n, 1))(*[p.numel() for p in ps]))
+    # the moment buffers are held (their addresses are baked in); parameters and gradients
+    # are not (holding last step's gradients would move the next step's), so a user of a
+    # kept plan must check their addresses first, as FusedAdamW.step does
+    return n, (arrs, list(ms), list(vs)), tuple(ctypes.cast(a, ctypes.c_void_p) for a in arrs), \
+        28.0 * sum(p.numel() for p in ps)
+
+
+def adamw_multi_run(plan, lr, betas, eps, wd, step, grad_scale=1.0):
+    n, _, (pp, pg, pm, pv, pc), work = plan
+    call("lthm_adamw_multi", n, pp, pg, pm, pv, pc, lr, betas[0], betas[1], eps, wd, step, grad_scale, stream(),
+         _key="lthm_adamw", _work=work, _unit="byte")
 
 
 def adagrad_(p, g, s, lr, lr_decay, eps, wd, step, zero_grad=False):

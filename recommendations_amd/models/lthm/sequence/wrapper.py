@@ -32,6 +32,7 @@ from ....optim import FusedAdamW, SparseRowAdamW
 from .encoder import Encoder
 
 NSTAT_BASE = 7
+_KS_DEV: Dict[tuple, torch.Tensor] = {}  # (metric ks, device) -> int32 device copy
 
 
 class ContrastiveLossFn(torch.autograd.Function):
@@ -61,7 +62,9 @@ class ContrastiveLossFn(torch.autograd.Function):
         rank = torch.empty((NH, n_mb, n_max), dtype=torch.int32, device=dev)
         nstat = NSTAT_BASE + len(ks)
         stats = torch.empty((NH, n_mb, nstat), **f32)
-        ks_dev = torch.tensor(ks, dtype=torch.int32).to(dev, non_blocking=True)
+        ks_dev = _KS_DEV.get((tuple(ks), dev))  # uploaded once per (ks, device), not per step
+        if ks_dev is None:
+            ks_dev = _KS_DEV[(tuple(ks), dev)] = torch.tensor(ks, dtype=torch.int32).to(dev)
         lqc = torch.empty((NH, n_mb, n_max), **f32) if logq is not None else None
         # every head in one set of launches (head h's buffers at h * n_mb * n_max)
         d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, 0, De, mbs, n_mb, n_max, tau, offsets_dev,

@@ -19,13 +19,34 @@ from . import kernels as K
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self._plans = {}
+
+    def load_state_dict(self, state_dict):
+        self._plans = {}  # the plans point at the moment buffers being replaced
+        super().load_state_dict(state_dict)
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
         """One multi-tensor launch per (param group, step count) bucket of up to 48
         tensors (lthm_adamw_multi) instead of one launch per parameter."""
         loss = closure() if closure is not None else None
-        for g in self.param_groups:
+        fast = self.__dict__.setdefault("_plans", {})  # (set in __init__; kept for unpickled optimizers)
+        for gi, g in enumerate(self.param_groups):
+            # steady state: the same parameters, gradients at the same addresses and one
+            # shared step count -> reuse the previous step's pointer arrays (the per-tensor
+            # checks and ctypes packing cost ~0.6 ms of host time per C2 step)
+            live = [p for p in g["params"] if p.grad is not None]
+            key = tuple((id(p), p.data_ptr(), p.grad.data_ptr()) for p in live)
+            hit = fast.get(gi)
+            if hit is not None and hit[0] == key:
+                step = hit[2] + 1
+                for p in live:
+                    self.state[p]["step"] = step
+                fast[gi] = (key, hit[1], step)
+                K.adamw_multi_run(hit[1], g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
+                                  grad_scale=grad_scale)
+                continue
+            fast.pop(gi, None)
             buckets = {}
             for p in g["params"]:
                 if p.grad is None:
@@ -45,6 +66,9 @@ class FusedAdamW(torch.optim.Optimizer):
             for step, (ps, gs, ms, vs) in buckets.items():
                 K.adamw_multi_(ps, gs, ms, vs, g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
                                grad_scale=grad_scale)
+            if len(buckets) == 1 and all(p.grad.is_contiguous() for p in live):
+                (step, (ps, gs, ms, vs)), = buckets.items()
+                fast[gi] = (key, K.adamw_multi_plan(ps, gs, ms, vs), step)
         return loss
 
 

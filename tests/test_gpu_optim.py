@@ -31,6 +31,41 @@ def test_fused_adamw_multi_matches_torch(dev):
     assert st["step"] == 2 and o1.state[mine[6]]["step"] == 3
 
 
+def test_fused_adamw_kept_plan(dev):
+    """Gradients that stay at the same addresses (steady-state training) take the kept
+    pointer plan; the result still matches torch step for step, a load_state_dict in
+    between drops the plan, and a moved gradient falls back to the checked path."""
+    from recommendations_amd.optim import FusedAdamW
+    torch.manual_seed(1)
+    shapes = [(int(s),) for s in torch.randint(1, 3000, (60,))] + [(256, 64)]
+    ps = [torch.randn(s) for s in shapes]
+    mine = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    kw = dict(lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=1e-2)
+    o1, o2 = FusedAdamW(mine, **kw), torch.optim.AdamW(ref, **kw, foreach=False)
+    grads = [torch.empty(s, device=dev) for s in shapes]
+    for a, gbuf in zip(mine, grads):
+        a.grad = gbuf
+    for it in range(6):
+        gs = [torch.randn(s) for s in shapes]
+        for a, b, gr in zip(mine, ref, gs):
+            a.grad.copy_(gr.to(dev))
+            b.grad = gr.clone()
+        if it == 3:
+            o1.load_state_dict(o1.state_dict())
+            assert not o1._plans
+        if it == 4:  # one gradient moves: the checked path runs and a new plan is kept
+            mine[7].grad = mine[7].grad.clone()
+        o1.step()
+        o2.step()
+        if it in (1, 2, 5):
+            assert o1._plans, "steady-state step did not keep a plan"
+    for a, b in zip(mine, ref):
+        d = (a.detach().cpu() - b.detach()).abs().max()
+        assert float(d) <= 1e-6 * max(1.0, float(b.detach().abs().max()))
+    assert all(o1.state[p]["step"] == 6 for p in mine)
+
+
 def test_cast_multi_bf16_exact(dev):
     """lthm_cast_multi_bf16 (one launch for many fp32 tensors) rounds exactly as torch's bf16 cast,
     including sizes that are not a multiple of 4 and unaligned views."""
