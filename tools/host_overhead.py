@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--find-sync", action="store_true",
                     help="run one step under torch.cuda.set_sync_debug_mode('error') and print where it syncs")
+    ap.add_argument("--callsites", default="",
+                    help="comma-separated C-ABI names (e.g. lthm_fill_f32,lthm_cast): count their "
+                         "callers (first frame outside kernels.py / _lib.py) over one step")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     cfgd = dict(bench.CONFIGS[args.config])
@@ -55,6 +58,30 @@ def main():
         finally:
             torch.cuda.set_sync_debug_mode("default")
         torch.cuda.synchronize()
+    if args.callsites:
+        import collections
+        import traceback
+        from recommendations_amd import _lib
+        want = set(args.callsites.split(","))
+        seen = collections.Counter()
+        real = _lib.call
+
+        def counting(name, *a, **kw):
+            if name in want:
+                fr = [f for f in traceback.extract_stack()[:-1]
+                      if not f.filename.endswith(("kernels.py", "_lib.py"))]
+                f = fr[-1]
+                seen[(name, f"{os.path.relpath(f.filename)}:{f.lineno}")] += 1
+            return real(name, *a, **kw)
+        mods = [m for m in list(sys.modules.values()) if getattr(m, "call", None) is real]
+        for m in mods:
+            m.call = counting
+        step()
+        torch.cuda.synchronize()
+        for m in mods:
+            m.call = real
+        for (name, site), c in seen.most_common():
+            print(f"callsite {c:4d}  {name:24s} {site}")
     # host time per phase in steady state (a phase that blocks on the GPU shows up here)
     phases = {"forward": 0.0, "train_step": 0.0, "backward": 0.0, "optimizer": 0.0}
     t0 = time.perf_counter()
