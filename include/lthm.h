@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 23 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 24 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -467,7 +467,8 @@ typedef struct lthm_contrastive_desc {
   int32_t De;
   int32_t mb_size;        /* train_mini_batch_size (32) */
   int32_t n_mb;
-  int32_t n_max;          /* >= mb_size * T, <= 4096 */
+  int32_t n_max;          /* >= mb_size * T, a multiple of 64, n_max * T < 2^32 (no other limit: val_step
+                             runs the whole batch as one mini-batch, wrapper.py:75-80) */
   float tau;              /* softmax_temperature */
   const int32_t* offsets; /* [n_mb, n_heads] lookahead offset per mini-batch and head */
   float* lse;             /* [n_mb, n_max] per-row buffers (this head) */
@@ -491,7 +492,13 @@ typedef struct lthm_contrastive_desc {
   int32_t heads_run;      /* forward: heads head .. head + heads_run - 1 in one set of launches (0 or 1: one) */
   int64_t head_stride;    /* with heads_run > 1: elements between consecutive heads' lse / pos / cnt / rank /
                              diag / w / logq_col buffers; stats rows advance by n_mb * nstat */
+  void* stats_ws;         /* forward: device workspace of lthm_contrastive_ws_bytes(n_mb, n_max, heads_run)
+                             bytes (rank histograms + per-block partial sums) */
+  int64_t stats_ws_bytes;
 } lthm_contrastive_desc;
+
+/* bytes of lthm_contrastive_desc.stats_ws for one forward launch (-1: invalid sizes) */
+int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads);
 
 /* Forward for one head (or heads_run consecutive heads) over all mini-batches.  stats [n_mb, nstat] f32 per head:
  * {mean CE, used rows, mean negatives, min negatives, mean rank, median rank,

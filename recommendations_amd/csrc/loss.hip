@@ -258,7 +258,7 @@ struct Geo {
   int64_t b0;
   uint64_t Lm;  // ceil(2^32 / L): seq(c) = c / L by one 32 x 64 multiply (exact for c < 2^32 / L)
 };
-// sequence index c / L of a row / column c < n <= 4096
+// sequence index c / L of a row / column c < n (exact while n L < 2^32, cl_check)
 __device__ __forceinline__ int seq_of(const Geo& g, int c) {
   return (int)(((uint64_t)(uint32_t)c * g.Lm) >> 32);
 }
@@ -367,129 +367,174 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
   }
 }
 
-// ---------------------------------------------------------------- stats (one block per mini-batch)
-// per (mb): used rows, mean CE, weights w_r = used / (U * n_mb_total); metrics.
-// stats[mb][*] = {loss, used, sum_negatives, min_negatives, sum_rank, median_rank, hits@k...}
-__global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, float* __restrict__ stats, int nstat, const int* __restrict__ ks,
-                                                  int nk, float loss_scale, float* __restrict__ wout) {
+// ---------------------------------------------------------------- stats
+// Three launches, any n (the rank histogram and the per-row flags live in HBM, no
+// per-block limit on the rows of a mini-batch):
+//  cl_rowstats_k  (CL_SROWS rows per block): per row, used = not pad and >= 1 finite
+//                 negative (wrapper.py:193-201); block partial sums {CE, negatives, ranks,
+//                 used, min negatives} in fixed order (f64), used flag into w, one integer
+//                 atomic per used row into the rank histogram (order-free, deterministic);
+//  cl_stats_k     (one block per (mini-batch, head)): the partials in fixed order, hits@k as
+//                 prefix counts of the histogram, the median rank from its order statistics;
+//  cl_wscale_k    row weights w_r = used_r * loss_scale / U.
+// stats[mb][*] = {mean CE, used, mean negatives, min negatives, mean rank, median rank,
+//                 offset, hits@k...}
+constexpr int CL_SROWS = 2048;
+constexpr int CL_NPART = 5;  // f64 partials per (head, mb, block)
+
+__device__ __forceinline__ double block_dsum(double v, double* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const double t = red[0];
+  __syncthreads();
+  return t;
+}
+
+// workspace: [heads][n_mb][n_max] int32 histogram, then [heads][n_mb][nblk][CL_NPART] f64
+__global__ __launch_bounds__(256) void cl_rowstats_k(ClArgs a0, int* __restrict__ hist, double* __restrict__ part) {
   const ClArgs a = head_args(a0, blockIdx.z);
-  stats += (int64_t)blockIdx.z * a0.n_mb * nstat;
-  wout += (int64_t)blockIdx.z * a0.head_stride;
-  constexpr int RPT = 4096 / 256;  // rows per thread (n <= 4096)
-  __shared__ int hist[4096];       // histogram of the used rows' ranks (rank < n <= 4096)
-  __shared__ float red[256];
-  __shared__ int ired[256];
-  const int mb = blockIdx.x;
+  const int mb = blockIdx.y, nblk = gridDim.x;
+  const int64_t hm = (int64_t)blockIdx.z * a0.n_mb + mb;
+  hist += hm * a0.n_max;
+  part += (hm * nblk + blockIdx.x) * CL_NPART;
   const Geo g = geo(a, mb);
   const int tid = threadIdx.x;
-  float ls = 0.f, neg = 0.f, rks = 0.f;
-  int used = 0, mneg = 0x7fffffff;
   const int64_t base = (int64_t)mb * a.n_max;
-  for (int i = tid; i < 4096; i += 256) hist[i] = 0;
-  // one pass over the rows, all loads of a thread's rows in flight together;
-  // the used flags and ranks stay in registers for the later passes
-  int rkv[RPT];
-  unsigned umask = 0u;
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int r = tid + 256 * i;
-    rkv[i] = 0x7fffffff;
+  float ls = 0.f, neg = 0.f, rks = 0.f;  // <= 8 rows per thread: integer sums stay exact
+  int used = 0, mneg = 0x7fffffff;
+  for (int i = 0; i < CL_SROWS / 256; ++i) {
+    const int r = blockIdx.x * CL_SROWS + tid + 256 * i;
+    if (r >= a.n_max) break;
+    bool u = false;
     if (r < g.n) {
       const int nn = a.cnt[base + r] - 1;
-      const bool u = !pad_of(a, g, r) && nn > 0;
+      u = !pad_of(a, g, r) && nn > 0;
       if (u) {
-        umask |= 1u << i;
-        rkv[i] = a.rank[base + r];
+        const int rk = a.rank[base + r];
         ls += a.lse[base + r] - a.pos[base + r];
         neg += (float)nn;
-        rks += (float)rkv[i];
+        rks += (float)rk;
         used += 1;
         mneg = min(mneg, nn);
+        atomicAdd(hist + rk, 1);
       }
     }
+    a.colb[base + r] = u ? 1.f : 0.f;  // used flag into w (colb = w in the forward); cl_wscale_k scales it
   }
+  __shared__ double red[256];
+  __shared__ int imn[256];
+  const double Ls = block_dsum(ls, red), Ns = block_dsum(neg, red), Rs = block_dsum(rks, red);
+  const double U = block_dsum(used, red);
+  imn[tid] = mneg;
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < RPT; ++i)
-    if (umask & (1u << i)) atomicAdd(&hist[rkv[i]], 1);
-  // block reductions
-  auto fsum = [&](float v) {
-    red[tid] = v; __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) { if (tid < s) red[tid] += red[tid + s]; __syncthreads(); }
-    const float t = red[0]; __syncthreads(); return t;
-  };
-  auto isum = [&](int v) {
-    ired[tid] = v; __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) { if (tid < s) ired[tid] += ired[tid + s]; __syncthreads(); }
-    const int t = ired[0]; __syncthreads(); return t;
-  };
-  auto imin = [&](int v) {
-    ired[tid] = v; __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) { if (tid < s) ired[tid] = min(ired[tid], ired[tid + s]); __syncthreads(); }
-    const int t = ired[0]; __syncthreads(); return t;
-  };
-  const float Ls = fsum(ls), Ns = fsum(neg), Rs = fsum(rks);
-  const int U = isum(used), Mn = imin(mneg);
-  const float wr = U > 0 ? loss_scale / (float)U : 0.f;
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int r = tid + 256 * i;
-    if (r < a.n_max) wout[base + r] = (umask & (1u << i)) ? wr : 0.f;
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) imn[tid] = min(imn[tid], imn[tid + s]);
+    __syncthreads();
   }
-  // hits@k: rank < min(k, min negatives)
-  float* st = stats + (int64_t)mb * nstat;
+  if (tid == 0) {
+    part[0] = Ls; part[1] = Ns; part[2] = Rs; part[3] = U; part[4] = (double)imn[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, const int* __restrict__ hist,
+                                                  const double* __restrict__ part, int nblk, float* __restrict__ stats,
+                                                  int nstat, const int* __restrict__ ks, int nk) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  const int mb = blockIdx.x;
+  const int64_t hm = (int64_t)blockIdx.z * a0.n_mb + mb;
+  hist += hm * a0.n_max;
+  part += hm * nblk * CL_NPART;
+  float* st = stats + hm * nstat;
+  const Geo g = geo(a, mb);
+  const int tid = threadIdx.x;
+  __shared__ double red[256];
+  __shared__ int ired[256];
+  __shared__ int sel[2];
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  double mn = 2147483647.0;
+  for (int b = tid; b < nblk; b += 256) {  // fixed order: thread tid folds blocks tid, tid + 256, ...
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] += part[b * CL_NPART + k];
+    mn = fmin(mn, part[b * CL_NPART + 4]);
+  }
+  const double Ls = block_dsum(v[0], red), Ns = block_dsum(v[1], red), Rs = block_dsum(v[2], red);
+  const int U = (int)block_dsum(v[3], red);
+  ired[tid] = (int)mn;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) ired[tid] = min(ired[tid], ired[tid + s]);
+    __syncthreads();
+  }
+  const int Mn = ired[0];
+  __syncthreads();
+  // hits@k (wrapper.py:235-238): rank < min(k, min negatives), a prefix count of the histogram
   for (int q = 0; q < nk; ++q) {
     const int kq = min(ks[q], Mn);
     int h = 0;
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) h += (rkv[i] < kq) ? 1 : 0;  // unused rows hold INT_MAX
-    h = isum(h);
-    if (tid == 0) st[7 + q] = U > 0 ? (float)h / (float)U : 0.f;
+    for (int i = tid; i < kq && i < a.n_max; i += 256) h += hist[i];
+    const int H = (int)block_dsum(h, red);
+    if (tid == 0) st[7 + q] = U > 0 ? (float)((double)H / U) : 0.f;
   }
-  // median of the used ranks (torch.quantile(0.5): linear interpolation between the
-  // order statistics lo and hi) from the rank histogram: this thread's 16 bins,
-  // an exclusive scan of the 256 bin-group totals, then the owner of each
-  // order statistic reports its value
-  const int p_lo = U > 0 ? (int)floorf(0.5f * (float)(U - 1)) : 0;
+  // median of the used ranks (torch.quantile(0.5): linear interpolation between the order
+  // statistics p_lo and p_hi): each thread owns a contiguous run of bins, an exclusive scan of
+  // the run totals, then the owner of each order statistic reports its bin
+  const int p_lo = U > 0 ? (U - 1) / 2 : 0;
   const int p_hi = U > 0 ? min(p_lo + 1, U - 1) : 0;
-  int cnt16 = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) cnt16 += hist[tid * 16 + i];
-  ired[tid] = cnt16;
+  const int nb = g.n > 0 ? g.n : 1;  // ranks < n
+  const int per = (nb + 255) / 256;
+  const int i0 = min(tid * per, nb), i1 = min(i0 + per, nb);
+  int csum = 0;
+  for (int i = i0; i < i1; ++i) csum += hist[i];
+  ired[tid] = csum;
+  if (tid < 2) sel[tid] = 0;
   __syncthreads();
   for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan
-    const int v = tid >= o ? ired[tid - o] : 0;
+    const int t = tid >= o ? ired[tid - o] : 0;
     __syncthreads();
-    ired[tid] += v;
+    ired[tid] += t;
     __syncthreads();
   }
-  int run = ired[tid] - cnt16;  // order statistics before this thread's bins
-  __syncthreads();
-  float* sel = red;  // red[0] = value at p_lo, red[1] = value at p_hi
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = hist[tid * 16 + i];
-    if (c > 0) {
-      if (p_lo >= run && p_lo < run + c) sel[0] = (float)(tid * 16 + i);
-      if (p_hi >= run && p_hi < run + c) sel[1] = (float)(tid * 16 + i);
+  int run = ired[tid] - csum;
+  if (U > 0 && p_hi >= run && p_lo < run + csum) {
+    for (int i = i0; i < i1; ++i) {
+      const int c = hist[i];
+      if (c > 0) {
+        if (p_lo >= run && p_lo < run + c) sel[0] = i;
+        if (p_hi >= run && p_hi < run + c) sel[1] = i;
+      }
+      run += c;
     }
-    run += c;
   }
   __syncthreads();
   if (tid == 0) {
-    st[0] = U > 0 ? Ls / (float)U : 0.f;
+    st[0] = U > 0 ? (float)(Ls / U) : 0.f;
     st[1] = (float)U;
-    st[2] = U > 0 ? Ns / (float)U : 0.f;
+    st[2] = U > 0 ? (float)(Ns / U) : 0.f;
     st[3] = (float)(U > 0 ? Mn : 0);
-    st[4] = U > 0 ? Rs / (float)U : 0.f;
+    st[4] = U > 0 ? (float)(Rs / U) : 0.f;
     float med = 0.f;
     if (U > 0) {
       const float p = 0.5f * (float)(U - 1);
-      med = sel[0] + (p - (float)p_lo) * (sel[1] - sel[0]);
+      med = (float)sel[0] + (p - (float)p_lo) * (float)(sel[1] - sel[0]);
     }
     st[5] = med;
     st[6] = (float)g.off;
   }
+}
+
+__global__ __launch_bounds__(256) void cl_wscale_k(ClArgs a0, const float* __restrict__ stats, int nstat,
+                                                   float loss_scale) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  const int mb = blockIdx.y;
+  const float U = stats[((int64_t)blockIdx.z * a0.n_mb + mb) * nstat + 1];
+  const float wr = U > 0.f ? loss_scale / U : 0.f;
+  float* w = a.colb + (int64_t)mb * a.n_max;  // = the row weights w in the forward
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < a.n_max; r += gridDim.x * 256) w[r] = w[r] != 0.f ? wr : 0.f;
 }
 
 // ---------------------------------------------------------------- tile engine
@@ -561,7 +606,7 @@ struct RowCursor {
   __device__ __forceinline__ void stage(unsigned char* img, int n, int w, int lane) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const void* src = (c + 4 * k < n) ? (const void*)(base + (b[k] * sb + t[k] * st + choff[k]))
+      const void* src = (c + 4 * k < n) ? (const void*)(base + ((int64_t)b[k] * sb + t[k] * st + choff[k]))
                                         : (const void*)(cl_zero_row + 16 * (lane & 15));
       glds16(src, img + (16 * w + 4 * k) * 256);
       t[k] += r64;
@@ -1047,11 +1092,19 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
 
 static int cl_check(const lthm_contrastive_desc* d) {
   if (!d || d->De != DE || d->B <= 0 || d->T <= 0 || d->mb_size <= 0 || d->n_mb <= 0) return 1;
-  if ((int64_t)d->mb_size * d->T > d->n_max || d->n_max > 4096) return 1;
-  if ((int64_t)d->mb_size * (d->T + 1) * d->n_heads * DE >= (1ll << 31)) return 1;  // RowCursor offsets
+  if ((int64_t)d->mb_size * d->T > d->n_max || d->n_max % 64 != 0) return 1;
+  if ((int64_t)d->n_max * d->T >= (1ll << 32)) return 1;  // seq_of: c / L by one 32 x 64 multiply
   if (d->head < 0 || d->head >= d->n_heads) return 1;
   if (d->logq && (!d->logq_col || d->logq_stride < d->T)) return 1;
   return 0;
+}
+
+static int64_t cl_stats_blocks(int32_t n_max) { return (n_max + CL_SROWS - 1) / CL_SROWS; }
+
+extern "C" int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads) {
+  if (n_mb <= 0 || n_max <= 0 || heads <= 0) return -1;
+  const int64_t hm = (int64_t)heads * n_mb;
+  return hm * n_max * 4 + ((hm * n_max * 4) % 8) + hm * cl_stats_blocks(n_max) * CL_NPART * 8;
 }
 
 template <typename TX>
@@ -1120,9 +1173,15 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   const int nrun = d->heads_run > 1 ? d->heads_run : 1;
   LTHM_REQUIRE(d->head + nrun <= d->n_heads);
   LTHM_REQUIRE(nrun == 1 || d->head_stride >= (int64_t)d->n_mb * d->n_max);
+  const int64_t ws = lthm_contrastive_ws_bytes(d->n_mb, d->n_max, nrun);
+  LTHM_REQUIRE(d->stats_ws && d->stats_ws_bytes >= ws);
   ClArgs a = cl_args(d);
-  a.colb = d->w;  // scratch until cl_stats_k writes the row weights
+  a.colb = d->w;  // scratch until cl_rowstats_k writes the used flags
   hipStream_t s = (hipStream_t)stream;
+  const int64_t hm = (int64_t)nrun * d->n_mb;
+  int* hist = (int*)d->stats_ws;
+  double* part = (double*)((char*)d->stats_ws + ((hm * d->n_max * 4 + 7) / 8) * 8);
+  if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
   hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb, nrun), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
@@ -1133,8 +1192,14 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb, 1, nrun), dim3(256), 0, s, a, stats, nstat, (const int*)ks, nk,
-                     loss_scale, (float*)d->w);
+  const int nblk = (int)cl_stats_blocks(d->n_max);
+  hipLaunchKernelGGL(cl_rowstats_k, dim3(nblk, d->n_mb, nrun), dim3(256), 0, s, a, hist, part);
+  LTHM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cl_stats_k, dim3(d->n_mb, 1, nrun), dim3(256), 0, s, a, (const int*)hist, (const double*)part,
+                     nblk, stats, nstat, (const int*)ks, nk);
+  LTHM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cl_wscale_k, dim3(min((d->n_max + 255) / 256, 64), d->n_mb, nrun), dim3(256), 0, s, a,
+                     (const float*)stats, nstat, loss_scale);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

@@ -16,6 +16,7 @@ real data parallelism:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Iterable, List, Optional
 
@@ -47,11 +48,20 @@ class GradBucketAllReduce:
 
     Parameters are dealt into ~``bucket_bytes`` buckets in reverse registration order
     (roughly the order the backward produces their gradients).  A post-accumulate-grad
-    hook counts each bucket's ready gradients; the moment the last one lands, the bucket
-    is flattened into its persistent buffer and its all-reduce is launched asynchronously
-    (RCCL runs it on its own stream while the backward's kernels continue).  ``__call__``
-    (after ``loss.backward()``) launches any bucket whose parameters received no gradient
-    this step, waits for every all-reduce and writes the averages back."""
+    hook records each gradient that lands; the moment every parameter of a bucket has
+    received exactly one, the bucket is flattened into a buffer and its all-reduce is
+    launched asynchronously (RCCL runs it on its own stream while the backward's kernels
+    continue).  ``__call__`` (after the last ``loss.backward()`` of the step) launches any
+    bucket that did not complete that way, waits for every all-reduce and writes the
+    averages back.
+
+    Gradient accumulation (the reference's ``gradient_accumulation_steps``,
+    accelerate_training_strategy.py:144, 351): run the backward of every micro-batch but
+    the last inside ``with ar.no_sync():`` (hooks ignored, as DDP's ``no_sync``), so the
+    launches see the accumulated ``.grad``.  A bucket whose hooks fired more than once per
+    parameter (an accumulating backward outside ``no_sync``) or that was launched in an
+    earlier, never-reduced step is re-flattened from the current ``.grad`` in
+    ``__call__``: the result is always the average of what ``.grad`` holds then."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 64 << 20, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
@@ -68,17 +78,37 @@ class GradBucketAllReduce:
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
-        self._ready = [0] * len(self.buckets)
-        self._work: List[Optional[tuple]] = [None] * len(self.buckets)
+        self._sync = True
+        self._reset()
         self._hooks = []
         if overlap and world_size() > 1 and hasattr(torch.Tensor, "register_post_accumulate_grad_hook"):
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
+    def _reset(self) -> None:
+        self._fires = [0] * len(self.buckets)  # hook firings since the last __call__
+        self._seen: List[set] = [set() for _ in self.buckets]
+        self._work: List[Optional[tuple]] = [None] * len(self.buckets)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside accumulate gradients without launching any all-reduce."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def _complete(self, i: int) -> bool:
+        return self._fires[i] == len(self.buckets[i]) and len(self._seen[i]) == len(self.buckets[i])
+
     def _on_grad(self, p: torch.Tensor) -> None:
+        if not self._sync:
+            return
         i = self._bucket_of[id(p)]
-        self._ready[i] += 1
-        if self._ready[i] == len(self.buckets[i]) and self._work[i] is None:
+        self._fires[i] += 1
+        self._seen[i].add(id(p))
+        if self._work[i] is None and self._complete(i):
             self._launch(i)
 
     def _launch(self, i: int) -> None:
@@ -92,9 +122,13 @@ class GradBucketAllReduce:
     def __call__(self):
         ws = world_size()
         if ws == 1:
+            self._reset()
             return
         for i in range(len(self.buckets)):
-            if self._work[i] is None:  # no hook fired for the whole bucket this step
+            w = self._work[i]
+            if w is None or not self._complete(i):
+                if w:  # launched on gradients that later backward passes changed: drop it
+                    w[2].wait()
                 self._launch(i)
         for i, w in enumerate(self._work):
             if w:
@@ -103,8 +137,7 @@ class GradBucketAllReduce:
                 flat.div_(ws)
                 for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
                     g.copy_(f)
-        self._ready = [0] * len(self.buckets)
-        self._work = [None] * len(self.buckets)
+        self._reset()
 
 
 def all_gather_rows(t: torch.Tensor) -> torch.Tensor:

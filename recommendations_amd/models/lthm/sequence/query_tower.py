@@ -212,12 +212,17 @@ class QueryTower(nn.Module):
             done = torch.cuda.Event()
             done.record(side)
         work.record_stream(side)
+        # the speculative pass draws dropout seeds from the CPU generator: on a miss the
+        # re-run restarts from the same generator state, so masks and RNG state after the
+        # forward do not depend on the trim-guess history (identical to the synchronous path)
+        rng = torch.get_rng_state()
         out = self._forward_trimmed(guess[1], input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome)
         done.synchronize()
         first, n_all_pad = self._trim_host.tolist()
         trim = effective_trim(T_full, self.export_span, first, n_all_pad)
         self._trim_guess = (T_full, trim)
         if trim != guess[1]:
+            torch.set_rng_state(rng)
             out = self._forward_trimmed(trim, input, target, mask_inp, labels, timestamp, ids, ctx, future_outcome)
         return out
 

@@ -10,9 +10,10 @@ lookahead offsets drawn per mini-batch exactly as wrapper.py:147-153 does
 
 Bug resolutions: #11 ``self._model_config`` -> ``self.model_config``;
 #12 ``current_token_id`` -> ``current_token_ids``; #13 ``sparse`` /
-``log_q_config`` / ``loss_type`` declared in the config.  The logQ correction is
-applied only when ``log_q_config.beta != 0`` (the shipped YAML has beta = 0, so
-its lookups cannot change the loss).
+``log_q_config`` / ``loss_type`` declared in the config.  The logQ streaming
+estimates are trained on every helper call as in the reference; the correction
+enters the loss kernels only when ``log_q_config.beta != 0`` (the shipped YAML has
+beta = 0, where the correction is exactly zero).
 """
 from __future__ import annotations
 
@@ -25,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
-from ...._lib import STRUCTS, call, ptr, stream
+from ...._lib import STRUCTS, call, load, ptr, stream
 from ....commons.base_model_wrapper import BaseModelWrapper
 from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
@@ -71,6 +72,9 @@ class ContrastiveLossFn(torch.autograd.Function):
                                     lse[0], pos[0], cnt[0], rank[0], diag[0], w[0], logq,
                                     None if lqc is None else lqc[0])
         d.heads_run, d.head_stride = NH, n_mb * n_max
+        wsb = load().lthm_contrastive_ws_bytes(n_mb, n_max, NH)
+        ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
+        d.stats_ws, d.stats_ws_bytes = ptr(ws), ws.numel() * 8
         call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
              1.0 / n_mb, stream(), _key="cl_fwd_k", _work=float(sum(cfg["flops"])), _unit="flop")
         # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
@@ -80,6 +84,7 @@ class ContrastiveLossFn(torch.autograd.Function):
         ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc)
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
+        cfg.get("stats_out", []).append(stats)
         ctx.flops = cfg["flops"]
         return loss
 
@@ -124,6 +129,33 @@ class ContrastiveLossFn(torch.autograd.Function):
             dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
         dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
         return dy.view(yc.shape), dt.view(tc.shape), None, None, None, None
+
+
+def contrastive_step(y, tgt, mask, offs: np.ndarray, mbs: int, tau: float, ks: List[int], logq=None):
+    """All helper calls of one train / val step (wrapper.py:78-245) on the fused kernels.
+
+    y [B, T+1, NH, De] next_token_emb, tgt [B, T, De] current_token_emb, mask [B, T] pad
+    mask, offs [n_mb, NH] the lookahead offsets drawn per helper call, mbs sequences per
+    helper call (B: the whole batch).  Returns the loss (mean over helper calls of the
+    per-call sum over heads) and the device statistics [NH, n_mb, 7 + len(ks)]."""
+    B, T = y.shape[0], y.shape[1] - 1
+    n_mb = (B + mbs - 1) // mbs
+    assert offs.shape[0] == n_mb, (offs.shape, n_mb)
+    offsets_dev = torch.from_numpy(np.ascontiguousarray(offs, dtype=np.int32)).pin_memory().to(
+        y.device, non_blocking=True)
+    flops = []  # algorithmic logits flops per head: sum over mini-batches of 2 n^2 De
+    for h in range(offs.shape[1]):
+        tot = 0.0
+        for mb in range(n_mb):
+            n = min(mbs, B - mb * mbs) * max(T - int(offs[mb, h]), 0)
+            tot += 2.0 * n * n * y.shape[-1]
+        flops.append(tot)
+    holder = []
+    cfg = dict(mb=mbs, tau=tau, ks=list(ks), flops=flops, stats_out=holder)
+    if mask.dtype == torch.bool:
+        mask = mask.view(torch.uint8)
+    loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg, logq)
+    return loss, holder[0]
 
 
 class LTHMModelWrapper(BaseModelWrapper):
@@ -177,52 +209,47 @@ class LTHMModelWrapper(BaseModelWrapper):
         return out
 
     def train_step(self, batch, output):
-        return self._loss_and_metrics(output, "train")
+        return self._loss_and_metrics(output, training=True)
 
     def val_step(self, batch, output):
-        return self._loss_and_metrics(output, "val")
+        return self._loss_and_metrics(output, training=False)
 
-    def _loss_and_metrics(self, output, step_type: str):
+    def _loss_and_metrics(self, output, training: bool):
+        """_mini_batch_mapper (wrapper.py:78-112): training splits the batch into
+        train_mini_batch_size sequences per helper call; val_step and a negative
+        train_mini_batch_size run the helper (wrapper.py:114-245) once over the whole
+        batch.  Every helper call of the step runs in one fused launch set."""
         y = output["next_token_emb"]
         tgt = output["current_token_emb"]
         mask = output["current_token_mask"]
         B, Tp = y.shape[0], y.shape[1]
-        mbs = self.model_config.train_mini_batch_size if step_type == "train" else B
-        if mbs < 0:
-            mbs = B
-        mbs = min(mbs, B)
-        n_mb = (B + mbs - 1) // mbs
-        offs = self.draw_offsets(n_mb)
-        if (Tp - 1 - offs).min() <= 0:
-            raise ValueError("a lookahead offset reaches past the (trimmed) history")
-        offsets_dev = torch.from_numpy(offs).pin_memory().to(y.device, non_blocking=True)
         T = Tp - 1
-        flops = []  # algorithmic logits flops per head: sum over mini-batches of 2 n^2 De
-        for h in range(offs.shape[1]):
-            tot = 0.0
-            for mb in range(n_mb):
-                n = min(mbs, B - mb * mbs) * (T - int(offs[mb, h]))
-                tot += 2.0 * n * n * y.shape[-1]
-            flops.append(tot)
-        cfg = dict(mb=mbs, tau=self._softmax_temperature, ks=self._metrics_k_all, flops=flops)
-        logq = None
-        if self._log_q_beta != 0.0:
-            # wrapper.py:126-130 per mini-batch in order: logQ train_step on its non-pad ids,
-            # then the correction -beta * logQ of its ids (zeroed on the positive in-kernel)
-            logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
-                                                      self._log_q_beta)
-        loss = ContrastiveLossFn.apply(y, tgt, mask, offsets_dev, cfg, logq)
+        step_type = "train" if training else "val"
+        mbs = self.model_config.train_mini_batch_size
+        whole = (not training) or mbs < 0
+        mbs = B if whole else min(mbs, B)
+        n_mb = (B + mbs - 1) // mbs
+        offs = self.draw_offsets(n_mb)  # a head whose offset reaches past T has no rows (wrapper.py:157-159)
+        # wrapper.py:126-130 per helper call in order, train and val alike: logQ train_step on its
+        # non-pad ids, then the correction -beta * logQ of its ids (zeroed on the positive
+        # in-kernel).  The streaming estimates advance whatever beta is, as the reference's do;
+        # the correction enters the loss only when beta != 0 (with beta = 0 it is exactly zero)
+        logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
+                                                  self._log_q_beta)
+        if self._log_q_beta == 0.0:
+            logq = None
+        loss, stats = contrastive_step(y, tgt, mask, offs, mbs, self._softmax_temperature, self._metrics_k_all, logq)
         self.batch_idx += n_mb  # the reference counts helper calls, one per mini-batch
-        self.last_stats = (loss.grad_fn, offs, step_type, B)
+        self.last_stats = (stats, offs, step_type, B, T, mbs, whole)
         return loss, {}
 
     def metrics(self) -> Dict[str, float]:
-        """Metric dict of the last step, keyed like wrapper.py:222-242 (one device->host copy)."""
+        """Metric dict of the last train_step / val_step, with the reference's keys and
+        values (wrapper.py:95-111, 139-142, 221-242; one device->host copy)."""
         if self.last_stats is None:
             return {}
-        fn, offs, step_type, B = self.last_stats
-        stats = fn.stats.cpu().numpy()  # [NH, n_mb, nstat]
-        return lthm_metrics(stats, offs, step_type, self._metrics_k_all, B)
+        stats, offs, step_type, B, T, mbs, whole = self.last_stats
+        return lthm_metrics(stats.cpu().numpy(), offs, step_type, self._metrics_k_all, B, T, mbs, whole)
 
     def is_sparse(self, param_name: str):
         return super().is_sparse(param_name) or "user_context.tables" in param_name
@@ -248,14 +275,19 @@ class LTHMModelWrapper(BaseModelWrapper):
         return groups
 
 
-def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[int], B: int) -> Dict[str, float]:
-    """Per-mini-batch metrics averaged over the mini-batches that produced each key (wrapper.py:95-111)."""
-    acc: Dict[str, float] = {}
-    cnt: Dict[str, int] = {}
+def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[int], B: int, T: int, mbs: int,
+                 whole: bool) -> Dict[str, float]:
+    """The reference's metric dict from the per-(head, mini-batch) kernel statistics.
+
+    Per helper call (wrapper.py:139-142, 221-242): batch size, sequence length, and per head
+    with a usable row the offset-keyed effective batch size, mean negatives, used tokens,
+    mean CE, mean / median hit position and hits@k, then the summed loss.  With mini-batches
+    (wrapper.py:95-111) each key is averaged over the helper calls that produced it and
+    ``{step}_overall_batch_size`` is added; a whole-batch call returns its dict as is."""
     NH, n_mb, _ = stats.shape
-    T_loss = 0.0
+    per = []
     for mb in range(n_mb):
-        m = {f"{step_type}_batch_size": None}
+        m = {f"{step_type}_batch_size": min(mbs, B - mb * mbs), f"{step_type}_seq_len": T}
         loss_mb = 0.0
         for h in range(NH):
             st = stats[h, mb]
@@ -273,7 +305,12 @@ def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[i
             for q, k in enumerate(ks):
                 m[f"{step_type}_hit_rate_at_{k}_offset_{off}"] = float(st[NSTAT_BASE + q])
         m[f"{step_type}_loss"] = loss_mb
-        m.pop(f"{step_type}_batch_size")
+        per.append(m)
+    if whole:
+        return per[0]
+    acc: Dict[str, float] = {}
+    cnt: Dict[str, int] = {}
+    for m in per:
         for k, v in m.items():
             acc[k] = acc.get(k, 0.0) + v
             cnt[k] = cnt.get(k, 0) + 1

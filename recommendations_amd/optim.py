@@ -36,13 +36,13 @@ class FusedAdamW(torch.optim.Optimizer):
             # shared step count -> reuse the previous step's pointer arrays (the per-tensor
             # checks and ctypes packing cost ~0.6 ms of host time per C2 step)
             live = [p for p in g["params"] if p.grad is not None]
-            key = tuple((id(p), p.data_ptr(), p.grad.data_ptr()) for p in live)
+            key = self._plan_key(live)
             hit = fast.get(gi)
             if hit is not None and hit[0] == key:
                 step = hit[2] + 1
                 for p in live:
                     self.state[p]["step"] = step
-                fast[gi] = (key, hit[1], step)
+                fast[gi] = (self._plan_key(live), hit[1], step)
                 K.adamw_multi_run(hit[1], g["lr"], g["betas"], g["eps"], g["weight_decay"], step,
                                   grad_scale=grad_scale)
                 continue
@@ -68,8 +68,23 @@ class FusedAdamW(torch.optim.Optimizer):
                                grad_scale=grad_scale)
             if len(buckets) == 1 and all(p.grad.is_contiguous() for p in live):
                 (step, (ps, gs, ms, vs)), = buckets.items()
-                fast[gi] = (key, K.adamw_multi_plan(ps, gs, ms, vs), step)
+                fast[gi] = (self._plan_key(live), K.adamw_multi_plan(ps, gs, ms, vs), step)
         return loss
+
+    def _plan_key(self, live):
+        """What a kept pointer plan depends on: each parameter, its gradient, its moment
+        buffers (a state entry replaced other than by load_state_dict invalidates the plan
+        instead of leaving the kernel updating orphaned buffers) and its step count."""
+        out = []
+        for p in live:
+            st = self.state.get(p)
+            if st:
+                step = st["step"]
+                out.append((id(p), p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                            st["exp_avg_sq"].data_ptr(), float(step) if torch.is_tensor(step) else step))
+            else:
+                out.append((id(p), p.data_ptr(), p.grad.data_ptr(), 0, 0, -1))
+        return tuple(out)
 
 
 class FusedAdagrad(torch.optim.Optimizer):

@@ -301,10 +301,172 @@ def gen_vecemb():
     save("simhash63", x=x, projection_mat=sv.projection_mat, out=sv(x))
 
 
+def _reference_wrapper_class():
+    """models.lthm.sequence.wrapper.LTHMModelWrapper from the reference itself.
+
+    Its module imports Encoder (encoder.py), whose import chain reaches packages that
+    are absent here (ray, the S3 data store).  The loss helper never touches the
+    encoder, so that one module is registered as a placeholder holding an empty
+    `Encoder` class before the import; every line the loss executes is the
+    reference's own (wrapper.py:78-245) on torch."""
+    import types
+    name = "models.lthm.sequence.encoder"
+    if name not in sys.modules:
+        import models.lthm.sequence  # noqa: F401  (the real package)
+        placeholder = types.ModuleType(name)
+
+        class Encoder:  # never constructed: the helper is called on a namespace `self`
+            pass
+
+        placeholder.Encoder = Encoder
+        sys.modules[name] = placeholder
+    from models.lthm.sequence.wrapper import LTHMModelWrapper
+    return LTHMModelWrapper
+
+
+class _FixedLogQ:
+    """Stands in for the wrapper's CascadedStreamingLogQCorrectionModule, whose
+    train_step is broken in the reference: train_step does
+    nothing, the forward returns fixed per-token logQ values.  The ids passed in are
+    token indices b * T + t, so a mini-batch slice looks up its own rows."""
+
+    def __init__(self, logq):
+        self.flat = logq.reshape(-1)
+
+    def train_step(self, ids, batch_idx):
+        pass
+
+    def __call__(self, ids):
+        return self.flat[ids]
+
+
+def _rank_bounds(case, inp, offs):
+    """Exact-input cases: per metric key, the interval that the argsort / topk metrics
+    (wrapper.py:228-238) can take under every order of tied logits.  Logits are exact
+    (integer dot products / 65536), so ties are exact and computed here in float64."""
+    from contrastive_inputs import NORM2
+    B, T, NH = case["B"], case["T"], len(case["lookahead"])
+    whole = case["mode"] == "val" or case["mbs"] < 0
+    mbs = B if whole else case["mbs"]
+    n_mb = (B + mbs - 1) // mbs
+    st = "val" if case["mode"] == "val" else "train"
+    y = inp["y"] / np.linalg.norm(inp["y"], axis=-1, keepdims=True)
+    t = inp["tgt"] / np.linalg.norm(inp["tgt"], axis=-1, keepdims=True)
+    acc, cnt = {}, {}
+    for mb in range(n_mb):
+        sl = slice(mb * mbs, min((mb + 1) * mbs, B))
+        m = inp["mask"][sl]
+        Bm = m.shape[0]
+        for h in range(NH):
+            off = int(offs[mb, h])
+            L = T - off
+            if L <= 0:
+                continue
+            o = (y[sl][:, :L, h] * 256).reshape(-1, y.shape[-1]).astype(np.float64)
+            i_ = (t[sl][:, off:] * 256).reshape(-1, t.shape[-1]).astype(np.float64)
+            dots = o @ i_.T  # exact integers
+            assert np.abs(dots).max() <= NORM2
+            n = Bm * L
+            seq = np.repeat(np.arange(Bm), L)
+            pad = m[:, off:].reshape(-1)
+            excl = (seq[:, None] == seq[None, :]) & ~np.eye(n, dtype=bool)
+            excl |= pad[None, :] | pad[:, None]
+            nneg = (~excl).sum(1) - 1
+            used = ~(pad | (nneg <= 0))
+            if not used.any():
+                continue
+            d = dots[used]
+            ex = excl[used]
+            posv = d[np.arange(d.shape[0]), np.nonzero(used)[0]]
+            gt = ((d > posv[:, None]) & ~ex).sum(1)
+            tie = ((d == posv[:, None]) & ~ex).sum(1) - 1  # the positive itself is not a tie
+            lo, hi = gt.astype(np.float64), (gt + tie).astype(np.float64)
+            bounds = {f"{st}_average_hit_position_offset_{off}": (lo.mean(), hi.mean()),
+                      f"{st}_median_hit_position_offset_{off}": (np.quantile(lo, 0.5), np.quantile(hi, 0.5))}
+            mn = int(nneg[used].min())
+            for k_ in case["ks"]:
+                k = min(k_, mn)
+                bounds[f"{st}_hit_rate_at_{k_}_offset_{off}"] = (float((hi < k).mean()), float((lo < k).mean()))
+            for key, (a, b) in bounds.items():
+                pa, pb = acc.get(key, (0.0, 0.0))
+                acc[key] = (pa + a, pb + b)
+                cnt[key] = cnt.get(key, 0) + 1
+    return {k: (acc[k][0] / cnt[k], acc[k][1] / cnt[k]) for k in acc}
+
+
+def gen_contrastive(only=None):
+    """Contrastive loss + metrics goldens from the reference's own
+    LTHMModelWrapper._mini_batch_mapper / _train_or_val_step_helper (wrapper.py:72-245),
+    called unbound on a namespace `self`.  Inputs are rebuilt by the test from the case
+    parameters (tests/golden/contrastive_inputs.py) and checked by digest."""
+    import functools
+    import random
+    import time
+    from types import SimpleNamespace
+    sys.path.insert(0, HERE)
+    from contrastive_inputs import CASES, draw_offsets, inputs_digest, make_inputs
+    W = _reference_wrapper_class()
+    for name, case in CASES.items():
+        if only and name not in only:
+            continue
+        t0 = time.time()
+        inp = make_inputs(case)
+        B, T, De, NH = case["B"], case["T"], case["De"], len(case["lookahead"])
+        whole = case["mode"] == "val" or case["mbs"] < 0
+        n_mb = 1 if whole else (B + case["mbs"] - 1) // case["mbs"]
+        ids = torch.arange(B * T, dtype=torch.int64).view(B, T)
+        ns = SimpleNamespace(_export_tokens=NH, _lookahead=list(case["lookahead"]),
+                             _softmax_temperature=case["tau"], _log_q_beta=case["beta"],
+                             _log_q_calc=_FixedLogQ(torch.from_numpy(inp["logq"])), batch_idx=0,
+                             _metrics_k_all=list(case["ks"]),
+                             _model_config=SimpleNamespace(train_mini_batch_size=case["mbs"]),
+                             _convert_metrics_tensor_to_float=W._convert_metrics_tensor_to_float)
+        ns._train_or_val_step_helper = functools.partial(W._train_or_val_step_helper, ns)
+        ns._mini_batch_mapper = functools.partial(W._mini_batch_mapper, ns)
+        y = torch.from_numpy(inp["y"]).requires_grad_(True)
+        tg = torch.from_numpy(inp["tgt"]).requires_grad_(True)
+        out = {"next_token_emb": y, "current_token_emb": tg, "current_token_mask": torch.from_numpy(inp["mask"]),
+               "current_token_id": ids}
+        random.seed(case["seed"])
+        if case["mode"] == "val":
+            loss, metrics = W.val_step(ns, {}, out)
+        else:
+            loss, metrics = W._mini_batch_mapper(ns, {}, out, True)
+        offs = draw_offsets(case["lookahead"], n_mb, case["seed"])
+        loss.sum().backward() if loss.requires_grad else None
+        dy = y.grad if y.grad is not None else torch.zeros_like(y)
+        dt = tg.grad if tg.grad is not None else torch.zeros_like(tg)
+        keys = sorted(metrics)
+        arrays = dict(digest=np.array(inputs_digest(inp)), offsets=offs, loss=loss.detach().reshape(-1)[:1],
+                      metric_keys=np.array(keys), metric_values=np.array([float(metrics[k]) for k in keys]),
+                      dy_norm=np.float64(dy.double().norm()), dt_norm=np.float64(dt.double().norm()),
+                      dy_sum=np.float64(dy.double().sum()), dt_sum=np.float64(dt.double().sum()))
+        if dy.numel() <= 2 ** 18:
+            arrays.update(dy=dy, dt=dt)
+        else:  # gradients at a fixed sample of rows (plus the norms and sums above)
+            g = np.random.default_rng(case["seed"] + 1000)
+            ry = np.sort(g.choice(B * (T + 1) * NH, 512, replace=False))
+            rt = np.sort(g.choice(B * T, 256, replace=False))
+            arrays.update(dy_rows=ry, dy_sample=dy.reshape(-1, De)[ry], dt_rows=rt, dt_sample=dt.reshape(-1, De)[rt])
+        if case["kind"] == "exact":
+            bnd = _rank_bounds(case, inp, offs)
+            bk = sorted(bnd)
+            for k in bk:  # the reference's own value lies in the tie interval
+                v = float(metrics[k])
+                assert bnd[k][0] - 1e-6 <= v <= bnd[k][1] + 1e-6, (name, k, v, bnd[k])
+            arrays.update(bound_keys=np.array(bk), bound_lo=np.array([bnd[k][0] for k in bk]),
+                          bound_hi=np.array([bnd[k][1] for k in bk]))
+        save("contrastive_" + name, **arrays)
+        print(f"  {name}: loss {float(loss.detach().reshape(-1)[0]):.6f}, {len(keys)} metrics, {time.time() - t0:.1f}s")
+
+
 if __name__ == "__main__":
     if not any("reference" in p for p in sys.path + os.environ.get("PYTHONPATH", "").split(":")):
         sys.exit("run with PYTHONPATH=/root/reference (build container only)")
     torch.set_num_threads(4)
-    which = sys.argv[1:] or ["hashing", "kshift", "layers", "transformer"]
+    which = sys.argv[1:] or ["hashing", "kshift", "layers", "transformer", "contrastive"]
     for w in which:
-        globals()["gen_" + w]()
+        if w.startswith("contrastive:"):  # contrastive:case1,case2 regenerates only those cases
+            gen_contrastive(w.split(":", 1)[1].split(","))
+        else:
+            globals()["gen_" + w]()

@@ -142,6 +142,42 @@ def test_grad_bucket_allreduce_overlaps_backward():
             torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
 
 
+def _bucket_allreduce_accumulate(rank, world):
+    """Two micro-batch backward passes before ar(): with the first inside no_sync (the
+    DDP pattern) and without it (hooks fire twice; the stale launch is redone)."""
+    from recommendations_amd.distributed import GradBucketAllReduce
+    out = []
+    for use_no_sync in (True, False):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+        ar = GradBucketAllReduce(net.parameters(), bucket_bytes=512)
+        for step in range(2):  # the second step checks that state was reset
+            net.zero_grad(set_to_none=True)
+            xs = [torch.randn(8, 16, generator=torch.Generator().manual_seed(100 * step + 10 * mb + rank))
+                  for mb in range(2)]
+            if use_no_sync:
+                with ar.no_sync():
+                    net(xs[0]).square().mean().backward()
+            else:
+                net(xs[0]).square().mean().backward()
+            net(xs[1]).square().mean().backward()
+            ar()
+        ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+        ref.load_state_dict(net.state_dict())
+        loss = sum(ref(torch.randn(8, 16, generator=torch.Generator().manual_seed(100 + 10 * mb + r))).square().mean()
+                   for r in range(world) for mb in range(2)) / world
+        loss.backward()
+        out.append(([p.grad.clone() for p in net.parameters()], [p.grad for p in ref.parameters()]))
+    return out
+
+
+def test_grad_bucket_allreduce_gradient_accumulation():
+    for per_rank in spawn(_bucket_allreduce_accumulate):
+        for grads, ref in per_rank:
+            for g, r in zip(grads, ref):
+                torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
+
+
 def _gather_sparse(rank, world):
     from recommendations_amd.distributed import gather_sparse_grads
     from oracle.ref import kshift_bwd_c

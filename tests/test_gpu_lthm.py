@@ -311,6 +311,36 @@ def test_speculative_trim_matches_synchronous(dev):
     assert trims[0] == 0 and trims[2] > 0 and trims[4] == 0, trims
 
 
+def test_speculative_trim_dropout_rng(dev):
+    """Train mode with dropout: the speculative pass draws dropout seeds from the CPU
+    generator; on a trim miss the re-run restarts from the state the speculative pass
+    started from, so outputs and the generator state after the forward equal the
+    synchronous path's whatever the trim-guess history."""
+    import copy
+    from recommendations_amd.data import synthetic_lthm_batch
+    cfg, m = _model(dev)
+    m.train()
+    m._model.query_tower.transformer.dropout.p = 0.2
+    ref_m = copy.deepcopy(m)
+    full = synthetic_lthm_batch(64, 32, n_cat=2, seed=11, device=dev)
+    short = synthetic_lthm_batch(64, 32, n_cat=2, seed=12, device=dev)
+    short["product_ids"][:, 20:] = 0
+    trims = []
+    with torch.no_grad():
+        for i, batch in enumerate((full, full, short, short, full)):
+            torch.manual_seed(100 + i)
+            out = m(batch)
+            s_out = torch.get_rng_state()
+            ref_m._model.query_tower._trim_guess = None
+            torch.manual_seed(100 + i)
+            exp = ref_m(batch)
+            assert torch.equal(s_out, torch.get_rng_state())
+            trims.append(out["_trim"])
+            for k in ("next_token_emb", "current_token_emb", "current_token_mask"):
+                assert torch.equal(out[k], exp[k]), k
+    assert trims[0] == 0 and trims[2] > 0 and trims[4] == 0, trims
+
+
 @pytest.mark.parametrize("sharded", [False, True])
 def test_item_prefetch_matches_inline(dev, sharded):
     """Encoder.prefetch runs the frozen item-table lookup of a later forward on a side

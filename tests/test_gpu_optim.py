@@ -51,6 +51,9 @@ def test_fused_adamw_kept_plan(dev):
         for a, b, gr in zip(mine, ref, gs):
             a.grad.copy_(gr.to(dev))
             b.grad = gr.clone()
+        if it == 2:  # a moment buffer replaced directly: the kept plan must not update the orphan
+            o1.state[mine[3]]["exp_avg"] = o1.state[mine[3]]["exp_avg"].clone()
+            o1.state[mine[5]]["exp_avg_sq"] = o1.state[mine[5]]["exp_avg_sq"].clone()
         if it == 3:
             o1.load_state_dict(o1.state_dict())
             assert not o1._plans
