@@ -119,9 +119,9 @@ CONFIGS = {
     # SURVEY §8 C3 per GPU: 100M-row item table row-sharded over the ranks, 64 categorical tables
     "c3": dict(B=4096, T=128, d=256, L=4, H=4, n_cat=64, cat_vocab=1_000_000, item_vocab=100_000_000,
                item_table_sharded=True),
-    # BASELINE.json configs[4]: long history, fp8 encoder GEMMs; 8-sequence loss
-    # mini-batches keep the in-batch logits at 8 x 512 = 4096 rows (C2's size)
-    "c5": dict(B=1024, T=512, d=512, L=6, H=8, n_cat=0, cat_vocab=1_000_000, item_vocab=1_000_000, fp8=True, mbs=8),
+    # BASELINE.json configs[4]: long history, fp8 encoder GEMMs; the reference
+    # yaml's 32-sequence loss mini-batches (model/lthm.yaml:64): 32 x 512 = 16,384 logit rows
+    "c5": dict(B=1024, T=512, d=512, L=6, H=8, n_cat=0, cat_vocab=1_000_000, item_vocab=1_000_000, fp8=True),
     # BASELINE.json configs[3]: ranker, 128 dense + 64 cat x 1M, interaction layers only
     "c4": dict(kind="ranker", B=65536, n_dense=128, n_cat=64, cat_vocab=1_000_000),
 }

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 24 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 25 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -485,13 +485,21 @@ typedef struct lthm_contrastive_desc {
                              of every input token (wrapper.py:131-135, 204-208; zero on the positive) */
   int64_t logq_stride;
   float* logq_col;        /* with logq: [n_mb, n_max] scratch written by the forward, read by the backward */
-  const void* y_raw;      /* backward, optional: bf16 [B, T+1, n_heads, De] next_token_emb before F.normalize */
+  const void* y_raw;      /* backward, optional: [B, T+1, n_heads, De] next_token_emb before F.normalize (dtype y_dtype;
+                             bf16 only without t_raw) */
   const float* y_norm;    /* with y_raw: f32 [B, T+1, n_heads] its row norms (lthm_rownorm) */
-  void* dy;               /* with y_raw: bf16 [B, T+1, n_heads, De] written INSTEAD of d_out: the gradient through
+  void* dy;               /* with y_raw: [B, T+1, n_heads, De] (dtype y_dtype) written INSTEAD of d_out: the gradient through
                              F.normalize (wrapper.py:118-119), every row of this head written */
   int32_t heads_run;      /* forward: heads head .. head + heads_run - 1 in one set of launches (0 or 1: one) */
   int64_t head_stride;    /* with heads_run > 1: elements between consecutive heads' lse / pos / cnt / rank /
                              diag / w / logq_col buffers; stats rows advance by n_mb * nstat */
+  int32_t y_dtype;        /* LTHM_F32 / LTHM_BF16: dtype of y_raw and dy */
+  const void* t_raw;      /* backward, with y_raw / dy: [B, T, De] current_token_emb before F.normalize (dtype t_dtype);
+                             then every head runs in ONE call (head 0, heads_run = n_heads) and dIn is summed over
+                             the heads on chip: dt is written once, through F.normalize, instead of d_in */
+  int32_t t_dtype;
+  const float* t_norm;    /* with t_raw: f32 [B, T] its row norms (lthm_rownorm) */
+  void* dt;               /* with t_raw: [B, T, De] (dtype t_dtype): d current_token_emb, every row written */
   void* stats_ws;         /* forward: device workspace of lthm_contrastive_ws_bytes(n_mb, n_max, heads_run)
                              bytes (rank histograms + per-block partial sums) */
   int64_t stats_ws_bytes;
@@ -575,7 +583,9 @@ int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed, void* str
 int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride, int64_t B,
                      int32_t T, int32_t mb_size, float* b_tables, float* a_tables, const int64_t* hash_offsets,
                      int32_t n_modules, int64_t num_buckets, float alpha, int64_t batch_idx0, float beta,
-                     int32_t update, float* out, void* stream);
+                     int32_t update, float* out, float* scratch, void* stream);
+/* (scratch: with update, f32 [min(mb_size, B) * T]: every token of a mini-batch computes its
+ * bucket's new value before any is written, the semantics of the reference's index_put) */
 /* History-trim statistics of mask [B, T] (uint8, 1 = pad) for query_tower.py:73-86:
  * work[0] = first column holding a non-pad entry (T if none), work[1] = number of
  * all-pad columns; work is a device int32 buffer of T + 2 entries (work[2..] scratch). */

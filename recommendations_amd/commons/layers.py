@@ -534,9 +534,10 @@ def _logq_call(mods, ids, mask, mb_size, batch_idx0, beta, update, want_out=True
     offs = torch.tensor([int(m.hash_offset) for m in mods], dtype=torch.int64).to(ids.device, non_blocking=True)
     B, T = ids2.shape
     out = torch.empty((B, T), dtype=torch.float32, device=ids.device) if want_out else None
+    scratch = torch.empty(min(mb_size, B) * T, dtype=torch.float32, device=ids.device) if update else None
     call("lthm_logq_stream", ptr(ids2), ids2.stride(0), ptr(mask), 0 if mask is None else mask.stride(0), B, T,
          mb_size, ptr(bt), ptr(at), ptr(offs), len(mods), nb, float(mods[0].alpha), int(batch_idx0), float(beta),
-         int(update), ptr(out), stream())
+         int(update), ptr(out), ptr(scratch), stream())
     return out.view(shp) if want_out else None
 
 

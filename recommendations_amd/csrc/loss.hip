@@ -18,6 +18,8 @@
 // count #{c != r : logit[r, c] > logit[r, r]}.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace lthm {
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -47,6 +49,12 @@ __device__ __forceinline__ int swz(int row) {
   return ((((row & 7) << 1) + (h << 3)) & 15) | h;
 }
 __device__ __forceinline__ int ks_off256(int row, int ch) { return row * 256 + ((ch ^ swz(row)) << 4); }
+// The 32x32x16 tile engine's image (cdna_hip_programming.md T10, image (b)): chunk ch of
+// row r at slot ch ^ swz32(r), conflict-free for the ds_read_b128 row fragments of the
+// 32x32x16 A operand and for the ds_read_b64_tr_b16 transposed B fragments (each aligned
+// quad of rows takes four distinct aligned blocks of four slots).
+__device__ __forceinline__ int swz32(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int ko32(int row, int ch) { return row * 256 + ((ch ^ swz32(row)) << 4); }
 
 // ---------------------------------------------------------------- row normalisation
 // out[r] = bf16(x[r] / max(|x[r]|, 1e-12)), norms[r] = |x[r]|   (F.normalize, wrapper.py:118-119)
@@ -236,7 +244,15 @@ struct ClArgs {
   const bf16_t* y_raw;  // [B, Tp, NH, DE] or null
   const float* y_norm;  // [B, Tp, NH]
   bf16_t* dy;           // [B, Tp, NH, DE], written instead of d_out
-  int64_t head_stride;  // forward over several heads: per-head buffer stride (blockIdx.z = head - head0)
+  int64_t head_stride;  // several heads per launch: per-head buffer stride (head = head0 + z)
+  int y_dtype;          // dtype of y_raw / dy (LTHM_F32 / LTHM_BF16)
+  int heads_run;        // heads head0 .. head0 + heads_run - 1
+  int prio;             // backward: s_setprio 1 around the MFMA clusters (A/B switch LTHM_CL_PRIO)
+  // COLS epilogue through F.normalize: dt = (g - t^ (t^ . g)) / |t| of current_token_emb
+  const void* t_raw;    // [B, T, DE], dtype t_dtype
+  int t_dtype;
+  const float* t_norm;  // [B, T]
+  void* dt;             // [B, T, DE], dtype t_dtype, every row written
 };
 
 // the per-head view of a multi-head forward launch: head head0 + z, buffers advanced by z strides
@@ -345,7 +361,9 @@ __global__ __launch_bounds__(256) void cl_diag_k(ClArgs a0) {
 
 // backward prologue: shift[r] = log2 w_r - lse_r log2 e (-inf where w_r = 0 or r >= n),
 // the exp2 shift that folds the row weight into dS = w (e^(S/tau - lse) - [r == c])
-__global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ shift) {
+__global__ __launch_bounds__(256) void cl_shift_k(ClArgs a0) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  float* shift = a.colb;  // = diag of this head (the backward's scratch for the shift)
   const int mb = blockIdx.y;
   const Geo g = geo(a, mb);
   const int64_t base = (int64_t)mb * a.n_max;
@@ -353,8 +371,8 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
     const float wv = r < g.n ? a.w[base + r] : 0.f;
     shift[base + r] = wv != 0.f ? __log2f(wv) - a.lse[base + r] * 1.4426950408889634f : -INFINITY;
   }
-  // d_out rows of this head that the ROWS kernel never writes (t >= L of each of the
-  // mini-batch's sequences) are zeroed here, so d_out needs no whole-tensor fill
+  // d_out / dy rows of this head that the ROWS kernel never writes (t >= L of each of the
+  // mini-batch's sequences) are zeroed here, so they need no whole-tensor fill
   const int tl0 = max(g.L, 0), ntail = a.T + 1 - tl0;
   const int per_seq = ntail * (DE / 4);
   const int64_t cnt = (int64_t)g.Bm * per_seq;
@@ -362,7 +380,8 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a, float* __restrict__ 
     const int b = (int)(i / per_seq), rem = (int)(i - (int64_t)b * per_seq);
     const int t = tl0 + rem / (DE / 4), c4 = rem % (DE / 4);
     const int64_t o = (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
-    if (a.dy) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
+    if (a.dy && a.y_dtype == LTHM_BF16) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
+    else if (a.dy) *reinterpret_cast<float4*>((float*)a.dy + o) = float4{0.f, 0.f, 0.f, 0.f};
     else *reinterpret_cast<float4*>(a.d_out + o) = float4{0.f, 0.f, 0.f, 0.f};
   }
 }
@@ -585,6 +604,7 @@ __device__ float cl_zero_f = 0.f;
 // source row of column c = (b, t) (sequence b of the mini-batch, position t) sits
 // at base + b * sb + t * st elements; the cursor advances (b, t) by 64 columns a
 // tile without a division.
+template <bool SW32 = false>
 struct RowCursor {
   const bf16_t* base;
   int sb, st, L, q64, r64;
@@ -599,7 +619,7 @@ struct RowCursor {
       const int row = c + 4 * k;
       b[k] = row / L;
       t[k] = row - b[k] * L;
-      choff[k] = ((lane & 15) ^ swz(row)) * 8;
+      choff[k] = ((lane & 15) ^ (SW32 ? swz32(row) : swz(row))) * 8;
     }
   }
   // stage the next tile into img (the tile's 64-row image), then advance by 64 columns
@@ -736,7 +756,7 @@ __global__ __launch_bounds__(256, OCC) void cl_fwd_k(ClArgs a0) {
   }
   const int ntile = (g.n + 63) / 64;
   // 5 DMAs per wave and tile: 4 image pieces + the diag (pad flag) of the tile's columns
-  RowCursor cur_in;
+  RowCursor<> cur_in;
   cur_in.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
   auto stage = [&](int t) {
     const int buf = t % NB;
@@ -914,7 +934,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
   trp_offsets(toff, lane);
   const int ntile = (g.n + 63) / 64;
   // ROWS: 4 image DMAs per wave and tile; COLS: + shift and weight of the image rows
-  RowCursor cur_img;
+  RowCursor<> cur_img;
   if (ROWS) cur_img.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
   else cur_img.init(a.out_n + (g.b0 * (a.T + 1) * a.NH + a.head) * DE, (a.T + 1) * a.NH * DE, a.NH * DE, g.L, w,
                     lane);
@@ -1071,6 +1091,358 @@ __global__ __launch_bounds__(256, 2) void cl_bwd_k(ClArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------- backward on 32x32x16 MFMA
+// The same tile math as cl_bwd_k with v_mfma_f32_32x32x16_bf16: an MFMA holds the SIMD's
+// vector issue for 8 of its 32 cycles instead of 8 of 16 (MI355X_MICROARCH.md, constants),
+// so the per-element exp2 / fma / bf16 packing of dS fits beside the matrix work.
+//  * S^T tile (64 image rows x 32 register rows per wave): acc[ib][v] = img[32 ib + 8(v>>2) +
+//    4 hh + (v&3)] . X[x], hh = lane >> 5; the lane's register row x = x0 + 32 w + (lane & 31)
+//    is the MFMA column, so every per-row quantity is a per-lane scalar.
+//  * dS in place, then dS^T . img as the A operand with no lane movement (registers
+//    8s..8s+7 of block ib are k-step 2 ib + s; cdna_hip_programming.md §3): the B operand is
+//    read transposed from the same image (ds_read_b64_tr_b16), rows in that k order.
+//  * the accumulator is restaged through LDS for the epilogue, where the gradient goes
+//    through F.normalize (wrapper.py:118-119) and is written once in the operand's dtype.
+// ROWS: grid (row blocks, n_mb, heads): register rows = out rows of one head; image = `in`.
+// COLS: grid (physical-row blocks, n_mb): register rows = physical `in` rows (b, t) (the same
+//   operand for every head); the image walks the out rows of every head in turn, so dIn is
+//   summed over the heads in registers (no f32 d_in read-modify-write per head).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8v a, bf16x8v b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr int CL_EPS = 132;  // epilogue restage row stride (floats): conflict-free b32 writes / b128 reads
+
+struct ClTile32 {
+  union {
+    struct {
+      unsigned char img[CL_NBUF][64 * 256];
+      float m0[CL_NBUF][4][64];  // per-wave copies of a per-image-row vector (COLS: shift; ROWS !FIXED: logQ)
+      float m1[CL_NBUF][4][64];  // COLS: row weights of the image rows
+    } r;
+    float ep[4][32][CL_EPS];     // epilogue: each wave's 32 x 128 f32 accumulator, row-major
+  };
+};
+
+// per-lane byte offsets of the 8 row fragments (k-step s) of an image row block and of the
+// 8 transposed fragments (column block nd, lower / upper 4 k) of a 16-row k-step
+__device__ __forceinline__ void frag32_offsets(int (&roff)[8], int (&toff)[4][2], int lane) {
+  const int hh = lane >> 5, r32 = lane & 31, sw = swz32(r32);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) roff[s] = r32 * 256 + (((2 * s + hh) ^ sw) << 4);
+  const int g16 = lane >> 4, colhalf = g16 & 1, li = lane & 15, q = li >> 2, pp = li & 3;
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int row = 4 * hh + 8 * hi + q;
+      toff[nd][hi] = row * 256 + (((4 * nd + 2 * colhalf + (pp >> 1)) ^ swz32(row)) << 4) + 8 * (pp & 1);
+    }
+}
+
+__device__ __forceinline__ bf16x8v tr_frag32(const unsigned char* img, int off_lo, int off_hi) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)((lds_u8*)img + off_lo));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)((lds_u8*)img + off_hi));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// the register row's per-lane state for one head
+struct XRow {
+  int x;        // row / column index in the head's logit matrix (-1: none)
+  int sq;       // sequence of x (-2: none)
+  bool live;    // contributes (COLS: a valid, non-pad column of this head; ROWS: x < n)
+  float sh;     // ROWS: exp2 shift of row x (log2 w - lse log2 e)
+  float w;      // ROWS: row weight
+  float cap;    // ROWS, running shift: log2 w
+  float q;      // COLS, logQ: the correction of column x (log2 units)
+};
+
+// dacc[nd] += dS^T . img over every image tile of one head (ROWS: image = `in` columns of the
+// head; COLS: image = out rows of the head).  The special range [spec_lo, spec_hi) holds the
+// image rows of the register rows' own sequences (diagonal, same-sequence exclusion).
+template <bool ROWS, bool FIXED, bool SB>
+__device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], const bf16x8v (&qf)[8],
+                                              const int (&roff)[8], const int (&toff)[4][2], const ClArgs& a,
+                                              const Geo& g, int64_t base, const XRow& xr, bool wmask, int spec_lo,
+                                              int spec_hi, RowCursor<true>& cur, int w, int lane) {
+  const int hh = lane >> 5;
+  const float it = 1.f / a.tau, c1 = it * LOG2E;
+  const float* shift = a.diag;
+  const int ntile = (g.n + 63) / 64;
+  auto stage = [&](int t) {
+    const int buf = t % CL_NBUF, y0 = t * 64;
+    cur.stage(sh.r.img[buf], g.n, w, lane);
+    if (!ROWS) {
+      const bool inr = y0 + lane < a.n_max;  // past n_max: shift -inf, weight 0
+      glds4(inr ? shift + base + y0 + lane : &cl_ninf, sh.r.m0[buf][w]);
+      glds4(inr ? a.w + base + y0 + lane : &cl_zero_f, sh.r.m1[buf][w]);
+    } else if (!FIXED) {
+      glds4(a.lq && y0 + lane < a.n_max ? a.lqcol + base + y0 + lane : &cl_zero_f, sh.r.m0[buf][w]);
+    }
+  };
+  retire_loads();
+  stage(0);
+  if (ntile > 1) stage(1);
+  for (int tI = 0; tI < ntile; ++tI) {
+    const int cb = tI % CL_NBUF, y0 = tI * 64;
+    if (tI + 1 < ntile) {
+      if (ROWS) wait_vm<FIXED ? 4 : 5>();
+      else wait_vm<6>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (tI + 2 < ntile) stage(tI + 2);
+    const unsigned char* img = sh.r.img[cb];
+    f32x16 acc[2];
+    // phases are fenced with sched_barrier so that the compiler does not hoist every LDS
+    // fragment of the tile at once (that alone needs 128 VGPRs): two waves per SIMD overlap
+    // one wave's exp2 / packing with the other's MFMAs instead
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[ib][v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8v af = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ib * 8192 + roff[s]));
+        acc[ib] = mfma32(af, qf[s], acc[ib]);
+      }
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    const bool special = !FIXED || (y0 < spec_hi && y0 + 64 > spec_lo);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      if (!special) {
+        if (ROWS) {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[ib][v] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][v], c1, xr.sh));
+        } else {
+#pragma unroll
+          for (int qd = 0; qd < 4; ++qd) {
+            const float4 ys = *reinterpret_cast<const float4*>(&sh.r.m0[cb][w][32 * ib + 8 * qd + 4 * hh]);
+            const float yv[4] = {ys.x, ys.y, ys.z, ys.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[ib][4 * qd + j] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][4 * qd + j], c1, yv[j]));
+          }
+        }
+      } else {
+        // y0 laundered: without it loop strength reduction keeps a 64-bit running product of
+        // seq_of for each of the 32 elements across the tile loop (64 VGPRs, spills)
+        int ys0 = y0;
+        asm volatile("" : "+s"(ys0));
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int yl = 32 * ib + 8 * (v >> 2) + 4 * hh + (v & 3), y = ys0 + yl;
+          const int ysq = y < g.n ? seq_of(g, y) : -1;
+          const bool keep = xr.live && (ysq != xr.sq || xr.x == y);
+          float ds = 0.f;
+          if (ROWS) {
+            const float yq = FIXED ? 0.f : sh.r.m0[cb][w][yl] * LOG2E;
+            if (keep && xr.w != 0.f) {
+              float t = __builtin_fmaf(acc[ib][v], c1, xr.sh + (xr.x == y ? 0.f : yq));
+              if (!FIXED) t = fminf(t, xr.cap);
+              ds = __builtin_amdgcn_exp2f(t) - (xr.x == y ? xr.w : 0.f);
+            }
+          } else {
+            const float ysh = sh.r.m0[cb][w][yl], yw = sh.r.m1[cb][w][yl];
+            if (keep && yw != 0.f)
+              ds = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][v], c1, ysh + (xr.x == y ? 0.f : xr.q))) -
+                   (xr.x == y ? yw : 0.f);
+          }
+          acc[ib][v] = ds;
+        }
+      }
+      // dacc[32 x 128] += dS[32 x 32] . img[32 x 128] of this image block: k-step ks = 2 ib + hf
+      // holds image rows 16 ks + 8 (j>>2) + 4 hh + (j&3) in element j (registers 8 hf .. 8 hf + 7)
+      if (a.prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int ks = 2 * ib + hf, o = 8 * hf;
+        const f32x16& pv = acc[ib];
+        u32x4 hpk = {pk_bf16(pv[o], pv[o + 1]), pk_bf16(pv[o + 2], pv[o + 3]), pk_bf16(pv[o + 4], pv[o + 5]),
+                     pk_bf16(pv[o + 6], pv[o + 7])};
+        if (wmask && !xr.live) hpk = u32x4{0u, 0u, 0u, 0u};  // COLS: a column this head does not have
+        const bf16x8v af = __builtin_bit_cast(bf16x8v, hpk);
+#pragma unroll
+        for (int nd = 0; nd < 4; ++nd) {
+          const bf16x8v bfr = tr_frag32(img, toff[nd][0] + ks * 4096, toff[nd][1] + ks * 4096);
+          dacc[nd] = mfma32(af, bfr, dacc[nd]);
+        }
+      }
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// gradient through F.normalize, written in the operand's dtype: dx = (g - y (y . g)) / |x|,
+// y = x / max(|x|, eps) (the eps branch: g / eps).  16 lanes per row, 8 columns per lane.
+__device__ __forceinline__ void normalize_bwd_store(const float (&gv)[8], const void* xraw, int xdt, float nrm,
+                                                    void* dst, int64_t elem, bool write) {
+  const float den = fmaxf(nrm, 1e-12f);
+  float yv[8], dot = 0.f;
+  if (xdt == LTHM_BF16) load_vec<bf16_t, 16>((const bf16_t*)xraw + elem, yv);
+  else {
+    load_vec<float, 16>((const float*)xraw + elem, yv);
+    load_vec<float, 16>((const float*)xraw + elem + 4, yv + 4);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    yv[i] /= den;
+    dot += yv[i] * gv[i];
+  }
+  dot = group16_sum(dot);
+  if (!write) return;
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = nrm > 1e-12f ? (gv[i] - yv[i] * dot) / nrm : gv[i] / 1e-12f;
+  if (xdt == LTHM_BF16) store_vec<bf16_t, 8>((bf16_t*)dst + elem, o);
+  else {
+    store_vec<float, 4>((float*)dst + elem, o);
+    store_vec<float, 4>((float*)dst + elem + 4, o + 4);
+  }
+}
+
+template <bool ROWS, bool FIXED, bool SB>
+__global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
+  __shared__ __attribute__((aligned(16))) ClTile32 sh;
+  const int nz = ROWS ? gridDim.z : 1;
+  const int per = gridDim.x * gridDim.y;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (ROWS ? blockIdx.z : 0)), per * nz);
+  const int z = lin / per, bid = lin - z * per;
+  const int mb = bid / gridDim.x, xb = bid - mb * gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int64_t base = (int64_t)mb * a0.n_max;
+  const int64_t b0 = (int64_t)mb * a0.mbs;
+  const int Bm = (int)min((int64_t)a0.mbs, a0.B - b0);
+  int roff[8], toff[4][2];
+  frag32_offsets(roff, toff, lane);
+  f32x16 dacc[4];
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) dacc[nd][v] = 0.f;
+  bf16x8v qf[8];
+  const float gs = (a0.gscale ? *a0.gscale : 1.f) / a0.tau;
+  if (ROWS) {
+    const ClArgs a = head_args(a0, z);
+    const Geo g = geo(a, mb);
+    const int x0 = xb * CL_ROWS;
+    if (x0 >= g.n) return;
+    XRow xr;
+    xr.x = x0 + 32 * w + r32;
+    xr.live = xr.x < g.n;
+    {
+      const bf16_t* rp = xr.live ? out_row(a, g, xr.x) : nullptr;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (xr.live) v = *reinterpret_cast<const u32x4*>(rp + 16 * s + 8 * (lane >> 5));
+        qf[s] = __builtin_bit_cast(bf16x8v, v);
+      }
+    }
+    xr.w = xr.live ? a.w[base + xr.x] : 0.f;
+    xr.sh = xr.live ? a.diag[base + xr.x] : -INFINITY;
+    xr.cap = xr.w != 0.f ? __log2f(xr.w) : -INFINITY;
+    xr.sq = xr.live ? seq_of(g, xr.x) : -2;
+    xr.q = 0.f;
+    int spec_lo, spec_hi;
+    own_cols(g, x0, spec_lo, spec_hi);
+    RowCursor<true> cur;
+    cur.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
+    cl_bwd32_head<true, FIXED, SB>(sh, dacc, qf, roff, toff, a, g, base, xr, false, spec_lo, spec_hi, cur, w, lane);
+    // epilogue: restage, then 16 lanes per row through F.normalize into dy
+    __syncthreads();
+#pragma unroll
+    for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) sh.ep[w][8 * (v >> 2) + 4 * (lane >> 5) + (v & 3)][32 * nd + r32] = dacc[nd][v];
+    const int sub = lane & 15;
+#pragma unroll 1
+    for (int ps = 0; ps < 8; ++ps) {
+      const int rl = 4 * ps + (lane >> 4), x = x0 + 32 * w + rl;
+      const int xc = min(x, g.n - 1);  // every lane takes part in the row reduction
+      const int b = xc / g.L, t = xc - b * g.L;
+      const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
+      float gv[8];
+      const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
+      const float4 u1 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub + 4]);
+      gv[0] = gs * u0.x; gv[1] = gs * u0.y; gv[2] = gs * u0.z; gv[3] = gs * u0.w;
+      gv[4] = gs * u1.x; gv[5] = gs * u1.y; gv[6] = gs * u1.z; gv[7] = gs * u1.w;
+      normalize_bwd_store(gv, a.y_raw, a.y_dtype, a.y_norm[ro], a.dy, ro * DE + 8 * sub, x < g.n);
+    }
+    return;
+  }
+  // COLS: physical `in` rows p = b T + t of the mini-batch
+  const int T = a0.T;
+  const int nphys = Bm * T;
+  const int p0 = xb * CL_ROWS;
+  if (p0 >= nphys) return;
+  const int p = p0 + 32 * w + r32;
+  const bool pin = p < nphys;
+  const int pb = pin ? p / T : 0, pt = pin ? p - pb * T : 0;
+  const bool ppad = !pin || a0.mask[(b0 + pb) * a0.mask_stride + pt] != 0;
+  {
+    const bf16_t* rp = a0.in_n + ((b0 + pb) * T + pt) * DE;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (pin) v = *reinterpret_cast<const u32x4*>(rp + 16 * s + 8 * (lane >> 5));
+      qf[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
+  const int b_lo = p0 / T, b_hi = (min(p0 + CL_ROWS, nphys) - 1) / T;
+  const int nrun = a0.heads_run;
+#pragma unroll 1
+  for (int hz = 0; hz < nrun; ++hz) {
+    const ClArgs a = head_args(a0, hz);
+    const Geo g = geo(a, mb);
+    if (g.n == 0) continue;
+    XRow xr;
+    xr.live = !ppad && pt >= g.off;
+    xr.x = xr.live ? pb * g.L + pt - g.off : -1;
+    xr.sq = xr.live ? pb : -2;
+    xr.sh = 0.f; xr.w = 0.f; xr.cap = 0.f;
+    xr.q = (!FIXED && a.lq && xr.live) ? a.lqcol[base + xr.x] * LOG2E : 0.f;
+    const bool wmask = __ballot(!xr.live) != 0ull;
+    RowCursor<true> cur;
+    cur.init(a.out_n + (g.b0 * (a.T + 1) * a.NH + a.head) * DE, (a.T + 1) * a.NH * DE, a.NH * DE, g.L, w, lane);
+    __syncthreads();  // the previous head's last tiles are read before this head's prologue restages the ring
+    cl_bwd32_head<false, FIXED, SB>(sh, dacc, qf, roff, toff, a, g, base, xr, wmask, b_lo * g.L, (b_hi + 1) * g.L, cur,
+                                w, lane);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) sh.ep[w][8 * (v >> 2) + 4 * (lane >> 5) + (v & 3)][32 * nd + r32] = dacc[nd][v];
+  const int sub = lane & 15;
+#pragma unroll 1
+  for (int ps = 0; ps < 8; ++ps) {
+    const int rl = 4 * ps + (lane >> 4), q = p0 + 32 * w + rl;
+    const int qc = min(q, nphys - 1);
+    const int b = qc / T, t = qc - b * T;
+    const int64_t ro = (b0 + b) * T + t;
+    const bool pad = a0.mask[(b0 + b) * a0.mask_stride + t] != 0;
+    float gv[8];
+    const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
+    const float4 u1 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub + 4]);
+    const float gz = pad ? 0.f : gs;  // pad rows of `in`: every logit against them is excluded
+    gv[0] = gz * u0.x; gv[1] = gz * u0.y; gv[2] = gz * u0.z; gv[3] = gz * u0.w;
+    gv[4] = gz * u1.x; gv[5] = gz * u1.y; gv[6] = gz * u1.z; gv[7] = gz * u1.w;
+    normalize_bwd_store(gv, a0.t_raw, a0.t_dtype, a0.t_norm[ro], a0.dt, ro * DE + 8 * sub, q < nphys);
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -1087,6 +1459,10 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.lq = d->logq; a.lq_stride = d->logq_stride; a.lqcol = d->logq_col;
   a.y_raw = (const bf16_t*)d->y_raw; a.y_norm = d->y_norm; a.dy = (bf16_t*)d->dy;
   a.head_stride = d->head_stride;
+  a.y_dtype = d->y_dtype;
+  a.heads_run = d->heads_run > 1 ? d->heads_run : 1;
+  a.t_raw = d->t_raw; a.t_dtype = d->t_dtype; a.t_norm = d->t_norm; a.dt = d->dt;
+  a.prio = 0;
   return a;
 }
 
@@ -1205,14 +1581,50 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
 }
 
 extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream) {
-  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->diag && (d->d_out || d->dy) && d->d_in);
-  LTHM_REQUIRE(!d->dy || (d->y_raw && d->y_norm));
+  LTHM_REQUIRE(cl_check(d) == 0 && d->lse && d->w && d->diag);
+  const int nrun = d->heads_run > 1 ? d->heads_run : 1;
+  LTHM_REQUIRE(d->head + nrun <= d->n_heads);
+  LTHM_REQUIRE(nrun == 1 || d->head_stride >= (int64_t)d->n_mb * d->n_max);
+  const bool fused = d->y_raw && d->y_norm && d->dy && d->t_raw && d->t_norm && d->dt;
   ClArgs a = cl_args(d);
+  a.colb = d->diag;  // the shift scratch (advanced per head by head_args)
+  static const int prio = getenv("LTHM_CL_PRIO") ? atoi(getenv("LTHM_CL_PRIO")) : 0;
+  a.prio = prio;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb), dim3(256), 0, s, a, d->diag);
+  const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
+  if (fused) {
+    // every head in one call: the COLS pass sums dIn over the heads and writes dt once
+    LTHM_REQUIRE(d->head == 0 && nrun == d->n_heads);
+    LTHM_REQUIRE((d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32) &&
+                 (d->t_dtype == LTHM_BF16 || d->t_dtype == LTHM_F32));
+    hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+    const dim3 grows((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
+    const dim3 gcols((int)(((int64_t)d->mb_size * d->T + CL_ROWS - 1) / CL_ROWS), d->n_mb, 1);
+    static const int sb = getenv("LTHM_CL_SB") ? atoi(getenv("LTHM_CL_SB")) : 1;  // A/B switch (phase fences)
+    if (fixed && sb) {
+      hipLaunchKernelGGL((cl_bwd32_k<true, true, true>), grows, dim3(256), 0, s, a);
+      LTHM_CHECK_LAUNCH();
+      hipLaunchKernelGGL((cl_bwd32_k<false, true, true>), gcols, dim3(256), 0, s, a);
+    } else if (fixed) {
+      hipLaunchKernelGGL((cl_bwd32_k<true, true, false>), grows, dim3(256), 0, s, a);
+      LTHM_CHECK_LAUNCH();
+      hipLaunchKernelGGL((cl_bwd32_k<false, true, false>), gcols, dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((cl_bwd32_k<true, false, true>), grows, dim3(256), 0, s, a);
+      LTHM_CHECK_LAUNCH();
+      hipLaunchKernelGGL((cl_bwd32_k<false, false, true>), gcols, dim3(256), 0, s, a);
+    }
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
+  // one head, f32 d_in accumulated (16x16x32 kernels)
+  LTHM_REQUIRE(nrun == 1 && (d->d_out || d->dy) && d->d_in);
+  LTHM_REQUIRE(!d->dy || (d->y_raw && d->y_norm && d->y_dtype == LTHM_BF16));
+  hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb);
-  if (2.f / d->tau <= 80.f && !d->logq) {
+  if (fixed) {
     hipLaunchKernelGGL((cl_bwd_k<true, true>), grid, dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     hipLaunchKernelGGL((cl_bwd_k<false, true>), grid, dim3(256), 0, s, a);

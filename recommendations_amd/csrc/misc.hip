@@ -85,7 +85,7 @@ __global__ __launch_bounds__(1024) void logq_stream_k(const int64_t* __restrict_
                                                       float* __restrict__ btab, float* __restrict__ atab,
                                                       const int64_t* __restrict__ offs, int n_mod, int64_t nb,
                                                       float alpha, int64_t batch_idx0, float beta, int update,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, float* __restrict__ scratch) {
   const int n_mb = (int)((B + mbs - 1) / mbs);
   for (int mb = 0; mb < n_mb; ++mb) {
     const int64_t b0 = (int64_t)mb * mbs;
@@ -94,24 +94,26 @@ __global__ __launch_bounds__(1024) void logq_stream_k(const int64_t* __restrict_
     for (int m = 0; m < (update ? n_mod : 0); ++m) {
       float* bt = btab + (int64_t)m * nb;
       float* at = atab + (int64_t)m * nb;
-      for (int64_t i0 = 0; i0 < cnt; i0 += 1024) {
-        const int64_t i = i0 + threadIdx.x;
-        int64_t h = -1;
-        float nbv = 0.f;
-        if (i < cnt) {
-          const int64_t bb = b0 + i / T, t = i % T;
-          if (!mask || !mask[bb * mask_stride + t]) {
-            h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
-            nbv = (1.f - alpha) * bt[h] + alpha * (idx - at[h]);
-          }
+      // every token of the mini-batch computes its bucket's new value from the state before
+      // the mini-batch (the reference's index_put: duplicates agree, whichever writes last),
+      // then all of them write: two passes over the whole mini-batch with a barrier between
+      for (int64_t i = threadIdx.x; i < cnt; i += 1024) {
+        const int64_t bb = b0 + i / T, t = i % T;
+        if (!mask || !mask[bb * mask_stride + t]) {
+          const int64_t h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
+          scratch[i] = (1.f - alpha) * bt[h] + alpha * (idx - at[h]);
         }
-        __syncthreads();  // every read of this chunk before any write
-        if (h >= 0) {
-          bt[h] = nbv;
+      }
+      __syncthreads();
+      for (int64_t i = threadIdx.x; i < cnt; i += 1024) {
+        const int64_t bb = b0 + i / T, t = i % T;
+        if (!mask || !mask[bb * mask_stride + t]) {
+          const int64_t h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
+          bt[h] = scratch[i];
           at[h] = idx;
         }
-        __syncthreads();
       }
+      __syncthreads();
     }
     for (int64_t i = threadIdx.x; out && i < cnt; i += 1024) {
       const int64_t bb = b0 + i / T, t = i % T;
@@ -262,13 +264,15 @@ extern "C" int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed
 extern "C" int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride,
                                 int64_t B, int32_t T, int32_t mb_size, float* b_tables, float* a_tables,
                                 const int64_t* hash_offsets, int32_t n_modules, int64_t num_buckets, float alpha,
-                                int64_t batch_idx0, float beta, int32_t update, float* out, void* stream) {
+                                int64_t batch_idx0, float beta, int32_t update, float* out, float* scratch,
+                                void* stream) {
   LTHM_REQUIRE(B >= 0 && T > 0 && mb_size > 0 && n_modules > 0 && num_buckets > 0);
   LTHM_REQUIRE(ids_stride >= T && (!mask || mask_stride >= T));
+  LTHM_REQUIRE(!update || scratch);
   if (B == 0) return 0;
   hipLaunchKernelGGL(logq_stream_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, ids, mask, B, T, ids_stride,
                      mask_stride, mb_size, b_tables, a_tables, hash_offsets, n_modules, num_buckets, alpha, batch_idx0,
-                     beta, update, out);
+                     beta, update, out, scratch);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

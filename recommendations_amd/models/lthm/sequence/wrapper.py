@@ -18,6 +18,7 @@ beta = 0, where the correction is exactly zero).
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 from typing import Dict, List, Optional
 
@@ -26,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
-from ...._lib import STRUCTS, call, load, ptr, stream
+from ...._lib import STRUCTS, call, dcode, load, ptr, stream
 from ....commons.base_model_wrapper import BaseModelWrapper
 from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
@@ -105,30 +106,52 @@ class ContrastiveLossFn(torch.autograd.Function):
     def backward(ctx, dloss):
         yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc = ctx.saved_tensors
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
-        dev = yc.device
         g = dloss.contiguous().float()
-        # dy (bf16, the gradient through F.normalize) comes straight out of the ROWS kernel:
-        # every element is written (kept rows by the kernel, the t >= L tail of each head
-        # by its prologue), so no fill and no f32 d_out round trip
+        if _OLD_BWD:
+            return ContrastiveLossFn._backward_per_head(ctx, g)
+        # every head in one call: the ROWS kernel writes dy per head through F.normalize, the
+        # COLS kernel sums dIn over the six heads on chip and writes dt once through F.normalize
+        dy = torch.empty_like(yc)
+        dt = torch.empty_like(tc)
+        d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, 0, De, mbs, n_mb, n_max, tau, offsets_dev,
+                                    lse[0], None, None, None, diag[0], w[0],  # diag: shift scratch
+                                    logq, None if lqc is None else lqc[0])
+        d.heads_run, d.head_stride = NH, n_mb * n_max
+        d.gscale = ptr(g)
+        d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
+        d.t_raw, d.t_norm, d.dt, d.t_dtype = ptr(tc), ptr(tnorm), ptr(dt), dcode(tc)
+        # algorithmic work 3 x 2 n^2 De per head (one S recompute, dS . in, dS^T . out);
+        # the ROWS and COLS kernels each recompute S, so they execute 4 x
+        call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
+             _work=3.0 * float(sum(ctx.flops)), _unit="flop")
+        return dy, dt, None, None, None, None
+
+    @staticmethod
+    def _backward_per_head(ctx, g):
+        """The round-2 backward (16x16x32 kernels, one call per head, f32 d_in read-modify-written
+        per head); kept behind LTHM_CL_BWD_OLD=1 for A/B measurements."""
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc = ctx.saved_tensors
+        B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
+        dev = yc.device
         fuse = yc.dtype == torch.bfloat16
         dy = torch.empty_like(yc) if fuse else None
         d_out = None if fuse else torch.empty((B, T + 1, NH, De), dtype=torch.float32, device=dev)
         d_in = K.zeros((B, T, De), torch.float32, dev)
         for h in range(NH):
             d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, h, De, mbs, n_mb, n_max, tau, offsets_dev,
-                                        lse[h], None, None, None, diag[h], w[h],  # diag: shift scratch
-                                        logq, None if lqc is None else lqc[h])
+                                        lse[h], None, None, None, diag[h], w[h], logq, None if lqc is None else lqc[h])
             d.gscale, d.d_out, d.d_in = ptr(g), ptr(d_out), ptr(d_in)
             if fuse:
-                d.y_raw, d.y_norm, d.dy = ptr(yc), ptr(ynorm), ptr(dy)
-            # algorithmic work 3 x 2 n^2 De per head (one S recompute, dS . in, dS^T . out);
-            # the ROWS and COLS kernels each recompute S, so they execute 4 x
+                d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
             call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
                  _work=3.0 * ctx.flops[h], _unit="flop")
         if not fuse:
             dy, _ = K.rownorm_bwd(yc.view(-1, De), ynorm, d_out.view(-1, De))
         dt, _ = K.rownorm_bwd(tc.view(-1, De), tnorm, d_in.view(-1, De))
         return dy.view(yc.shape), dt.view(tc.shape), None, None, None, None
+
+
+_OLD_BWD = os.environ.get("LTHM_CL_BWD_OLD") == "1"
 
 
 def contrastive_step(y, tgt, mask, offs: np.ndarray, mbs: int, tau: float, ks: List[int], logq=None):
@@ -234,10 +257,10 @@ class LTHMModelWrapper(BaseModelWrapper):
         # non-pad ids, then the correction -beta * logQ of its ids (zeroed on the positive
         # in-kernel).  The streaming estimates advance whatever beta is, as the reference's do;
         # the correction enters the loss only when beta != 0 (with beta = 0 it is exactly zero)
-        logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
-                                                  self._log_q_beta)
-        if self._log_q_beta == 0.0:
-            logq = None
+        logq = None
+        if self._log_q_beta != 0.0:
+            logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
+                                                      self._log_q_beta)
         loss, stats = contrastive_step(y, tgt, mask, offs, mbs, self._softmax_temperature, self._metrics_k_all, logq)
         self.batch_idx += n_mb  # the reference counts helper calls, one per mini-batch
         self.last_stats = (stats, offs, step_type, B, T, mbs, whole)

@@ -178,13 +178,13 @@ def test_lthm_training_steps(dev):
 
 def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     """BASELINE configs[4] (C5) shape at a small batch: T = 512 (T' = 513, the windowed
-    attention), d = 512, H = 8, fp8 e4m3 forward encoder GEMMs, 8-sequence loss
-    mini-batches, vs the fp32 oracle.  e4m3 operands (3 mantissa bits, per-tensor
+    attention), d = 512, H = 8, fp8 e4m3 forward encoder GEMMs, the yaml's 32-sequence loss
+    mini-batch (here the whole 16-sequence batch: 8,192 logit rows per head), vs the fp32 oracle.  e4m3 operands (3 mantissa bits, per-tensor
     scales): 5e-2 on the loss and the head outputs, 8e-2 relative on gradients (2x the
     measured maximum)."""
     from recommendations_amd.data import synthetic_lthm_batch
     B, T = 16, 512
-    cfg, m = _model(dev, T=T, d=512, L=2, H=8, n_cat=0, fp8=True, train_mini_batch_size=8)
+    cfg, m = _model(dev, T=T, d=512, L=2, H=8, n_cat=0, fp8=True, train_mini_batch_size=32)
     batch = synthetic_lthm_batch(B, T, n_cat=0, seed=5)
     sd = {k: (v.detach().cpu().float().clone().requires_grad_(True) if v.is_floating_point() else v.cpu())
           for k, v in m.state_dict().items()}
@@ -192,7 +192,7 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     state = m._rng.getstate()
     loss, _ = m.train_step(batch, out)
     m._rng.setstate(state)
-    offs = m.draw_offsets((B + 7) // 8)
+    offs = m.draw_offsets((B + 31) // 32)
     loss_ref, ro = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs, return_outputs=True)
     check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 5e-2)
     check('out["next_token_emb"].float(), ro["y"]', relerr(out["next_token_emb"].float(), ro["y"]), 5e-2)
@@ -205,6 +205,37 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
         check(f"grad {n}", relerr(p.grad, sd[n].grad), 8e-2)  # measured max 4.0e-2 (r02a)
         checked += 1
     assert checked > 20
+
+
+def test_lthm_val_step_whole_batch(dev):
+    """val_step runs the loss helper once over the whole batch (wrapper.py:75-80): here
+    B = 256, T = 32, i.e. 8,192 logit rows per head in one mini-batch.  Checked against
+    the oracle loss on the model's own outputs (bf16-rounded unit vectors, as in
+    test_gpu_loss) at 1e-4, and the metric keys of a whole-batch helper call."""
+    import torch.nn.functional as F
+    from oracle.lthm_ref import contrastive_loss
+    from recommendations_amd.data import synthetic_lthm_batch
+    cfg, m = _model(dev)
+    m.eval()
+    B = 256
+    batch = synthetic_lthm_batch(B, 32, n_cat=2, seed=9, device=dev)
+    with torch.no_grad():
+        out = m(batch)
+        state = m._rng.getstate()
+        loss, _ = m.val_step(batch, out)
+    m._rng.setstate(state)
+    offs = m.draw_offsets(1)
+
+    def unit(x):
+        n = F.normalize(x.float().cpu(), p=2.0, dim=-1)
+        return n.to(torch.bfloat16).float()
+    ref_loss, _ = contrastive_loss(unit(out["next_token_emb"]), unit(out["current_token_emb"]),
+                                   out["current_token_mask"].cpu().bool(), offs, B, cfg.softmax_temperature,
+                                   list(cfg.metrics_k_all), normalize=False)
+    check("val loss (whole batch)", abs(float(loss) - float(ref_loss)) / abs(float(ref_loss)), 1e-4)
+    met = m.metrics()
+    assert met["val_batch_size"] == B and "val_overall_batch_size" not in met and "val_loss" in met
+    assert abs(met["val_loss"] - float(loss)) <= 1e-5 * abs(float(loss))
 
 
 def test_lthm_multi_step_vs_oracle_adamw(dev):
