@@ -148,7 +148,8 @@ def load_torch_ops() -> None:
 class KernelTimer:
     """Live per-entry-point timing with HIP events on torch's current stream (the
     stream every launch goes to).  bench.py enables it over the timed region;
-    ``work`` is the algorithmic bytes / flops the wrapper declares per call."""
+    ``work`` is the algorithmic bytes / flops the wrapper declares per call, or a
+    callable evaluated in summary() for data-dependent work (e.g. touched rows)."""
 
     def __init__(self, only=None):
         self.records = []  # (key, ev0, ev1, work, unit, bytes)
@@ -161,6 +162,8 @@ class KernelTimer:
             s = out.setdefault(key, {"calls": 0, "ms": 0.0, "work": 0.0, "unit": unit, "bytes": 0.0})
             s["calls"] += 1
             s["ms"] += e0.elapsed_time(e1)
+            if callable(work):  # data-dependent work (a device count snapshot), read after the timed region
+                work = work()
             s["work"] += work or 0.0
             s["bytes"] += nbytes or 0.0
         return out

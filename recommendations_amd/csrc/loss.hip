@@ -18,8 +18,6 @@
 // count #{c != r : logit[r, c] > logit[r, r]}.
 #include "common.hpp"
 
-#include <cstdlib>
-
 namespace lthm {
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -247,7 +245,6 @@ struct ClArgs {
   int64_t head_stride;  // several heads per launch: per-head buffer stride (head = head0 + z)
   int y_dtype;          // dtype of y_raw / dy (LTHM_F32 / LTHM_BF16)
   int heads_run;        // heads head0 .. head0 + heads_run - 1
-  int prio;             // backward: s_setprio 1 around the MFMA clusters (A/B switch LTHM_CL_PRIO)
   // COLS epilogue through F.normalize: dt = (g - t^ (t^ . g)) / |t| of current_token_emb
   const void* t_raw;    // [B, T, DE], dtype t_dtype
   int t_dtype;
@@ -1116,12 +1113,13 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8v a, bf16x8v b, f32x16 c) {
 
 constexpr int CL_EPS = 132;  // epilogue restage row stride (floats): conflict-free b32 writes / b128 reads
 
+constexpr int CL_NB32 = 4;  // image ring depth of the 32x32x16 backward: three tiles of DMA in flight
 struct ClTile32 {
   union {
     struct {
-      unsigned char img[CL_NBUF][64 * 256];
-      float m0[CL_NBUF][4][64];  // per-wave copies of a per-image-row vector (COLS: shift; ROWS !FIXED: logQ)
-      float m1[CL_NBUF][4][64];  // COLS: row weights of the image rows
+      unsigned char img[CL_NB32][64 * 256];
+      float m0[CL_NB32][4][64];  // per-wave copies of a per-image-row vector (COLS: shift; ROWS !FIXED: logQ)
+      float m1[CL_NB32][4][64];  // COLS: row weights of the image rows
     } r;
     float ep[4][32][CL_EPS];     // epilogue: each wave's 32 x 128 f32 accumulator, row-major
   };
@@ -1165,7 +1163,7 @@ struct XRow {
 // dacc[nd] += dS^T . img over every image tile of one head (ROWS: image = `in` columns of the
 // head; COLS: image = out rows of the head).  The special range [spec_lo, spec_hi) holds the
 // image rows of the register rows' own sequences (diagonal, same-sequence exclusion).
-template <bool ROWS, bool FIXED, bool SB>
+template <bool ROWS, bool FIXED>
 __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], const bf16x8v (&qf)[8],
                                               const int (&roff)[8], const int (&toff)[4][2], const ClArgs& a,
                                               const Geo& g, int64_t base, const XRow& xr, bool wmask, int spec_lo,
@@ -1175,7 +1173,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
   const float* shift = a.diag;
   const int ntile = (g.n + 63) / 64;
   auto stage = [&](int t) {
-    const int buf = t % CL_NBUF, y0 = t * 64;
+    const int buf = t % CL_NB32, y0 = t * 64;
     cur.stage(sh.r.img[buf], g.n, w, lane);
     if (!ROWS) {
       const bool inr = y0 + lane < a.n_max;  // past n_max: shift -inf, weight 0
@@ -1185,25 +1183,20 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
       glds4(a.lq && y0 + lane < a.n_max ? a.lqcol + base + y0 + lane : &cl_zero_f, sh.r.m0[buf][w]);
     }
   };
+  constexpr int PT = ROWS ? (FIXED ? 4 : 5) : 6;  // DMAs per wave and tile
   retire_loads();
   stage(0);
   if (ntile > 1) stage(1);
+  if (ntile > 2) stage(2);
   for (int tI = 0; tI < ntile; ++tI) {
-    const int cb = tI % CL_NBUF, y0 = tI * 64;
-    if (tI + 1 < ntile) {
-      if (ROWS) wait_vm<FIXED ? 4 : 5>();
-      else wait_vm<6>();
-    } else {
-      wait_vm<0>();
-    }
+    const int cb = tI % CL_NB32, y0 = tI * 64;
+    if (tI + 2 < ntile) wait_vm<2 * PT>();
+    else if (tI + 1 < ntile) wait_vm<PT>();
+    else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    if (tI + 2 < ntile) stage(tI + 2);
+    if (tI + 3 < ntile) stage(tI + 3);
     const unsigned char* img = sh.r.img[cb];
     f32x16 acc[2];
-    // phases are fenced with sched_barrier so that the compiler does not hoist every LDS
-    // fragment of the tile at once (that alone needs 128 VGPRs): two waves per SIMD overlap
-    // one wave's exp2 / packing with the other's MFMAs instead
-    if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
 #pragma unroll
@@ -1213,9 +1206,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
         const bf16x8v af = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ib * 8192 + roff[s]));
         acc[ib] = mfma32(af, qf[s], acc[ib]);
       }
-      if (SB) __builtin_amdgcn_sched_barrier(0);
     }
-    if (a.prio) __builtin_amdgcn_s_setprio(0);
     const bool special = !FIXED || (y0 < spec_hi && y0 + 64 > spec_lo);
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
@@ -1262,8 +1253,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
       }
       // dacc[32 x 128] += dS[32 x 32] . img[32 x 128] of this image block: k-step ks = 2 ib + hf
       // holds image rows 16 ks + 8 (j>>2) + 4 hh + (j&3) in element j (registers 8 hf .. 8 hf + 7)
-      if (a.prio) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
+  #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         const int ks = 2 * ib + hf, o = 8 * hf;
         const f32x16& pv = acc[ib];
@@ -1277,9 +1267,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
           dacc[nd] = mfma32(af, bfr, dacc[nd]);
         }
       }
-      if (a.prio) __builtin_amdgcn_s_setprio(0);
-      if (SB) __builtin_amdgcn_sched_barrier(0);
-    }
+      }
   }
 }
 
@@ -1311,7 +1299,7 @@ __device__ __forceinline__ void normalize_bwd_store(const float (&gv)[8], const 
   }
 }
 
-template <bool ROWS, bool FIXED, bool SB>
+template <bool ROWS, bool FIXED>
 __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
   __shared__ __attribute__((aligned(16))) ClTile32 sh;
   const int nz = ROWS ? gridDim.z : 1;
@@ -1359,7 +1347,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
     own_cols(g, x0, spec_lo, spec_hi);
     RowCursor<true> cur;
     cur.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
-    cl_bwd32_head<true, FIXED, SB>(sh, dacc, qf, roff, toff, a, g, base, xr, false, spec_lo, spec_hi, cur, w, lane);
+    cl_bwd32_head<true, FIXED>(sh, dacc, qf, roff, toff, a, g, base, xr, false, spec_lo, spec_hi, cur, w, lane);
     // epilogue: restage, then 16 lanes per row through F.normalize into dy
     __syncthreads();
 #pragma unroll
@@ -1417,7 +1405,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
     RowCursor<true> cur;
     cur.init(a.out_n + (g.b0 * (a.T + 1) * a.NH + a.head) * DE, (a.T + 1) * a.NH * DE, a.NH * DE, g.L, w, lane);
     __syncthreads();  // the previous head's last tiles are read before this head's prologue restages the ring
-    cl_bwd32_head<false, FIXED, SB>(sh, dacc, qf, roff, toff, a, g, base, xr, wmask, b_lo * g.L, (b_hi + 1) * g.L, cur,
+    cl_bwd32_head<false, FIXED>(sh, dacc, qf, roff, toff, a, g, base, xr, wmask, b_lo * g.L, (b_hi + 1) * g.L, cur,
                                 w, lane);
   }
   __syncthreads();
@@ -1462,7 +1450,6 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.y_dtype = d->y_dtype;
   a.heads_run = d->heads_run > 1 ? d->heads_run : 1;
   a.t_raw = d->t_raw; a.t_dtype = d->t_dtype; a.t_norm = d->t_norm; a.dt = d->dt;
-  a.prio = 0;
   return a;
 }
 
@@ -1588,8 +1575,6 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
   const bool fused = d->y_raw && d->y_norm && d->dy && d->t_raw && d->t_norm && d->dt;
   ClArgs a = cl_args(d);
   a.colb = d->diag;  // the shift scratch (advanced per head by head_args)
-  static const int prio = getenv("LTHM_CL_PRIO") ? atoi(getenv("LTHM_CL_PRIO")) : 0;
-  a.prio = prio;
   hipStream_t s = (hipStream_t)stream;
   const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
   if (fused) {
@@ -1601,19 +1586,14 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
     LTHM_CHECK_LAUNCH();
     const dim3 grows((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
     const dim3 gcols((int)(((int64_t)d->mb_size * d->T + CL_ROWS - 1) / CL_ROWS), d->n_mb, 1);
-    static const int sb = getenv("LTHM_CL_SB") ? atoi(getenv("LTHM_CL_SB")) : 1;  // A/B switch (phase fences)
-    if (fixed && sb) {
-      hipLaunchKernelGGL((cl_bwd32_k<true, true, true>), grows, dim3(256), 0, s, a);
+    if (fixed) {
+      hipLaunchKernelGGL((cl_bwd32_k<true, true>), grows, dim3(256), 0, s, a);
       LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL((cl_bwd32_k<false, true, true>), gcols, dim3(256), 0, s, a);
-    } else if (fixed) {
-      hipLaunchKernelGGL((cl_bwd32_k<true, true, false>), grows, dim3(256), 0, s, a);
-      LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL((cl_bwd32_k<false, true, false>), gcols, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<false, true>), gcols, dim3(256), 0, s, a);
     } else {
-      hipLaunchKernelGGL((cl_bwd32_k<true, false, true>), grows, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<true, false>), grows, dim3(256), 0, s, a);
       LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL((cl_bwd32_k<false, false, true>), gcols, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<false, false>), gcols, dim3(256), 0, s, a);
     }
     LTHM_CHECK_LAUNCH();
     return 0;

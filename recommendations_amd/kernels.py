@@ -637,16 +637,35 @@ def _check_sparse_rows(rows, max_rows, p, flags, *states):
         _need(t, p.numel(), "state")
 
 
+def _touched_work(count, max_rows, per_row):
+    """Algorithmic bytes of a row-wise update for the live kernel timer: the touched-row
+    count is on the device, so it is snapshotted (one 8-byte copy, timed runs only) and
+    read after the timed region."""
+    from . import _lib
+    if _lib.TIMER is None:
+        return None
+    snap = count.clone()
+    return lambda: float(min(int(snap.item()), max_rows)) * per_row
+
+
 def sparse_adamw_(rows, count, max_rows, p, g, m, v, flags, lr, betas, eps, wd, step, shadow=None):
     _check_sparse_rows(rows, max_rows, p, flags, g, m, v, shadow)
-    call("lthm_sparse_adamw", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(m), ptr(v),
-         ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), stream())
+    D = p.shape[1]
+    # per touched row: its index, p / g / m / v read, p / m / v written, g zeroed, the touched flag,
+    # the bf16 shadow row
+    per_row = 8 + 4 + 8 * 4 * D + (2 * D if shadow is not None else 0)
+    call("lthm_sparse_adamw", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(m), ptr(v),
+         ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), stream(), _key="lthm_sparse_adamw",
+         _work=_touched_work(count, max_rows, per_row), _unit="byte")
 
 
 def sparse_adagrad_(rows, count, max_rows, p, g, s, flags, lr, lr_decay, eps, step, shadow=None):
     _check_sparse_rows(rows, max_rows, p, flags, g, s, shadow)
-    call("lthm_sparse_adagrad", ptr(rows), ptr(count), max_rows, p.shape[1], ptr(p), ptr(g), ptr(s), ptr(flags),
-         lr, lr_decay, eps, step, ptr(shadow), stream())
+    D = p.shape[1]
+    per_row = 8 + 4 + 6 * 4 * D + (2 * D if shadow is not None else 0)  # p / g / s read, p / s written, g zeroed
+    call("lthm_sparse_adagrad", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(s), ptr(flags),
+         lr, lr_decay, eps, step, ptr(shadow), stream(), _key="lthm_sparse_adagrad",
+         _work=_touched_work(count, max_rows, per_row), _unit="byte")
 
 
 def sumsq(x, acc):
@@ -1034,7 +1053,9 @@ def segmented_table_bwd(rows, dY, R, segments, out=None):
         call("lthm_segmented_table_bwd", ptr(rows), nidx, seg.shape[1], seg[0].ctypes.data, seg[1].ctypes.data,
              seg[2].ctypes.data, seg[3].ctypes.data, ptr(dY), dcode(dY), D, n, D, ptr(out),
              ptr(ws) if ws is not None else None, wsb, stream(),
-             _key="seg_tab_bwd_k", _work=float(n) * D * dY.element_size(), _unit="byte")
+             _key="seg_tab_bwd_k", _unit="byte",
+             # dY and the uint16 bucket rows read once, the [R, D] f32 gradient read and written
+             _work=float(n) * (D * dY.element_size() + 2 * nidx) + 8.0 * R * D)
     return out
 
 
@@ -1051,7 +1072,8 @@ class BCEWithLogitsFn(torch.autograd.Function):
         z, y = z.contiguous(), y.contiguous()
         n = z.numel()
         out = zeros((1,), torch.float32, z.device)
-        call("lthm_bce_logits_fwd", ptr(z), ptr(y), n, 1.0 / max(n, 1), ptr(out), stream())
+        call("lthm_bce_logits_fwd", ptr(z), ptr(y), n, 1.0 / max(n, 1), ptr(out), stream(), _key="bce_fwd_k",
+             _work=8.0 * n, _unit="byte")
         ctx.save_for_backward(z, y)
         return out.view(())
 
@@ -1060,7 +1082,8 @@ class BCEWithLogitsFn(torch.autograd.Function):
         z, y = ctx.saved_tensors
         dz = torch.empty_like(z)
         g = g.contiguous().float()
-        call("lthm_bce_logits_bwd", ptr(z), ptr(y), z.numel(), ptr(g), 1.0 / max(z.numel(), 1), ptr(dz), stream())
+        call("lthm_bce_logits_bwd", ptr(z), ptr(y), z.numel(), ptr(g), 1.0 / max(z.numel(), 1), ptr(dz), stream(),
+             _key="bce_bwd_k", _work=12.0 * z.numel(), _unit="byte")
         return dz, None
 
 

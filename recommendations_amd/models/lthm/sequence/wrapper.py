@@ -34,6 +34,7 @@ from ....optim import FusedAdamW, SparseRowAdamW
 from .encoder import Encoder
 
 NSTAT_BASE = 7
+LOSS_DE = 128  # operand width the loss kernels are compiled for (csrc/loss.hip DE)
 _KS_DEV: Dict[tuple, torch.Tensor] = {}  # (metric ks, device) -> int32 device copy
 
 
@@ -185,6 +186,12 @@ class LTHMModelWrapper(BaseModelWrapper):
     def __init__(self, model_config, stats=None):
         super().__init__(dummy_params=model_config.sparse, sparse=model_config.sparse)
         self.model_config = model_config
+        de = model_config.product_tower.product_emb_dim
+        if de != LOSS_DE:
+            # the fused loss kernels are compiled for one operand width (csrc/loss.hip DE); refuse at
+            # construction instead of at the first train_step (query_tower.py:54-55, product_tower.py:37-39)
+            raise ValueError(f"product_emb_dim={de} is not supported by the fused contrastive loss kernels "
+                             f"(built for product_emb_dim={LOSS_DE}, model/lthm.yaml:22)")
         self._sparse = model_config.sparse
         self._softmax_temperature = model_config.softmax_temperature
         self._export_span = model_config.export_span

@@ -106,3 +106,15 @@ def test_loss_log_batches_host_syncs():
     ll.flush()
     assert seen == [("MASK", 0, 1, 0, 1.5)]
     _LossLog(None, "x", 1, 1).add(0, 0, torch.tensor(0.0))  # no logger: nothing kept
+
+
+def test_unsupported_loss_width_refused_at_construction():
+    """The fused loss kernels take product_emb_dim = 128 (model/lthm.yaml:22); another width
+    is refused when the wrapper is built, not at the first train_step."""
+    import pytest
+    from recommendations_amd.models.lthm.builder import LTHMModelBuilder
+    from recommendations_amd.models.lthm.config import lthm_config
+    cfg = lthm_config(T=16, d=64, n_layers=1, n_head=1, cat_features=0, item_vocab=1000, log_q_buckets=1 << 10)
+    cfg.product_tower.product_emb_dim = 64
+    with pytest.raises(ValueError, match="product_emb_dim=64"):
+        LTHMModelBuilder(None, cfg).build()
