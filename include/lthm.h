@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 25 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 26 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -441,6 +441,23 @@ int lthm_tokens_bwd(const lthm_tokens_desc* desc, const float* dx0, void* dP, fl
 int lthm_outcome_fwd(const float* x, const int64_t* labels, int64_t B, int32_t T_full, int32_t trim,
                      int64_t future, const float* table, int32_t n_outcomes, int32_t D, void* out,
                      uint16_t* rows, void* stream);
+
+/* Row-sharded KShift lookup routing (C3 item table; commons/layers.py:152-185 row math,
+ * SURVEY §8e): global row r on rank r % world at local index r / world.
+ * lthm_shard_route: the K rows of n_items ids, deduplicated per workgroup of 2,048 (row, shift)
+ * pairs (LDS bitonic sort), laid out owner-major in send_rows [capacity n_items * K];
+ * send_counts [world] and owner_base [world + 1] (owner_base[world] = the request total) stay on
+ * the device; inv [n_items * K] holds, for every pair, the position of its row's value in the
+ * buffer the exchange returns (owner-major, the send order).  Replaces torch.unique / argsort /
+ * bincount of the reference-style exchange; workspace: lthm_shard_route_ws_bytes bytes. */
+int64_t lthm_shard_route_ws_bytes(int64_t n_pairs, int32_t world);
+int lthm_shard_route(const int64_t* ids, int64_t n_items, int32_t K, int64_t P, int32_t world, int64_t* send_rows,
+                     int64_t* send_counts, int64_t* owner_base, int64_t* inv, void* workspace, int64_t ws_bytes,
+                     void* stream);
+/* out[i] = shard[rows[i] / world] (row_bytes a multiple of 16) for i < min(*count, cap) (count NULL: cap);
+ * the owner side of the exchange (and the whole lookup at world 1) */
+int lthm_shard_gather(const void* shard, int64_t n_local, int32_t row_bytes, const int64_t* rows,
+                      const int64_t* count, int64_t cap, int32_t world, void* out, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* In-batch contrastive loss (models/lthm/sequence/wrapper.py:114-245)        */

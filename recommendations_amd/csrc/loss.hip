@@ -601,18 +601,18 @@ __device__ float cl_zero_f = 0.f;
 // source row of column c = (b, t) (sequence b of the mini-batch, position t) sits
 // at base + b * sb + t * st elements; the cursor advances (b, t) by 64 columns a
 // tile without a division.
-template <bool SW32 = false>
+template <bool SW32 = false, int NK = 4>
 struct RowCursor {
   const bf16_t* base;
   int sb, st, L, q64, r64;
-  int b[4], t[4], choff[4];
+  int b[NK], t[NK], choff[NK];
   int c;  // column of this lane's k = 0 row in the next tile to stage
   __device__ __forceinline__ void init(const bf16_t* base_, int sb_, int st_, int L_, int w, int lane) {
     base = base_; sb = sb_; st = st_; L = L_;
     q64 = 64 / L; r64 = 64 - q64 * L;
-    c = 16 * w + (lane >> 4);
+    c = 4 * NK * w + (lane >> 4);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NK; ++k) {
       const int row = c + 4 * k;
       b[k] = row / L;
       t[k] = row - b[k] * L;
@@ -622,10 +622,10 @@ struct RowCursor {
   // stage the next tile into img (the tile's 64-row image), then advance by 64 columns
   __device__ __forceinline__ void stage(unsigned char* img, int n, int w, int lane) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NK; ++k) {
       const void* src = (c + 4 * k < n) ? (const void*)(base + ((int64_t)b[k] * sb + t[k] * st + choff[k]))
                                         : (const void*)(cl_zero_row + 16 * (lane & 15));
-      glds16(src, img + (16 * w + 4 * k) * 256);
+      glds16(src, img + (4 * NK * w + 4 * k) * 256);
       t[k] += r64;
       b[k] += q64;
       if (t[k] >= L) { t[k] -= L; b[k] += 1; }
@@ -1114,14 +1114,15 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8v a, bf16x8v b, f32x16 c) {
 constexpr int CL_EPS = 132;  // epilogue restage row stride (floats): conflict-free b32 writes / b128 reads
 
 constexpr int CL_NB32 = 4;  // image ring depth of the 32x32x16 backward: three tiles of DMA in flight
+template <int NW>
 struct ClTile32 {
   union {
     struct {
       unsigned char img[CL_NB32][64 * 256];
-      float m0[CL_NB32][4][64];  // per-wave copies of a per-image-row vector (COLS: shift; ROWS !FIXED: logQ)
-      float m1[CL_NB32][4][64];  // COLS: row weights of the image rows
+      float m0[CL_NB32][NW][64];  // per-wave copies of a per-image-row vector (COLS: shift; ROWS !FIXED: logQ)
+      float m1[CL_NB32][NW][64];  // COLS: row weights of the image rows
     } r;
-    float ep[4][32][CL_EPS];     // epilogue: each wave's 32 x 128 f32 accumulator, row-major
+    float ep[NW][32][CL_EPS];     // epilogue: each wave's 32 x 128 f32 accumulator, row-major
   };
 };
 
@@ -1163,11 +1164,11 @@ struct XRow {
 // dacc[nd] += dS^T . img over every image tile of one head (ROWS: image = `in` columns of the
 // head; COLS: image = out rows of the head).  The special range [spec_lo, spec_hi) holds the
 // image rows of the register rows' own sequences (diagonal, same-sequence exclusion).
-template <bool ROWS, bool FIXED>
-__device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], const bf16x8v (&qf)[8],
+template <bool ROWS, bool FIXED, int NW>
+__device__ __forceinline__ void cl_bwd32_head(ClTile32<NW>& sh, f32x16 (&dacc)[4], const bf16x8v (&qf)[8],
                                               const int (&roff)[8], const int (&toff)[4][2], const ClArgs& a,
                                               const Geo& g, int64_t base, const XRow& xr, bool wmask, int spec_lo,
-                                              int spec_hi, RowCursor<true>& cur, int w, int lane) {
+                                              int spec_hi, RowCursor<true, 16 / NW>& cur, int w, int lane) {
   const int hh = lane >> 5;
   const float it = 1.f / a.tau, c1 = it * LOG2E;
   const float* shift = a.diag;
@@ -1183,7 +1184,8 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32& sh, f32x16 (&dacc)[4], c
       glds4(a.lq && y0 + lane < a.n_max ? a.lqcol + base + y0 + lane : &cl_zero_f, sh.r.m0[buf][w]);
     }
   };
-  constexpr int PT = ROWS ? (FIXED ? 4 : 5) : 6;  // DMAs per wave and tile
+  constexpr int NK = 16 / NW;
+  constexpr int PT = ROWS ? (FIXED ? NK : NK + 1) : NK + 2;  // DMAs per wave and tile
   retire_loads();
   stage(0);
   if (ntile > 1) stage(1);
@@ -1299,9 +1301,12 @@ __device__ __forceinline__ void normalize_bwd_store(const float (&gv)[8], const 
   }
 }
 
-template <bool ROWS, bool FIXED>
-__global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
-  __shared__ __attribute__((aligned(16))) ClTile32 sh;
+// NW waves per workgroup (32 NW register rows): 4 (two workgroups per CU) or 8 (one workgroup
+// per CU: each image tile is staged once for 256 register rows, half the DMA issue per wave)
+template <bool ROWS, bool FIXED, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void cl_bwd32_k(ClArgs a0) {
+  constexpr int XR = 32 * NW;  // register rows per workgroup
+  __shared__ __attribute__((aligned(16))) ClTile32<NW> sh;
   const int nz = ROWS ? gridDim.z : 1;
   const int per = gridDim.x * gridDim.y;
   const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (ROWS ? blockIdx.z : 0)), per * nz);
@@ -1324,7 +1329,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
   if (ROWS) {
     const ClArgs a = head_args(a0, z);
     const Geo g = geo(a, mb);
-    const int x0 = xb * CL_ROWS;
+    const int x0 = xb * XR;
     if (x0 >= g.n) return;
     XRow xr;
     xr.x = x0 + 32 * w + r32;
@@ -1343,11 +1348,10 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
     xr.cap = xr.w != 0.f ? __log2f(xr.w) : -INFINITY;
     xr.sq = xr.live ? seq_of(g, xr.x) : -2;
     xr.q = 0.f;
-    int spec_lo, spec_hi;
-    own_cols(g, x0, spec_lo, spec_hi);
-    RowCursor<true> cur;
+    const int spec_lo = (x0 / g.L) * g.L, spec_hi = ((min(x0 + XR, g.n) - 1) / g.L + 1) * g.L;
+    RowCursor<true, 16 / NW> cur;
     cur.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
-    cl_bwd32_head<true, FIXED>(sh, dacc, qf, roff, toff, a, g, base, xr, false, spec_lo, spec_hi, cur, w, lane);
+    cl_bwd32_head<true, FIXED, NW>(sh, dacc, qf, roff, toff, a, g, base, xr, false, spec_lo, spec_hi, cur, w, lane);
     // epilogue: restage, then 16 lanes per row through F.normalize into dy
     __syncthreads();
 #pragma unroll
@@ -1373,7 +1377,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
   // COLS: physical `in` rows p = b T + t of the mini-batch
   const int T = a0.T;
   const int nphys = Bm * T;
-  const int p0 = xb * CL_ROWS;
+  const int p0 = xb * XR;
   if (p0 >= nphys) return;
   const int p = p0 + 32 * w + r32;
   const bool pin = p < nphys;
@@ -1388,7 +1392,7 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
       qf[s] = __builtin_bit_cast(bf16x8v, v);
     }
   }
-  const int b_lo = p0 / T, b_hi = (min(p0 + CL_ROWS, nphys) - 1) / T;
+  const int b_lo = p0 / T, b_hi = (min(p0 + XR, nphys) - 1) / T;
   const int nrun = a0.heads_run;
 #pragma unroll 1
   for (int hz = 0; hz < nrun; ++hz) {
@@ -1402,10 +1406,10 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32_k(ClArgs a0) {
     xr.sh = 0.f; xr.w = 0.f; xr.cap = 0.f;
     xr.q = (!FIXED && a.lq && xr.live) ? a.lqcol[base + xr.x] * LOG2E : 0.f;
     const bool wmask = __ballot(!xr.live) != 0ull;
-    RowCursor<true> cur;
+    RowCursor<true, 16 / NW> cur;
     cur.init(a.out_n + (g.b0 * (a.T + 1) * a.NH + a.head) * DE, (a.T + 1) * a.NH * DE, a.NH * DE, g.L, w, lane);
     __syncthreads();  // the previous head's last tiles are read before this head's prologue restages the ring
-    cl_bwd32_head<false, FIXED>(sh, dacc, qf, roff, toff, a, g, base, xr, wmask, b_lo * g.L, (b_hi + 1) * g.L, cur,
+    cl_bwd32_head<false, FIXED, NW>(sh, dacc, qf, roff, toff, a, g, base, xr, wmask, b_lo * g.L, (b_hi + 1) * g.L, cur,
                                 w, lane);
   }
   __syncthreads();
@@ -1584,16 +1588,18 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
                  (d->t_dtype == LTHM_BF16 || d->t_dtype == LTHM_F32));
     hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
-    const dim3 grows((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
-    const dim3 gcols((int)(((int64_t)d->mb_size * d->T + CL_ROWS - 1) / CL_ROWS), d->n_mb, 1);
+    // 4 waves per workgroup, two workgroups per CU (8 waves, one workgroup per CU: the same
+    // time within 1% at C2, tools/prof_loss_ab.sh)
+    const dim3 grows((d->n_max + 127) / 128, d->n_mb, nrun);
+    const dim3 gcols((int)(((int64_t)d->mb_size * d->T + 127) / 128), d->n_mb, 1);
     if (fixed) {
-      hipLaunchKernelGGL((cl_bwd32_k<true, true>), grows, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<true, true, 4>), grows, dim3(256), 0, s, a);
       LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL((cl_bwd32_k<false, true>), gcols, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<false, true, 4>), gcols, dim3(256), 0, s, a);
     } else {
-      hipLaunchKernelGGL((cl_bwd32_k<true, false>), grows, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<true, false, 4>), grows, dim3(256), 0, s, a);
       LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL((cl_bwd32_k<false, false>), gcols, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((cl_bwd32_k<false, false, 4>), gcols, dim3(256), 0, s, a);
     }
     LTHM_CHECK_LAUNCH();
     return 0;
