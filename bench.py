@@ -315,18 +315,24 @@ def main():
     else:
         batch = synthetic_lthm_batch(B, cfgd["T"], n_cat=cfgd["n_cat"], seed=1234, rank=rank, device=dev)
 
-    # C3 on N > 1 GPUs: the row-sharded item table's lookup of the next step (dedup,
-    # the count exchange the host reads, two all_to_alls) runs on a side stream behind
-    # this step's optimizer, issued at the same point on every rank (Encoder.prefetch),
-    # so its host read leaves the step's critical path.  On one GPU (and for the
-    # replicated table) the inline lookup is as fast: C2 74,964 vs 74,871, C3 71,911
-    # vs 71,185 samples/s inline vs prefetched (profiles/r02_prefetch_ab.log)
+    # C3 on N > 1 GPUs: the row-sharded item table's lookup of the next step (routing, the
+    # count exchange the host reads, two all_to_alls on a communicator of their own) runs on
+    # a side stream, issued right after this step's forward at the same point on every rank
+    # (Encoder.prefetch): the side stream waits only for the batch's ids (batch_ready), so
+    # the host's read of the counts waits for the routing alone while this step's backward is
+    # queued on the main stream.  On one GPU (and for the replicated table) the inline lookup
+    # is as fast: C2 74,964 vs 74,871, C3 71,911 vs 71,185 samples/s inline vs prefetched
+    # (profiles/r02_prefetch_ab.log)
     pipelined = bool(cfgd.get("item_table_sharded")) and world > 1 and not args.no_prefetch
+    batch_ready = torch.cuda.Event()
+    batch_ready.record()  # the synthetic batch is resident from here on
     if pipelined:
-        model.prefetch(batch)
+        model.prefetch(batch, batch_ready)
 
     def step():
         out = model(batch)
+        if pipelined:
+            model.prefetch(batch, batch_ready)
         loss, _ = model.train_step(batch, out)
         loss.backward()
         allreduce()
@@ -334,8 +340,6 @@ def main():
         for o in opts:
             o.step()
             o.zero_grad(set_to_none=True)
-        if pipelined:
-            model.prefetch(batch)
         return loss, flags
 
     for _ in range(args.warmup):
@@ -401,7 +405,8 @@ def main():
                                 + (", fp8 e4m3 forward encoder GEMMs" if cfgd.get("fp8") else "")
                                 + (f", {cfgd['mbs']}-sequence loss mini-batches" if cfgd.get("mbs") else "")),
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
-                   "item_lookup": ("one step ahead on a side stream (Encoder.prefetch), inside the timed loop"
+                   "item_lookup": ("one step ahead on a side stream (Encoder.prefetch after the forward), "
+                                   "inside the timed loop"
                                    if pipelined else "inline"),
                    "parallelism": f"dp{world}" + (
                        (" (item table row-sharded, all_to_all row exchange; categorical tables table-wise "

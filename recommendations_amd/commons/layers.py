@@ -331,9 +331,10 @@ class RowShardedKShiftEmbedding(nn.Module):
     C3 100M-row item table; the LTHM item table is frozen,
     product_tower.py:47).  Global row r lives on rank r % world (interleaved:
     the KShift hot rows P-1, P-2, ... spread over ranks) at local index r // world.
-    forward: K row indices per id (kernel) -> dedup -> all_to_all of row ids ->
-    owners gather -> all_to_all of rows back -> in-order f32 pool of the
-    gathered rows (kernel), bit-identical to the unsharded KShiftEmbedding."""
+    forward: K row indices per id, deduplicated per workgroup (LDS bitonic sort) and laid
+    out per owner on the device (lthm_shard_route) -> all_to_all of row ids -> owners
+    gather (lthm_shard_gather) -> all_to_all of rows back -> in-order f32 pool of the
+    gathered rows (lthm_gather_pool), bit-identical to the unsharded KShiftEmbedding."""
 
     def __init__(self, num_embeddings: int, emb_dim: int, num_shifts: int = 8, normalize_output: bool = False, *,
                  rank: Optional[int] = None, world: Optional[int] = None, dtype=torch.bfloat16,
@@ -366,17 +367,18 @@ class RowShardedKShiftEmbedding(nn.Module):
 
     @torch.no_grad()
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        from ..distributed import exchange_rows
+        from ..distributed import exchange_routed
         if self._needs_init:
             g = torch.Generator(device=self.shard.device).manual_seed(1234 + self._rank)
             self.shard.data.normal_(generator=g)
             self._needs_init = False
         flat = ids.reshape(-1).contiguous()
-        rows = K.kshift_rows(flat, self._num_embeddings, self._num_shifts)  # [N, K] global rows
-        uniq, inv = torch.unique(rows.view(-1), return_inverse=True)
-        vals = exchange_rows(uniq, self.shard)
-        out = K.gather_pool(inv.view(flat.shape[0], self._num_shifts), vals, self._mode, out_dtype=self._out_dtype)
-        return out.view(*ids.shape, vals.shape[1])
+        # K rows per id, deduplicated per workgroup and laid out per owner on the device
+        # (csrc/shard.hip), exchanged, then pooled in order (lthm_gather_pool)
+        send, cnt, base, inv = K.shard_route(flat, self._num_embeddings, self._num_shifts, self._world)
+        vals = exchange_routed(send, cnt, base, self.shard)
+        out = K.gather_pool(inv, vals, self._mode, out_dtype=self._out_dtype)
+        return out.view(*ids.shape, self.shard.shape[1])
 
 
 # ------------------------------------------------------------------ feature interaction

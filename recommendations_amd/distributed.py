@@ -167,31 +167,49 @@ def gather_sparse_grads(ids: torch.Tensor, gy: torch.Tensor, out: Optional[torch
     return ids_all, gy_all, out, norms
 
 
-def exchange_rows(uniq: torch.Tensor, shard: torch.Tensor) -> torch.Tensor:
-    """Row-sharded table lookup: global row r lives on rank
-    r % world at local index r // world.  ``uniq`` are this rank's deduplicated
-    global rows; returns their values [len(uniq), D] in the same order.
-    Two all_to_all_single exchanges: row ids out (int64), row values back
-    (the shard dtype, bf16 for the frozen item table); one host read of the
-    per-peer counts."""
+_ROW_GROUPS = {}
+
+
+def row_exchange_group():
+    """A communicator of its own for the row-sharded item table's exchange: its all_to_alls run
+    on a side stream (Encoder.prefetch) beside the backward's gradient all-reduce on the main
+    communicator, and collectives of one communicator must not interleave across streams.
+    Created on first use, which every rank reaches at the same program point."""
+    if world_size() == 1:
+        return None
+    key = dist.get_world_size()
+    g = _ROW_GROUPS.get(key)
+    if g is None:
+        g = _ROW_GROUPS[key] = dist.new_group(list(range(key)))
+    return g
+
+
+def exchange_routed(send_rows: torch.Tensor, send_counts: torch.Tensor, owner_base: torch.Tensor,
+                    shard: torch.Tensor) -> torch.Tensor:
+    """Row-sharded table lookup: global row r lives on rank r % world at
+    local index r // world.  ``send_rows`` / ``send_counts`` / ``owner_base`` come from
+    kernels.shard_route (owner-major, deduplicated per workgroup); returns the values of
+    send_rows[:owner_base[world]] in that order ([total, D], shard dtype).
+
+    world 1: one owner gather bounded by the device-side total, no host read.  world > 1:
+    an all_to_all of the device counts, ONE host read of them (the variable splits), the
+    row ids out, the owners gather (lthm_shard_gather), the rows back."""
+    from . import kernels as K
     ws = world_size()
     if ws == 1:
-        return shard.index_select(0, uniq)
-    owner = torch.remainder(uniq, ws)
-    order = torch.argsort(owner, stable=True)
-    send_rows = uniq.index_select(0, order)
-    send_counts = torch.bincount(owner, minlength=ws)
+        return K.shard_gather(shard, send_rows, 1, count=owner_base[1:2])
+    grp = row_exchange_group()
     recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    recv_rows = torch.empty(sum(rc), dtype=torch.int64, device=uniq.device)
-    dist.all_to_all_single(recv_rows, send_rows, rc, sc)
-    vals = shard.index_select(0, torch.div(recv_rows, ws, rounding_mode="floor"))
-    back = torch.empty((sum(sc),) + tuple(shard.shape[1:]), dtype=shard.dtype, device=shard.device)
-    dist.all_to_all_single(back, vals, sc, rc)
-    out = torch.empty_like(back)
-    out.index_copy_(0, order, back)
-    return out
+    dist.all_to_all_single(recv_counts, send_counts, group=grp)
+    both = torch.cat([send_counts, recv_counts]).tolist()
+    sc, rc = both[:ws], both[ws:]
+    total = sum(sc)
+    recv_rows = torch.empty(sum(rc), dtype=torch.int64, device=send_rows.device)
+    dist.all_to_all_single(recv_rows, send_rows[:total], rc, sc, group=grp)
+    vals = K.shard_gather(shard, recv_rows, ws)
+    back = torch.empty((total,) + tuple(shard.shape[1:]), dtype=shard.dtype, device=shard.device)
+    dist.all_to_all_single(back, vals, sc, rc, group=grp)
+    return back
 
 
 def step_flags(stop: bool, loss: torch.Tensor) -> torch.Tensor:

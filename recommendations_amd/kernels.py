@@ -11,7 +11,7 @@ from typing import Any, Dict, Optional
 
 import torch
 
-from ._lib import BF16, F32, call, dcode, ptr, require_gpu, stream
+from ._lib import BF16, F32, call, dcode, load, ptr, require_gpu, stream
 
 KSHIFT_SCALE, KSHIFT_NORMALIZE, KSHIFT_NONE = 0, 1, 2
 
@@ -115,6 +115,43 @@ def gather_pool(rows: torch.Tensor, W: torch.Tensor, mode: int, out_dtype=torch.
     call("lthm_gather_pool", ptr(rows), n, Kk, ptr(W), dcode(W), W.shape[0], D, mode, ptr(out), dcode(out), None,
          stream(), _key="kshift_fwd_k", _work=n * (8 * Kk + Kk * D * W.element_size() + D * out.element_size()),
          _unit="byte")
+    return out
+
+
+def shard_route(ids: torch.Tensor, P: int, K: int, world: int):
+    """Row-sharded KShift lookup routing (lthm_shard_route; C3 item table): the K rows of every
+    id deduplicated per 2,048 (row, shift) pairs, owner-major (row r on rank r % world).
+    Returns send_rows [n K] (the first owner_base[world] used), send_counts [world] and
+    owner_base [world + 1] (device int64) and inv [n, K]: each pair's position in the
+    owner-major value buffer the exchange returns."""
+    require_gpu(ids)
+    flat = ids.reshape(-1).contiguous()
+    n = flat.numel()
+    _check(flat.dtype == torch.int64 and 0 < K <= 64 and P > 0 and world > 0, "shard_route: int64 ids, 0 < K <= 64")
+    dev = ids.device
+    npairs = n * K
+    send = torch.empty(max(npairs, 1), dtype=torch.int64, device=dev)
+    cnt = torch.empty(world, dtype=torch.int64, device=dev)
+    base = torch.empty(world + 1, dtype=torch.int64, device=dev)
+    inv = torch.empty(max(npairs, 1), dtype=torch.int64, device=dev)
+    wsb = int(load().lthm_shard_route_ws_bytes(npairs, world))
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)  # stream-ordered by the allocator (side streams)
+    call("lthm_shard_route", ptr(flat), n, K, P, world, ptr(send), ptr(cnt), ptr(base), ptr(inv), ptr(ws), wsb,
+         stream(), _key="shard_route", _work=float(npairs) * (8 + 16 + 8 + 8), _unit="byte")
+    return send, cnt, base, inv[:npairs].view(n, K)
+
+
+def shard_gather(shard: torch.Tensor, rows: torch.Tensor, world: int, count: torch.Tensor = None):
+    """out[i] = shard[rows[i] // world] (lthm_shard_gather), for i < count[0] when ``count`` (a device
+    int64 scalar view) is given, else for every row."""
+    require_gpu(shard, rows, count)
+    _check(shard.dim() == 2 and (shard.shape[1] * shard.element_size()) % 16 == 0,
+           "shard_gather: [n, D] shard with 16-byte-multiple rows")
+    cap = rows.numel()
+    out = torch.empty((cap, shard.shape[1]), dtype=shard.dtype, device=shard.device)
+    rb = shard.shape[1] * shard.element_size()
+    call("lthm_shard_gather", ptr(shard), shard.shape[0], rb, ptr(rows), ptr(count), cap, world, ptr(out), stream(),
+         _key="shard_gather", _work=float(cap) * (8 + 2 * rb), _unit="byte")
     return out
 
 

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
+from ....distributed import world_size
 from ....commons.functional import cap_gradients
 from ....commons.layers import (KShiftEmbedding, MLP, RowShardedKShiftEmbedding, TableBatchedKShiftEmbedding,
                                 TableShardedKShiftEmbedding)
@@ -83,13 +84,14 @@ class Encoder(nn.Module):
     def prefetch(self, batch: Dict[str, torch.Tensor], ready: Optional["torch.cuda.Event"] = None) -> None:
         """Pipelined item lookup for a later ``forward(batch)`` (the same
         ``batch["product_ids"]`` tensor, unmodified): the item table is frozen
-        (product_tower.py:47), so the whole lookup -- for the row-sharded table
-        (C3) the id dedup, the count exchange the host reads and both all_to_alls --
-        can run ahead of the step that consumes it, on a side stream of the device.
-        ``ready`` marks when the ids are valid (default: everything issued so far
-        on the current stream).  Call it where every rank issues it at the same
-        point and no backward is in flight (e.g. after the optimizer step), so the
-        collectives keep one order on all ranks."""
+        (product_tower.py:47), so the whole lookup -- for the row-sharded table (C3) the
+        routing, the count exchange the host reads and both all_to_alls (on a communicator
+        of their own, distributed.row_exchange_group) -- runs on a side stream of the device.
+        ``ready`` marks when the ids are valid (default: everything issued so far on the
+        current stream).  Issue it early, e.g. right after the current step's forward with
+        ``ready`` recorded when the next batch landed: the host then waits only for the side
+        stream's routing and count exchange while the current step's backward is queued.
+        Every rank must issue it at the same program point (collective order)."""
         raw = batch["product_ids"]
         K.require_gpu(raw)
         side = _side_stream(raw.device)
@@ -106,14 +108,20 @@ class Encoder(nn.Module):
 
     def _item_lookup(self, raw: torch.Tensor):
         p = getattr(self, "_prefetched", None)
-        if p is not None and p[0] is raw and p[1] == raw._version:
+        if p is not None:
             self._prefetched = None
-            _, _, ids, embs, done = p
-            cur = torch.cuda.current_stream(raw.device)
-            cur.wait_event(done)
-            ids.record_stream(cur)
-            embs.record_stream(cur)
-            return ids, embs
+            if p[0] is raw and p[1] == raw._version:
+                _, _, ids, embs, done = p
+                cur = torch.cuda.current_stream(raw.device)
+                cur.wait_event(done)
+                ids.record_stream(cur)
+                embs.record_stream(cur)
+                return ids, embs
+            if isinstance(self.product_emb_module, RowShardedKShiftEmbedding) and world_size() > 1:
+                # the inline lookup's collectives would run on this rank alone if another rank's
+                # prefetch hit: refuse instead of hanging the group
+                raise RuntimeError("a prefetched item lookup does not match this forward's ids; with a "
+                                   "row-sharded item table every rank must consume its prefetch")
         ids = K.flip_tokens(raw.contiguous())
         with torch.no_grad():
             embs = self.product_emb_module(ids)

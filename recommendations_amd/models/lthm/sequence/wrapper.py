@@ -220,7 +220,8 @@ class LTHMModelWrapper(BaseModelWrapper):
 
     def prefetch(self, batch: Dict[str, torch.Tensor], ready=None) -> None:
         """Run the frozen item-table lookup of a later ``forward(batch)`` now, on a side
-        stream (``Encoder.prefetch``; build-defined, the reference has no pipelining)."""
+        stream (``Encoder.prefetch``; build-defined, the reference has no pipelining).
+        ``ready``: an event recorded when ``batch``'s ids became valid."""
         self._model.prefetch(self.format_inputs(batch), ready)
 
     def draw_offsets(self, n_mb: int) -> np.ndarray:

@@ -232,24 +232,45 @@ def test_all_gather_rows_rank_order():
         assert torch.equal(out, torch.cat([torch.arange(6).view(3, 2), torch.arange(6).view(3, 2) + 100]))
 
 
+def _oracle_shard_kernels():
+    """The two routing kernels of the row-sharded lookup (lthm_shard_route / lthm_shard_gather)
+    replaced by their CPU restatements (oracle.ref.shard_route, an index_select)."""
+    import recommendations_amd.kernels as K_
+    from oracle.ref import shard_route
+
+    def route(ids, P, K, world):
+        send, cnt, base, inv = shard_route(ids.numpy(), P, K, world)
+        return (torch.from_numpy(send), torch.from_numpy(cnt), torch.from_numpy(base),
+                torch.from_numpy(inv).view(-1, K))
+
+    def gather(shard, rows, world, count=None):
+        n = rows.numel() if count is None else int(count.reshape(-1)[0])
+        return shard.index_select(0, torch.div(rows[:n], world, rounding_mode="floor"))
+
+    K_.shard_route, K_.shard_gather = route, gather
+
+
 def _sharded_lookup(rank, world):
-    """Row-sharded table (r on rank r % world): every rank exchanges its own
-    deduplicated KShift rows and gets exactly the full table's rows back."""
-    from recommendations_amd.distributed import exchange_rows
-    from oracle.ref import kshift_rows, kshift_fwd_c
+    """Row-sharded table (r on rank r % world): every rank exchanges its own routed KShift
+    rows (per-block dedup, owner-major) and gets exactly the full table's rows back."""
+    import recommendations_amd.kernels as K_
+    from recommendations_amd.distributed import exchange_routed
+    from oracle.ref import kshift_fwd_c, kshift_rows
+    _oracle_shard_kernels()
     P, D, Kk = 1000, 8, 16
     W = torch.from_numpy(np.random.default_rng(5).standard_normal((P, D)).astype(np.float32))
     shard = W[rank::world].contiguous()
     g = np.random.default_rng(40 + rank)
-    ids = g.integers(-2**63, 2**63 - 1, size=300 + 50 * rank, dtype=np.int64)
-    rows = torch.from_numpy(kshift_rows(ids, P, Kk))
-    uniq, inv = torch.unique(rows.view(-1), return_inverse=True)
-    vals = exchange_rows(uniq, shard)
-    exact = torch.equal(vals, W.index_select(0, uniq))
+    ids = torch.from_numpy(g.integers(-2**63, 2**63 - 1, size=300 + 50 * rank, dtype=np.int64))
+    send, cnt, base, inv = K_.shard_route(ids, P, Kk, world)
+    vals = exchange_routed(send, cnt, base, shard)
+    exact = torch.equal(vals, W.index_select(0, send[:int(base[-1])]))
+    rows = torch.from_numpy(kshift_rows(ids.numpy(), P, Kk))
+    routed = torch.equal(send[inv], rows)
     # in-order pool of the exchanged rows == the unsharded gather (oracle)
-    pooled = vals[inv.view(-1, Kk)].sum(dim=1)
-    ref = torch.from_numpy(kshift_fwd_c(ids, W.numpy(), Kk, 2))
-    return exact, float((pooled - ref).abs().max())
+    pooled = vals[inv].sum(dim=1)
+    ref = torch.from_numpy(kshift_fwd_c(ids.numpy(), W.numpy(), Kk, 2))
+    return exact and routed, float((pooled - ref).abs().max())
 
 
 def test_row_sharded_exchange():
@@ -317,13 +338,13 @@ def test_table_sharded_routing_world2():
 
 
 def _row_sharded_module(rank, world):
-    """RowShardedKShiftEmbedding (C3 item table) itself at world 2, its two kernels
-    replaced by the oracle: bit-identical to the unsharded gather of the same ids."""
+    """RowShardedKShiftEmbedding (C3 item table) itself at world 2, its routing, gather and
+    pool kernels replaced by the oracle: bit-identical to the unsharded gather of the same ids."""
     import recommendations_amd.kernels as K_
     import recommendations_amd.commons.layers as L
-    from oracle.ref import kshift_fwd_c, kshift_rows
+    from oracle.ref import kshift_fwd_c
     P, D, Kk = 1000, 8, 16
-    K_.kshift_rows = lambda ids, P_, K2: torch.from_numpy(kshift_rows(ids.numpy(), P_, K2)).view(ids.shape + (K2,))
+    _oracle_shard_kernels()
 
     def pool(rows, vals, mode, out_dtype=torch.float32):
         acc = torch.zeros(rows.shape[0], vals.shape[1], dtype=torch.float32)

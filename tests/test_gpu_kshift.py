@@ -130,3 +130,33 @@ def test_qr_embedding_vs_oracle(dev, normalize):
     for got, want in ((m.emb_q.weight.grad, wq.grad), (m.emb_r.weight.grad, wr.grad)):
         np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-5,
                                    atol=1e-5 * float(want.abs().max()))
+
+
+@pytest.mark.parametrize("world,P", [(1, 100_000), (3, 1_000_003), (8, 100_000_000)])
+def test_shard_route_vs_oracle(dev, world, P):
+    """lthm_shard_route (the C3 row-sharded lookup's routing: per-2,048-pair LDS bitonic dedup,
+    owner-major layout, device counts) against its CPU restatement oracle.ref.shard_route:
+    identical per-owner counts and request multisets, and every (id, shift) pair's position
+    pointing at its own KShift row (commons/layers.py:174-185) -- exact.  lthm_shard_gather
+    then returns exactly the table rows, bounded by the device-side total."""
+    import numpy as np
+    from recommendations_amd import kernels as K
+    from oracle.ref import kshift_rows, shard_route
+    Kk = 16
+    g = np.random.default_rng(world)
+    ids = np.concatenate([g.integers(-2 ** 63, 2 ** 63 - 1, size=4000, dtype=np.int64),
+                          g.integers(0, 50, size=1000, dtype=np.int64)])  # repeats: in-block duplicates
+    send, cnt, base, inv = K.shard_route(torch.from_numpy(ids).to(dev), P, Kk, world)
+    o_send, o_cnt, o_base, o_inv = shard_route(ids, P, Kk, world)
+    assert np.array_equal(cnt.cpu().numpy(), o_cnt) and np.array_equal(base.cpu().numpy(), o_base)
+    send_h = send.cpu().numpy()
+    assert np.array_equal(send_h[inv.cpu().numpy()], kshift_rows(ids, P, Kk))
+    for o in range(world):
+        a, b = int(o_base[o]), int(o_base[o + 1])
+        assert np.array_equal(np.sort(send_h[a:b]), np.sort(o_send[a:b]))
+        assert (send_h[a:b] % world == o).all()
+    if world == 1:
+        W = torch.randn((P, 32), device=dev).to(torch.bfloat16)
+        vals = K.shard_gather(W, send, 1, count=base[1:2])
+        n = int(base[1])
+        assert torch.equal(vals[:n], W.index_select(0, send[:n]))
