@@ -61,7 +61,20 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
     if (valid) {
       const TW* colp = W + (size_t)gl * NE;
       int c = 0;
-      // issue 4 row loads ahead, then add in order c = 0..K-1 (bit-exact order)
+      // issue 8 row loads ahead, then add in order c = 0..K-1 (bit-exact order): with the
+      // table far past the Infinity Cache every load is an HBM miss, so the depth of
+      // independent loads per lane sets the achieved bandwidth
+      for (; c + 8 <= K; c += 8) {
+        float v[8][NE];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) load_vec<TW, VB>(colp + rows_lds[wave][gi * K + c + u] * D, v[u]);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] = (c == 0) ? v[0][e] : acc[e] + v[0][e];
+#pragma unroll
+        for (int u = 1; u < 8; ++u)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) acc[e] += v[u][e];
+      }
       for (; c + 4 <= K; c += 4) {
         float v0[NE], v1[NE], v2[NE], v3[NE];
         const int64_t r0 = rows_lds[wave][gi * K + c], r1 = rows_lds[wave][gi * K + c + 1];
