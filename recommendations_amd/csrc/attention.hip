@@ -13,6 +13,8 @@
 // no T x T buffer is needed at all.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace lthm {
 
 struct AttnArgs {
@@ -731,6 +733,441 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
   }
 }
 // ===========================================================================
+// Backward on 32x32x16 MFMA (E = 64, T' <= 256, no general mask): one workgroup per
+// (b, h) holding K, V, Q and dO images in LDS for the whole kernel, so the rows units (dQ)
+// and the columns units (dK, dV) run side by side over the 4 waves (longest first) with no
+// barrier and no global read between them.  The score tiles are oriented so that every
+// product after the first takes its operand straight from the accumulator
+// (cdna_hip_programming.md §3): no LDS scratch round trip, no bf16 hi / lo split of P and
+// dS, and the gradients leave as transposed accumulators (8-byte runs of a token's row).
+//  * rows unit, query tile i: S^T[k][q] = K . Q^T and dP^T = V . dO^T, dS^T elementwise
+//    (the query is the lane), dQ^T += K^T . dS^T with K read transposed; the bias gradient
+//    by rotating each register across the lane half by its key offset (ds_bpermute), which
+//    puts one diagonal per lane: one LDS atomic per lane and tile;
+//  * columns unit, key tile j: S = Q . K^T and dP = dO . V^T, P and dS elementwise (the key
+//    is the lane), dV^T += dO^T . P and dK^T += Q^T . dS with dO / Q read transposed.
+// Image rows are 128 B: chunk ch of row r at slot ch ^ s(r >> 1), s(u) = ((u & 1) << 2) |
+// ((u >> 1) & 3): the row-fragment reads (16 lanes, 16 rows, one chunk) and the
+// transposed reads (4 rows x 4 chunks per 32 lanes) are both conflict-free.
+constexpr int E_BWD32 = 64;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+// image of rows [0, Tk) (row r at src + r * ts; rows >= T zero) by LDS-DMA: 1-KiB pieces of
+// 8 rows, the lane loading the chunk that the swizzle puts in its lane-linear slot
+__device__ __forceinline__ void stage_img32(unsigned char* img, const bf16_t* __restrict__ src, int64_t ts, int T,
+                                            int Tk, int wave, int lane, int nw) {
+  for (int d = wave; d < Tk / 8; d += nw) {
+    const int row = 8 * d + (lane >> 3), slot = lane & 7;
+    const int u = row >> 1;
+    const int ch = slot ^ (((u & 1) << 2) | ((u >> 1) & 3));
+    const void* p = row < T ? (const void*)(src + (int64_t)row * ts + ch * 8) : (const void*)attn_zero16;
+    glds16(p, img + d * 1024);
+  }
+}
+
+__device__ __forceinline__ uint32_t pk_bf16_rne(float lo, float hi) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+
+// registers 8 s .. 8 s + 7 of a 32 x 32 accumulator as the bf16 A operand of k-step s
+__device__ __forceinline__ bf16x8v acc_frag32(const f32x16& x, int s) {
+  const int o = 8 * s;
+  const u32x4 h = {pk_bf16_rne(x[o], x[o + 1]), pk_bf16_rne(x[o + 2], x[o + 3]), pk_bf16_rne(x[o + 4], x[o + 5]),
+                   pk_bf16_rne(x[o + 6], x[o + 7])};
+  return __builtin_bit_cast(bf16x8v, h);
+}
+
+// dot of two bf16x8 fragments in fp32
+__device__ __forceinline__ float bf8_dot(const bf16x8v& x, const bf16x8v& y) {
+  const u32x4 u = __builtin_bit_cast(u32x4, x), w = __builtin_bit_cast(u32x4, y);
+  float d = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    d += __uint_as_float(u[i] << 16) * __uint_as_float(w[i] << 16) +
+         __uint_as_float(u[i] & 0xffff0000u) * __uint_as_float(w[i] & 0xffff0000u);
+  return d;
+}
+
+// the relative-position bias in log2 units, two shifted copies each way, so that the four
+// entries x .. x + 3 (columns units) or x .. x - 3 (rows units) of any x are two aligned
+// 8-byte reads: ext[e] = table[e - BPAD] * log2 e inside [0, 2T], 0 outside (every x a
+// tile forms lies in [-30, 2T + 30]).  ne = 34 (mod 64) puts the two copies' 32-lane read
+// groups on disjoint banks.
+constexpr int BPAD = 32;
+__host__ __device__ __forceinline__ int bias_ne(int T) { return ((2 * T + 2 * BPAD + 11 + 63) & ~63) + 34; }
+
+__device__ __forceinline__ int a32_swz(int row) {
+  const int u = row >> 1;
+  return ((u & 1) << 2) | ((u >> 1) & 3);
+}
+
+// lane-constant parts of the fragment offsets: tiles start at multiples of 16 image rows, so
+// the swizzle of (tile row + r) depends on r alone.  row[s]: k-step s of row r0 + (lane & 31);
+// tr[nd][hi]: the transposed read of columns 32 nd .. 32 nd + 31 (see a32 layout above)
+struct Frag32Off {
+  int row[4];
+  int tr[2][2];
+};
+__device__ __forceinline__ Frag32Off frag32_off(int lane) {
+  const int hh = lane >> 5, r32 = lane & 31;
+  Frag32Off o;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) o.row[s] = r32 * 128 + (((2 * s + hh) ^ a32_swz(r32)) << 4);
+  const int colhalf = (lane >> 4) & 1, li = lane & 15, q = li >> 2, pp = li & 3;
+#pragma unroll
+  for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int row = 4 * hh + 8 * hi + q, ch = 4 * nd + 2 * colhalf + (pp >> 1);
+      o.tr[nd][hi] = row * 128 + ((ch ^ a32_swz(row)) << 4) + 8 * (pp & 1);
+    }
+  return o;
+}
+__device__ __forceinline__ bf16x8v frag_at(const unsigned char* p) {
+  return __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(p));
+}
+__device__ __forceinline__ bf16x8v tr_at(const unsigned char* lo, const unsigned char* hi) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((address_space(3))) unsigned char lds_u8_t;
+  const s16x4 l = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_u8_t*)lo);
+  const s16x4 h = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_u8_t*)hi);
+  const s16x8 v = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// 32 x 32 transposed-gradient accumulator (row e = 32 nd + 8 g + 4 hh + j in the registers,
+// column = the token r0 + (lane & 31)) stored as 8-byte runs of the token's row
+__device__ __forceinline__ void store_accT32(const f32x16& x, float scale, bf16_t* __restrict__ base, int64_t ts,
+                                             int r0, int nd, int T, int lane) {
+  const int r = r0 + (lane & 31), hh = lane >> 5;
+  if (r >= T) return;
+  bf16_t* row = base + (int64_t)r * ts + 32 * nd + 4 * hh;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const uint2 w = {pk_bf16_rne(x[4 * g] * scale, x[4 * g + 1] * scale),
+                     pk_bf16_rne(x[4 * g + 2] * scale, x[4 * g + 3] * scale)};
+    *reinterpret_cast<uint2*>(row + 8 * g) = w;
+  }
+}
+
+// the wave's units over the NW waves, longest first: unit u < nt is the rows unit of query
+// tile u, unit nt + j the columns unit of key tile j (cost: tiles visited + 1)
+template <int NW>
+__device__ __forceinline__ uint32_t lpt_units(int nt, bool causal, int wave) {
+  int load[NW] = {};
+  uint32_t mine = 0;
+  for (int c = nt; c >= 1; --c)  // descending cost; causal: rows tile c - 1 and columns tile nt - c
+    for (int side = 0; side < 2; ++side) {
+      const int u = side == 0 ? c - 1 : nt + (nt - c);
+      const int cost = (causal ? c : nt) + 1;
+      int w = 0;
+#pragma unroll
+      for (int j = 1; j < NW; ++j)
+        if (load[j] < load[w]) w = j;
+      load[w] += cost;
+      if (w == wave) mine |= 1u << u;
+    }
+  return mine;
+}
+
+// LDS: the bias copies, lse, delta and the bias gradient first, then the K, Q, dO and V
+// images (rows 0 .. Timg - 1, zero from T) and a zero slack up to V's last tile.  Tile reads
+// past an image's end (the last, ragged tile) land in the next image or the slack, finite
+// data: the edge tiles select those elements' P and dS to zero after the products, so no
+// such read reaches a gradient.
+struct Bwd32Smem {
+  const unsigned char *IK, *IQ, *IO, *IV;
+  const float *bfw, *brv, *lse, *dlt;
+  float* dbias;
+  int ne;
+};
+
+// rows unit: dQ of query tile i (and the bias gradient of its tiles)
+template <bool EDGE>
+__device__ __forceinline__ void rows_math(f32x16& st, const f32x16& pt, const float* bp, float lq, float dl, float c2,
+                                          int kb0, int kmax) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float2 lo = *reinterpret_cast<const float2*>(bp + 8 * g);
+    const float2 hi = *reinterpret_cast<const float2*>(bp + 8 * g + 2);
+    const float bv[4] = {lo.x - lq, lo.y - lq, hi.x - lq, hi.y - lq};
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int v = 4 * g + jj;
+      const float p = __builtin_amdgcn_exp2f(fmaf(st[v], c2, bv[jj]));
+      const float ds = p * (pt[v] - dl);
+      st[v] = (!EDGE || kb0 + 8 * g + jj < kmax) ? ds : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
+                                           int i, int lane) {
+  constexpr float L2E = 1.4426950408889634f;
+  const int T = a.T, nt = (T + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
+  const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
+  const bool ragged = (T & 31) != 0;
+  const int q0 = 32 * i, q = q0 + r32;
+  const float lq = m.lse[q], dl = m.dlt[q];
+  const int kmax = q < T ? (a.causal ? q + 1 : T) : 0;  // keys k < kmax are live for this query
+  f32x16 dq[2];
+#pragma unroll
+  for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) dq[nd][v] = 0.f;
+  float carry = 0.f;
+  const bool has_tab = a.dtable_part != nullptr;
+  const int jend = a.causal ? i + 1 : nt;
+  // bias of (q, k0 + 4 hh - jj) for tile 0: descending copy, 32 entries on per tile
+  const int z0 = m.ne - 1 - (q - 4 * hh + T + BPAD);
+  const float* bp = m.brv + (z0 & 1) * m.ne + (z0 & ~1);
+  float wrap[16];  // lane constants of the diagonal rotation: 1 where register v wraps
+#pragma unroll
+  for (int v = 0; v < 16; ++v) wrap[v] = r32 + 4 * hh + 8 * (v >> 2) + (v & 3) >= 32 ? 1.f : 0.f;
+  for (int j = 0; j < jend; ++j, bp += 32) {
+    const int k0 = 32 * j;
+    f32x16 st, pt;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      st[v] = 0.f;
+      pt[v] = 0.f;
+    }
+    int qo = q0 * 128;  // laundered: the Q / dO fragments are re-read per tile, not kept live
+    asm volatile("" : "+v"(qo));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      st = MFMA32(frag_at(m.IK + k0 * 128 + fo.row[s]), frag_at(m.IQ + qo + fo.row[s]), st);
+      pt = MFMA32(frag_at(m.IV + k0 * 128 + fo.row[s]), frag_at(m.IO + qo + fo.row[s]), pt);
+    }
+    // S^T[k][q]: the key k = k0 + 8 g + 4 hh + jj in register 4 g + jj, the query q in the lane
+    if ((a.causal && j == i) || (ragged && (i == nt - 1 || j == nt - 1)))
+      rows_math<true>(st, pt, bp, lq, dl, c2, k0 + 4 * hh, kmax);
+    else
+      rows_math<false>(st, pt, bp, lq, dl, c2, k0 + 4 * hh, kmax);
+    if (has_tab) {
+      // diagonal sums of the tile: register v rotated across the lane half by its key
+      // offset puts diagonal q - k = r32 (r32 - 32 when wrapped) in lane r32
+      float tot = 0.f, neg = 0.f;
+      int rl = r32 + 4 * hh;  // laundered: the 16 rotation addresses are recomputed, not kept live
+      asm volatile("" : "+v"(rl));
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int kv = rl + 8 * (v >> 2) + (v & 3);
+        const float x =
+            __int_as_float(__builtin_amdgcn_ds_bpermute(((kv & 31) | (hh << 5)) << 2, __float_as_int(st[v])));
+        tot += x;
+        neg = fmaf(x, wrap[v], neg);
+      }
+      tot += __shfl_xor(tot, 32, 64);
+      neg += __shfl_xor(neg, 32, 64);
+      // diagonal q - k = 32 (i - j) + r32 is complete: this tile's pos, the previous tile's neg
+      const int d = 32 * (i - j) + r32 + T;
+      if (hh == 0 && d <= 2 * T) atomicAdd(&m.dbias[d], tot - neg + carry);
+      carry = neg;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8v gf = acc_frag32(st, s);
+      const unsigned char* kt = m.IK + (k0 + 16 * s) * 128;
+#pragma unroll
+      for (int nd = 0; nd < 2; ++nd) dq[nd] = MFMA32(tr_at(kt + fo.tr[nd][0], kt + fo.tr[nd][1]), gf, dq[nd]);
+    }
+  }
+  if (has_tab) {
+    const int d = 32 * (i - jend) + r32 + T;
+    if (hh == 0 && d >= 0 && d <= 2 * T) atomicAdd(&m.dbias[d], carry);
+  }
+  bf16_t* dqg = a.dq + b * a.q_bs + h * a.q_hs;
+#pragma unroll
+  for (int nd = 0; nd < 2; ++nd) store_accT32(dq[nd], rs, dqg, a.q_ts, q0, nd, T, lane);
+}
+
+// columns unit: dK, dV of key tile j
+template <bool EDGE>
+__device__ __forceinline__ void cols_math(f32x16& sx, f32x16& px, const float* bp, const float* lse, const float* dlt,
+                                          float c2, int qb0, int qlo, int span) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 l4 = *reinterpret_cast<const float4*>(lse + 8 * g);
+    const float4 d4 = *reinterpret_cast<const float4*>(dlt + 8 * g);
+    const float2 lo = *reinterpret_cast<const float2*>(bp + 8 * g);
+    const float2 hi = *reinterpret_cast<const float2*>(bp + 8 * g + 2);
+    const float bv[4] = {lo.x - l4.x, lo.y - l4.y, hi.x - l4.z, hi.y - l4.w};
+    const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int v = 4 * g + jj;
+      const float p = __builtin_amdgcn_exp2f(fmaf(sx[v], c2, bv[jj]));
+      const float ds = p * (px[v] - dv4[jj]);
+      const bool live = !EDGE || (unsigned)(qb0 + 8 * g + jj - qlo) < (unsigned)span;
+      px[v] = live ? ds : 0.f;
+      sx[v] = live ? p : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
+                                           int j, int lane) {
+  constexpr float L2E = 1.4426950408889634f;
+  const int T = a.T, nt = (T + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
+  const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
+  const bool ragged = (T & 31) != 0;
+  const int k0 = 32 * j, k = k0 + r32;
+  // live queries of this key: [qlo, T)
+  const int qlo = k < T ? (a.causal ? k : 0) : T, span = T - qlo;
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      dk[nd][v] = 0.f;
+      dv[nd][v] = 0.f;
+    }
+  const int i0 = a.causal ? j : 0;
+  // bias of (q0 + 4 hh + jj, k): ascending copy, 32 entries on per tile
+  const int e0 = 32 * i0 + 4 * hh - k + T + BPAD;
+  const float* bp = m.bfw + (e0 & 1) * m.ne + (e0 & ~1);
+  for (int i = i0; i < nt; ++i, bp += 32) {
+    const int q0 = 32 * i;
+    f32x16 sx, px;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      sx[v] = 0.f;
+      px[v] = 0.f;
+    }
+    int ko = k0 * 128;  // laundered: the K / V fragments are re-read per tile, not kept live
+    asm volatile("" : "+v"(ko));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sx = MFMA32(frag_at(m.IQ + q0 * 128 + fo.row[s]), frag_at(m.IK + ko + fo.row[s]), sx);
+      px = MFMA32(frag_at(m.IO + q0 * 128 + fo.row[s]), frag_at(m.IV + ko + fo.row[s]), px);
+    }
+    // S[q][k]: the query q = q0 + 8 g + 4 hh + jj in register 4 g + jj, the key k in the lane
+    const int qb0 = q0 + 4 * hh;
+    if ((a.causal && j == i) || (ragged && (i == nt - 1 || j == nt - 1)))
+      cols_math<true>(sx, px, bp, m.lse + qb0, m.dlt + qb0, c2, qb0, qlo, span);
+    else
+      cols_math<false>(sx, px, bp, m.lse + qb0, m.dlt + qb0, c2, qb0, qlo, span);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8v pf = acc_frag32(sx, s), gf = acc_frag32(px, s);
+      const unsigned char* ot = m.IO + (q0 + 16 * s) * 128;
+      const unsigned char* qt = m.IQ + (q0 + 16 * s) * 128;
+#pragma unroll
+      for (int nd = 0; nd < 2; ++nd) {
+        dv[nd] = MFMA32(tr_at(ot + fo.tr[nd][0], ot + fo.tr[nd][1]), pf, dv[nd]);
+        dk[nd] = MFMA32(tr_at(qt + fo.tr[nd][0], qt + fo.tr[nd][1]), gf, dk[nd]);
+      }
+    }
+  }
+  bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
+  bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
+#pragma unroll
+  for (int nd = 0; nd < 2; ++nd) {
+    store_accT32(dk[nd], rs, dkg, a.k_ts, k0, nd, T, lane);
+    store_accT32(dv[nd], 1.f, dvg, a.v_ts, k0, nd, T, lane);
+  }
+}
+
+__host__ __device__ __forceinline__ int bwd32_timg(int T) { return (T + 7) & ~7; }
+__host__ __device__ __forceinline__ int bwd32_fbytes(int T) {  // float region, 16-byte multiple
+  return (4 * bias_ne(T) + 2 * ((T + 31) & ~31) + ((2 * T + 1 + 3) & ~3)) * 4;
+}
+
+__host__ __device__ __forceinline__ int bwd32_slack(int T) {  // rows past V for the last tile
+  const int d = ((T + 31) & ~31) - bwd32_timg(T);
+  return d > 0 ? d : 0;
+}
+
+constexpr int BWD32_NW = 4, BWD32_WPE = 2;  // waves per (b, h); waves per SIMD the registers allow
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_WPE, BWD32_WPE))) void attn_bwd32_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr float L2E = 1.4426950408889634f;
+  const int T = a.T, Tk = (T + 31) & ~31, nt = Tk / 32, ne = bias_ne(T), Ti = bwd32_timg(T);
+  float* bfw = reinterpret_cast<float*>(smem);  // [2][ne] ascending copies
+  float* brv = bfw + 2 * ne;                     // [2][ne] descending copies
+  float* lse_s = brv + 2 * ne;                   // [Tk] lse * log2 e (0 past T)
+  float* dlt_s = lse_s + Tk;                     // [Tk] delta = dO . O (0 past T)
+  float* dbias = dlt_s + Tk;                     // [2T + 1]
+  unsigned char* IK = smem + bwd32_fbytes(T);
+  unsigned char* IQ = IK + Ti * 128;
+  unsigned char* IO = IQ + Ti * 128;
+  unsigned char* IV = IO + Ti * 128;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+  const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+  const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+  const bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+  const bf16_t* dog = a.dout + b * a.o_bs + h * a.o_hs;
+  const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  stage_img32(IK, kg, a.k_ts, T, Ti, wave, lane, NW);
+  stage_img32(IQ, qg, a.q_ts, T, Ti, wave, lane, NW);
+  stage_img32(IO, dog, a.o_ts, T, Ti, wave, lane, NW);
+  stage_img32(IV, vg, a.v_ts, T, Ti, wave, lane, NW);
+  {  // delta[q] = dO[q] . O[q]: four threads per row, every load in flight before the first use
+    constexpr int RPI = 16 * NW, NIT = (256 + RPI - 1) / RPI;  // rows per iteration, iterations for Tk <= 256
+    u32x4 du[NIT][2], ou[NIT][2];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid >> 2) + RPI * it, c = (tid & 3) * 16;
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        du[it][x] = ou[it][x] = (u32x4){0u, 0u, 0u, 0u};
+        if (r < T) {
+          du[it][x] = *reinterpret_cast<const u32x4*>(dog + (int64_t)r * a.o_ts + c + 8 * x);
+          ou[it][x] = *reinterpret_cast<const u32x4*>(og + (int64_t)r * a.o_ts + c + 8 * x);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid >> 2) + RPI * it;
+      float d = bf8_dot(__builtin_bit_cast(bf16x8v, du[it][0]), __builtin_bit_cast(bf16x8v, ou[it][0])) +
+                bf8_dot(__builtin_bit_cast(bf16x8v, du[it][1]), __builtin_bit_cast(bf16x8v, ou[it][1]));
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      if ((tid & 3) == 0 && r < Tk) {
+        dlt_s[r] = r < T ? d : 0.f;
+        lse_s[r] = r < T ? lse_g[r] * L2E : 0.f;
+      }
+    }
+  }
+  for (int c = 0; c < 2; ++c)
+    for (int y = tid; y < ne; y += 64 * NW) {
+      const int xf = y + c - BPAD, xr = ne - 1 - (y + c) - BPAD;
+      bfw[c * ne + y] = (a.table && xf >= 0 && xf <= 2 * T) ? a.table[(int64_t)xf * a.H + h] * L2E : 0.f;
+      brv[c * ne + y] = (a.table && xr >= 0 && xr <= 2 * T) ? a.table[(int64_t)xr * a.H + h] * L2E : 0.f;
+    }
+  for (int i = tid; i <= 2 * T; i += 64 * NW) dbias[i] = 0.f;
+  for (int i = tid; i < bwd32_slack(T) * 32; i += 64 * NW) reinterpret_cast<float*>(IV + Ti * 128)[i] = 0.f;
+  wait_vm<0>();
+  __syncthreads();
+  const Bwd32Smem m{IK, IQ, IO, IV, bfw, brv, lse_s, dlt_s, dbias, ne};
+  const Frag32Off fo = frag32_off(lane);
+  const uint32_t mine = lpt_units<NW>(nt, a.causal, wave);
+  // longest first: the rows unit of tile c - 1 and the columns unit of tile nt - c cost alike
+  for (int c = nt; c >= 1; --c) {
+    if (mine & (1u << (c - 1))) bwd32_rows(a, m, fo, b, h, c - 1, lane);
+    if (mine & (1u << (2 * nt - c))) bwd32_cols(a, m, fo, b, h, nt - c, lane);
+  }
+  if (a.dtable_part) {
+    __syncthreads();
+    for (int i = tid; i <= 2 * T; i += 64 * NW) a.dtable_part[((int64_t)b * (2 * T + 1) + i) * a.H + h] = dbias[i];
+  }
+}
+
+static size_t bwd32_lds(int T) {
+  return (size_t)bwd32_fbytes(T) + (size_t)(4 * bwd32_timg(T) + bwd32_slack(T)) * 128;
+}
+
+// ===========================================================================
 // Long sequences (T' > 256, e.g. the C5 config's T' = 513): the head no longer
 // fits LDS whole.  A workgroup owns 64 rows (one 16-row tile per wave) and
 // streams the other side through LDS in windows of AW_W rows by LDS-DMA (K/V
@@ -1118,6 +1555,12 @@ static size_t bwd_mfma_lds(int T, int E) {
 
 template <int E>
 static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
+  static const bool old_bwd = getenv("LTHM_ATTN_BWD_OLD") && atoi(getenv("LTHM_ATTN_BWD_OLD"));  // A/B switch
+  if (E == 64 && bwd && !old_bwd) {
+    hipLaunchKernelGGL(attn_bwd32_k<BWD32_NW>, dim3(B * a.H), dim3(64 * BWD32_NW), bwd32_lds(a.T), s, a);
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t sh = bwd ? bwd_mfma_lds(a.T, E) : fwd_mfma_lds(a.T, E);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   // backward: one block per (b, h) for both passes (C2: 0.98 -> 0.93 ms against one block per pass)
