@@ -30,11 +30,12 @@ FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md 
 
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
 PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
-    "cl_bwd_k": ["cl_bwd_k<", "cl_shift_k"],
-    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_stats_k"],
-    "attn_bwd_k": ["attn_bwd_mfma_k<", "attn_bwd_rows_win_k<", "attn_bwd_cols_win_k<", "attn_delta_k<"],
+    "cl_bwd_k": ["cl_bwd_k<", "cl_bwd32_k<", "cl_shift_k"],
+    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_stats_k", "cl_rowstats_k", "cl_wscale_k"],
+    "attn_bwd_k": ["attn_bwd_mfma_k<", "attn_bwd32_k<", "attn_bwd_rows_win_k<", "attn_bwd_cols_win_k<",
+                   "attn_delta_k<"],
     "attn_fwd_k": ["attn_fwd_mfma_k<", "attn_fwd_win_k<"],
     "gemm_k<1,1>": ["gemm_k<true, true>", "gemm_ps_k<true, "],
     "gemm_k<1,0>": ["gemm_k<true, false>", "gemm_ps_k<false, "],
