@@ -171,10 +171,21 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 // swizzled row-major [rows, D] bf16 LDS image (16-byte chunks XOR row group) and
 // its ds_read_tr16_b64 fragment B[k = 8(lane>>4) + i][n = nb + (lane&15)]
 template <int D>
-__device__ __forceinline__ int ct_off(int row, int ch) {
+__device__ __forceinline__ int ct_swz(int row) {
   constexpr int NC = D / 8;
-  constexpr int RPL = (256 / (2 * D)) > 0 ? 256 / (2 * D) : 1;
-  return row * (2 * D) + ((ch ^ ((row / RPL) & (NC - 1))) << 4);
+  if constexpr (NC >= 16) {
+    // bit permutation r0 -> b1, r1 -> b2, r2 -> b0 (r3, r4 stay): a transposed read's 32-lane
+    // half (rows kb + {0..3, 8..11} or kb + {4..7, 12..15}, two adjacent chunks) then covers
+    // 16 distinct 16-byte slots (64 banks); plain r & (NC - 1) gave 8, a 2-way conflict
+    return (((row & 3) << 1) | ((row >> 2) & 1) | (row & 24)) & (NC - 1);
+  } else {
+    constexpr int RPL = (256 / (2 * D)) > 0 ? 256 / (2 * D) : 1;
+    return (row / RPL) & (NC - 1);
+  }
+}
+template <int D>
+__device__ __forceinline__ int ct_off(int row, int ch) {
+  return row * (2 * D) + ((ch ^ ct_swz<D>(row)) << 4);
 }
 
 template <int D>
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
     }
   };
   // DMA slab k0 / 32 into ring slot `slot`: piece p = 1 KiB = 512 / D rows; lane l lands at
-  // row p (512 / D) + l / NC, slot l % NC, so it loads chunk slot ^ (row & (NC - 1)) (ct_off)
+  // row p (512 / D) + l / NC, slot l % NC, so it loads chunk slot ^ ct_swz(row) (ct_off)
   constexpr int NC = D / 8;
   constexpr int DPW = DMA ? D / 128 : 1;  // DMAs per wave and slab (16 or 8 pieces over 8 waves)
   auto ring = [&](int slot) -> unsigned char* {
@@ -483,7 +494,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
     for (int q = 0; q < DPW; ++q) {
       const int pc = w + 8 * q;
       const int row = pc * (512 / D) + lane / NC;
-      const int ch = (lane % NC) ^ (row & (NC - 1));
+      const int ch = (lane % NC) ^ ct_swz<D>(row);
       const void* src = k0 + row < R ? (const void*)(tab + (int64_t)(k0 + row) * ldt + ch * 8) : (const void*)pt_zero16;
       glds16(src, img + pc * 1024);
     }
