@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 26 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 27 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -520,6 +520,9 @@ typedef struct lthm_contrastive_desc {
   void* stats_ws;         /* forward: device workspace of lthm_contrastive_ws_bytes(n_mb, n_max, heads_run)
                              bytes (rank histograms + per-block partial sums) */
   int64_t stats_ws_bytes;
+  int32_t rows_done;      /* backward: the forward already wrote dy (it was given y_raw / y_norm / dy at the fixed
+                             shift: the fused forward + ROWS pass) for a unit upstream gradient; the backward
+                             then runs the COLS side only and scales dy by *gscale */
 } lthm_contrastive_desc;
 
 /* bytes of lthm_contrastive_desc.stats_ws for one forward launch (-1: invalid sizes) */
@@ -527,7 +530,10 @@ int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads);
 
 /* Forward for one head (or heads_run consecutive heads) over all mini-batches.  stats [n_mb, nstat] f32 per head:
  * {mean CE, used rows, mean negatives, min negatives, mean rank, median rank,
- *  offset, hit@ks[0..nk)}; loss_scale multiplies the row weights (1 / n_mb). */
+ *  offset, hit@ks[0..nk)}; loss_scale multiplies the row weights (1 / n_mb).
+ * Training at the fixed shift (2 / tau <= 80, no logq) with y_raw / y_norm / dy given (heads 0 .. n_heads - 1,
+ * mb_size <= 4096 sequences): one pass per row block computes the forward AND the row side of the backward,
+ * writing dy for a unit upstream gradient; the backward is then called with rows_done = 1. */
 int lthm_contrastive_fwd(const lthm_contrastive_desc* desc, float* stats, int32_t nstat, const int32_t* ks,
                          int32_t nk, float loss_scale, void* stream);
 int lthm_contrastive_bwd(const lthm_contrastive_desc* desc, void* stream);

@@ -18,6 +18,8 @@
 // count #{c != r : logit[r, c] > logit[r, r]}.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace lthm {
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a0) {
     const int64_t o = (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
     if (a.dy && a.y_dtype == LTHM_BF16) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
     else if (a.dy) *reinterpret_cast<float4*>((float*)a.dy + o) = float4{0.f, 0.f, 0.f, 0.f};
-    else *reinterpret_cast<float4*>(a.d_out + o) = float4{0.f, 0.f, 0.f, 0.f};
+    else if (a.d_out) *reinterpret_cast<float4*>(a.d_out + o) = float4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -1435,6 +1437,282 @@ __global__ __launch_bounds__(64 * NW, 2) void cl_bwd32_k(ClArgs a0) {
   }
 }
 
+// ---------------------------------------------------------------- fused forward + ROWS
+// Training at the fixed shift: P[x][y] = p / Z_x with p = 2^(S c1 - log2 e / tau) needs no lse
+// before the pass over the columns, so ONE pass gives the forward's Z_x (lse), counts and
+// ranks AND U_x = sum_y p[x][y] in_y; at the end dOut_x = w_x (U_x / Z_x - in_x) goes
+// through F.normalize into dy (unit upstream gradient: the backward scales dy by it).  The
+// row weights w_x are known before the pass (cl_used_k: they depend on the pad mask only),
+// so the row side of the backward costs no S recompute: forward + backward execute
+// 8 n^2 De per head, the algorithmic count.
+
+// row weights w_r = used_r * loss_scale / U of every head and mini-batch from the pad mask:
+// row r is used when it is not a pad and some valid column lies outside its sequence (the
+// forward's "at least one finite negative", wrapper.py:193-201); U = used rows of the
+// mini-batch.  Also zeroes the dy rows the fused kernel never writes (t >= L).  Grid
+// (n_mb, heads), one block each; V[b] valid tokens per sequence in LDS (Bm <= CL_UMAXB).
+constexpr int CL_UMAXB = 4096;
+__global__ __launch_bounds__(256) void cl_used_k(ClArgs a0, float* __restrict__ w0, float loss_scale) {
+  const ClArgs a = head_args(a0, blockIdx.y);
+  float* wout = w0 + (int64_t)blockIdx.y * a0.head_stride;
+  const int mb = blockIdx.x;
+  const Geo g = geo(a, mb);
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)mb * a.n_max;
+  __shared__ int V[CL_UMAXB];
+  __shared__ double red[256];
+  int nv = 0;
+  for (int b = tid; b < g.Bm; b += 256) {
+    int v = 0;
+    for (int t = 0; t < g.L; ++t) v += pad_of(a, g, b * g.L + t) ? 0 : 1;
+    V[b] = v;
+    nv += v;
+  }
+  const int N = (int)block_dsum((double)nv, red);  // block_dsum syncs: V is complete
+  int u = 0;
+  for (int b = tid; b < g.Bm; b += 256) u += (N - V[b] > 0) ? V[b] : 0;
+  const int U = (int)block_dsum((double)u, red);
+  const float wr = U > 0 ? loss_scale / (float)U : 0.f;
+  for (int r = tid; r < a.n_max; r += 256) {
+    float wv = 0.f;
+    if (r < g.n) {
+      const int b = seq_of(g, r);
+      wv = (!pad_of(a, g, r) && N - V[b] > 0) ? wr : 0.f;
+    }
+    wout[base + r] = wv;
+  }
+  const int tl0 = max(g.L, 0), ntail = a.T + 1 - tl0;
+  const int per_seq = ntail * (DE / 4);
+  const int64_t cnt = (int64_t)g.Bm * per_seq;
+  for (int64_t i = tid; i < cnt; i += 256) {
+    const int b = (int)(i / per_seq), rem = (int)(i - (int64_t)b * per_seq);
+    const int t = tl0 + rem / (DE / 4), c4 = rem % (DE / 4);
+    const int64_t o = (((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
+    if (a.y_dtype == LTHM_BF16) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
+    else *reinterpret_cast<float4*>((float*)a.dy + o) = float4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// dy *= *gscale (the fused forward wrote dy for a unit upstream gradient); nothing to do at 1
+template <typename TY>
+__global__ __launch_bounds__(256) void cl_dyscale_k(TY* __restrict__ dy, int64_t n, const float* __restrict__ gscale) {
+  const float gs = *gscale;
+  if (gs == 1.f) return;
+  for (int64_t i = (blockIdx.x * (int64_t)256 + threadIdx.x) * 8; i < n; i += (int64_t)gridDim.x * 256 * 8) {
+    float v[8];
+    if (i + 8 <= n) {
+      if constexpr (sizeof(TY) == 2) {
+        load_vec<TY, 16>(dy + i, v);
+      } else {
+        load_vec<TY, 16>(dy + i, v);
+        load_vec<TY, 16>(dy + i + 4, v + 4);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= gs;
+      if constexpr (sizeof(TY) == 2) {
+        store_vec<TY, 8>(dy + i, v);
+      } else {
+        store_vec<TY, 4>(dy + i, v);
+        store_vec<TY, 4>(dy + i + 4, v + 4);
+      }
+    } else {
+      for (int64_t k = i; k < n; ++k) Elem<TY>::st(dy + k, Elem<TY>::ld(dy + k) * gs);
+    }
+  }
+}
+
+// the fused pass of one head: Z, counts, ranks of the lane's register row x (lane & 31, the
+// two lane halves holding alternate 4-column groups of every tile) and dacc += p . img
+__device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4], const bf16x8v (&qf)[8],
+                                             const int (&roff)[8], const int (&toff)[4][2], const ClArgs& a,
+                                             const Geo& g, int64_t base, int x, int xsq, float thr, float& Z,
+                                             int& cn, int& rk, float& pv, int spec_lo, int spec_hi,
+                                             RowCursor<true, 4>& cur, int w, int lane) {
+  constexpr int NW = 4, NK = 16 / NW, PT = NK + 1;  // DMAs per wave and tile: image + column bias
+  const int hh = lane >> 5;
+  const float it = 1.f / a.tau, c1 = it * LOG2E;
+  const bool live = x < g.n;
+  const uint64_t hmask = hh ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full;  // this half's columns
+  const int ntile = (g.n + 63) / 64;
+  auto stage = [&](int t) {
+    const int buf = t % CL_NB32, y0 = t * 64;
+    cur.stage(sh.r.img[buf], g.n, w, lane);
+    glds4(y0 + lane < a.n_max ? a.colb + base + y0 + lane : &cl_ninf, sh.r.m0[buf][w]);
+  };
+  retire_loads();
+  stage(0);
+  if (ntile > 1) stage(1);
+  if (ntile > 2) stage(2);
+  for (int tI = 0; tI < ntile; ++tI) {
+    const int cb = tI % CL_NB32, y0 = tI * 64;
+    if (tI + 2 < ntile) wait_vm<2 * PT>();
+    else if (tI + 1 < ntile) wait_vm<PT>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (tI + 3 < ntile) stage(tI + 3);
+    const unsigned char* img = sh.r.img[cb];
+    const float* colb = sh.r.m0[cb][w];
+    f32x16 acc[2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[ib][v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8v af = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ib * 8192 + roff[s]));
+        acc[ib] = mfma32(af, qf[s], acc[ib]);
+      }
+    }
+    const bool special = y0 < spec_hi && y0 + 64 > spec_lo;
+    if (!special) {
+      // every valid column is kept; pad / beyond-n columns are zero image rows (S = 0) with a
+      // -inf bias: counted out of cn, and out of the rank when 0 > thr
+      const int np = __popcll(__ballot(colb[lane] == -INFINITY) & hmask);
+      cn += 32 - np;
+      rk -= (0.f > thr) ? np : 0;
+    }
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const float4 c4 = *reinterpret_cast<const float4*>(colb + 32 * ib + 8 * qd + 4 * hh);
+        const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+        if (!special) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int v = 4 * qd + j;
+            const float sv = acc[ib][v];
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j]));
+            Z += p;
+            rk += sv > thr ? 1 : 0;
+            acc[ib][v] = p;
+          }
+        } else {
+          int ys0 = y0;  // laundered (see cl_bwd32_head)
+          asm volatile("" : "+s"(ys0));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int v = 4 * qd + j, yl = 32 * ib + 8 * qd + 4 * hh + j, y = ys0 + yl;
+            const float sv = acc[ib][v];
+            if (y == x) pv = sv * it;
+            const int ysq = y < g.n ? seq_of(g, y) : -1;
+            const bool keep = live && cv[j] != -INFINITY && (ysq != xsq || y == x);
+            float p = 0.f;
+            if (keep) {
+              p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j]));
+              Z += p;
+              cn += 1;
+              rk += (y != x && sv > thr) ? 1 : 0;
+            }
+            acc[ib][v] = p;
+          }
+        }
+      }
+      // dacc[32 x 128] += p[32 x 32] . img[32 x 128] (as cl_bwd32_head)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int ks = 2 * ib + hf, o = 8 * hf;
+        const f32x16& pvv = acc[ib];
+        const u32x4 hpk = {pk_bf16(pvv[o], pvv[o + 1]), pk_bf16(pvv[o + 2], pvv[o + 3]), pk_bf16(pvv[o + 4], pvv[o + 5]),
+                           pk_bf16(pvv[o + 6], pvv[o + 7])};
+        const bf16x8v af = __builtin_bit_cast(bf16x8v, hpk);
+#pragma unroll
+        for (int nd = 0; nd < 4; ++nd) {
+          const bf16x8v bfr = tr_frag32(img, toff[nd][0] + ks * 4096, toff[nd][1] + ks * 4096);
+          dacc[nd] = mfma32(af, bfr, dacc[nd]);
+        }
+      }
+    }
+  }
+}
+
+// grid ((n_max + 127) / 128, n_mb, heads): 4 waves x 32 register rows
+__global__ __launch_bounds__(256, 2) void cl_fr32_k(ClArgs a0) {
+  constexpr int NW = 4, XR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) ClTile32<NW> sh;
+  __shared__ float rs_sc[NW][32], rs_w[NW][32];  // per register row: w / Z and w
+  const int z = blockIdx.z;
+  const ClArgs a = head_args(a0, z);
+  const int mb = blockIdx.y, xb = blockIdx.x;
+  const Geo g = geo(a, mb);
+  const int x0 = xb * XR;
+  if (x0 >= g.n) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int64_t base = (int64_t)mb * a.n_max;
+  int roff[8], toff[4][2];
+  frag32_offsets(roff, toff, lane);
+  f32x16 dacc[4];
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) dacc[nd][v] = 0.f;
+  const int x = x0 + 32 * w + r32;
+  const bool live = x < g.n;
+  bf16x8v qf[8];
+  {
+    const bf16_t* rp = live ? out_row(a, g, x) : nullptr;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (live) v = *reinterpret_cast<const u32x4*>(rp + 16 * s + 8 * hh);
+      qf[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
+  const float it = 1.f / a.tau;
+  const float dg = live ? a.diag[base + x] : 0.f;
+  const float thr = rank_threshold(dg, it, a.tau);
+  const int xsq = live ? seq_of(g, x) : -2;
+  float Z = 0.f, pv = -INFINITY;
+  int cn = 0, rk = 0;
+  const int spec_lo = (x0 / g.L) * g.L, spec_hi = ((min(x0 + XR, g.n) - 1) / g.L + 1) * g.L;
+  RowCursor<true, 4> cur;
+  cur.init(a.in_n + ((g.b0 * a.T) + g.off) * DE, a.T * DE, DE, g.L, w, lane);
+  cl_fr32_head(sh, dacc, qf, roff, toff, a, g, base, x, xsq, thr, Z, cn, rk, pv, spec_lo, spec_hi, cur, w, lane);
+  // the two lane halves hold the row's alternate column groups
+  Z += __shfl_xor(Z, 32, 64);
+  cn += __shfl_xor(cn, 32, 64);
+  rk += __shfl_xor(rk, 32, 64);
+  pv = fmaxf(pv, __shfl_xor(pv, 32, 64));
+  const float wx = live ? a.w[base + x] : 0.f;
+  if (hh == 0) {
+    if (live) {
+      a.lse[base + x] = cn > 0 ? it + __logf(Z) : -INFINITY;
+      a.pos[base + x] = pv;
+      a.cnt[base + x] = cn;
+      a.rank[base + x] = rk;
+    }
+    rs_sc[w][r32] = (wx != 0.f && Z > 0.f) ? wx / Z : 0.f;
+    rs_w[w][r32] = wx;
+  }
+  // epilogue (as the ROWS kernel): restage, then 16 lanes per row through F.normalize into dy
+  __syncthreads();
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) sh.ep[w][8 * (v >> 2) + 4 * hh + (v & 3)][32 * nd + r32] = dacc[nd][v];
+  __syncthreads();
+  const float gs = 1.f / a.tau;  // unit upstream gradient
+  const int sub = lane & 15;
+#pragma unroll 1
+  for (int ps = 0; ps < 8; ++ps) {
+    const int rl = 4 * ps + (lane >> 4), xr = x0 + 32 * w + rl;
+    const int xc = min(xr, g.n - 1);  // every lane takes part in the row reduction
+    const int b = xc / g.L, t = xc - b * g.L;
+    const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
+    const float sc = rs_sc[w][rl], wr = rs_w[w][rl];
+    float inv[8];
+    load_vec<bf16_t, 16>(in_row(a, g, xc) + 8 * sub, inv);
+    const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
+    const float4 u1 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub + 4]);
+    const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    float gv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = gs * (uu[i] * sc - wr * inv[i]);
+    normalize_bwd_store(gv, a.y_raw, a.y_dtype, a.y_norm[ro], a.dy, ro * DE + 8 * sub, xr < g.n);
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -1548,17 +1826,31 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   const int64_t hm = (int64_t)nrun * d->n_mb;
   int* hist = (int*)d->stats_ws;
   double* part = (double*)((char*)d->stats_ws + ((hm * d->n_max * 4 + 7) / 8) * 8);
+  const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
+  const bool rows = fixed && d->y_raw && d->y_norm && d->dy && d->head == 0 && nrun == d->n_heads &&
+                    d->mb_size <= CL_UMAXB && (d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32);
+  if (rows) a.colb = (float*)hist;  // the per-column bias lives in the histogram until the fused pass is done
   if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
   hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb, nrun), dim3(256), 0, s, a);
   LTHM_CHECK_LAUNCH();
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
-  // the fixed softmax shift 1/tau bounds the plain logits only: logQ takes the online max
-  // fixed shift: 3 blocks per CU (3 waves per SIMD hide more of the exp / count VALU
-  // latency: 0.91 -> 0.78-0.82 ms per C2 head; a 2-deep ring at 3 blocks measured the
-  // same, 4 blocks spill); running shift: 2
-  if (2.f / d->tau <= 80.f && !d->logq) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
-  LTHM_CHECK_LAUNCH();
+  if (rows) {
+    // forward + the row side of the backward in one pass (row weights from the pad mask first)
+    hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+    if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
+    a.colb = d->w;
+  } else {
+    // the fixed softmax shift 1/tau bounds the plain logits only: logQ takes the online max
+    // fixed shift: 3 blocks per CU (3 waves per SIMD hide more of the exp / count VALU
+    // latency: 0.91 -> 0.78-0.82 ms per C2 head; a 2-deep ring at 3 blocks measured the
+    // same, 4 blocks spill); running shift: 2
+    if (fixed) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+  }
   const int nblk = (int)cl_stats_blocks(d->n_max);
   hipLaunchKernelGGL(cl_rowstats_k, dim3(nblk, d->n_mb, nrun), dim3(256), 0, s, a, hist, part);
   LTHM_CHECK_LAUNCH();
@@ -1581,6 +1873,28 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
   a.colb = d->diag;  // the shift scratch (advanced per head by head_args)
   hipStream_t s = (hipStream_t)stream;
   const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
+  if (fused && d->rows_done) {
+    // the forward ran the ROWS side (dy for a unit upstream gradient): COLS, then dy *= gscale
+    LTHM_REQUIRE(fixed && d->head == 0 && nrun == d->n_heads);
+    LTHM_REQUIRE((d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32) &&
+                 (d->t_dtype == LTHM_BF16 || d->t_dtype == LTHM_F32));
+    ClArgs ash = a;
+    ash.dy = nullptr;
+    ash.d_out = nullptr;  // the dy tails were zeroed by the forward
+    hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, ash);
+    LTHM_CHECK_LAUNCH();
+    const dim3 gcols((int)(((int64_t)d->mb_size * d->T + 127) / 128), d->n_mb, 1);
+    hipLaunchKernelGGL((cl_bwd32_k<false, true, 4>), gcols, dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+    if (d->gscale) {
+      const int64_t n = (int64_t)d->B * (d->T + 1) * d->n_heads * DE;
+      const dim3 gs((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 2048));
+      if (d->y_dtype == LTHM_BF16) hipLaunchKernelGGL(cl_dyscale_k<bf16_t>, gs, dim3(256), 0, s, (bf16_t*)d->dy, n, d->gscale);
+      else hipLaunchKernelGGL(cl_dyscale_k<float>, gs, dim3(256), 0, s, (float*)d->dy, n, d->gscale);
+      LTHM_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   if (fused) {
     // every head in one call: the COLS pass sums dIn over the heads and writes dt once
     LTHM_REQUIRE(d->head == 0 && nrun == d->n_heads);

@@ -77,13 +77,23 @@ class ContrastiveLossFn(torch.autograd.Function):
         wsb = load().lthm_contrastive_ws_bytes(n_mb, n_max, NH)
         ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
         d.stats_ws, d.stats_ws_bytes = ptr(ws), ws.numel() * 8
+        # training at the fixed shift: the forward also runs the row side of the backward and
+        # writes dy (unit upstream gradient) -- one S pass instead of the forward's plus ROWS'
+        rows = (ctx.needs_input_grad[0] and not _OLD_BWD and not _NO_FUSED_ROWS and logq is None
+                and 2.0 / tau <= 80.0 and mbs <= 4096 and yc.dtype in (torch.bfloat16, torch.float32))
+        dy = None
+        if rows:
+            dy = torch.empty_like(yc)
+            d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
+        # algorithmic work: 2 n^2 De per head (S); with the row side also dS . in (2 n^2 De)
         call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
-             1.0 / n_mb, stream(), _key="cl_fwd_k", _work=float(sum(cfg["flops"])), _unit="flop")
+             1.0 / n_mb, stream(), _key="cl_fwd_k", _work=(2.0 if rows else 1.0) * float(sum(cfg["flops"])),
+             _unit="flop")
         # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
         loss = torch.empty(1, **f32)
         call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
         loss = loss / n_mb
-        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc)
+        ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc, dy)
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
         cfg.get("stats_out", []).append(stats)
@@ -105,14 +115,15 @@ class ContrastiveLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dloss):
-        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc = ctx.saved_tensors
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc, dy_f = ctx.saved_tensors
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         g = dloss.contiguous().float()
         if _OLD_BWD:
             return ContrastiveLossFn._backward_per_head(ctx, g)
-        # every head in one call: the ROWS kernel writes dy per head through F.normalize, the
-        # COLS kernel sums dIn over the six heads on chip and writes dt once through F.normalize
-        dy = torch.empty_like(yc)
+        # every head in one call: the ROWS kernel writes dy per head through F.normalize (or the
+        # forward already did: rows_done, dy scaled by g here), the COLS kernel sums dIn over the
+        # six heads on chip and writes dt once through F.normalize
+        dy = dy_f if dy_f is not None else torch.empty_like(yc)
         dt = torch.empty_like(tc)
         d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, 0, De, mbs, n_mb, n_max, tau, offsets_dev,
                                     lse[0], None, None, None, diag[0], w[0],  # diag: shift scratch
@@ -121,17 +132,18 @@ class ContrastiveLossFn(torch.autograd.Function):
         d.gscale = ptr(g)
         d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
         d.t_raw, d.t_norm, d.dt, d.t_dtype = ptr(tc), ptr(tnorm), ptr(dt), dcode(tc)
-        # algorithmic work 3 x 2 n^2 De per head (one S recompute, dS . in, dS^T . out);
-        # the ROWS and COLS kernels each recompute S, so they execute 4 x
+        d.rows_done = 1 if dy_f is not None else 0
+        # algorithmic work per head: one S recompute + dS^T . out (2 x 2 n^2 De) with the row side
+        # done in the forward; else also dS . in (3 x; the ROWS and COLS kernels each recompute S)
         call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
-             _work=3.0 * float(sum(ctx.flops)), _unit="flop")
+             _work=(2.0 if dy_f is not None else 3.0) * float(sum(ctx.flops)), _unit="flop")
         return dy, dt, None, None, None, None
 
     @staticmethod
     def _backward_per_head(ctx, g):
         """The round-2 backward (16x16x32 kernels, one call per head, f32 d_in read-modify-written
         per head); kept behind LTHM_CL_BWD_OLD=1 for A/B measurements."""
-        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc = ctx.saved_tensors
+        yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc, _ = ctx.saved_tensors
         B, T, NH, De, mbs, n_mb, n_max, tau = ctx.meta
         dev = yc.device
         fuse = yc.dtype == torch.bfloat16
@@ -153,6 +165,7 @@ class ContrastiveLossFn(torch.autograd.Function):
 
 
 _OLD_BWD = os.environ.get("LTHM_CL_BWD_OLD") == "1"
+_NO_FUSED_ROWS = os.environ.get("LTHM_CL_NO_FUSED_ROWS") == "1"  # A/B: separate forward and ROWS passes
 
 
 def contrastive_step(y, tgt, mask, offs: np.ndarray, mbs: int, tau: float, ks: List[int], logq=None):
