@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lthm {
 
@@ -252,6 +253,7 @@ struct ClArgs {
   int t_dtype;
   const float* t_norm;  // [B, T]
   void* dt;             // [B, T, DE], dtype t_dtype, every row written
+  int xcd_order;        // fused forward: XCD-remapped block order (A/B switch LTHM_CL_FR_XCD)
 };
 
 // the per-head view of a multi-head forward launch: head head0 + z, buffers advanced by z strides
@@ -1631,9 +1633,16 @@ __global__ __launch_bounds__(256, 2) void cl_fr32_k(ClArgs a0) {
   constexpr int NW = 4, XR = 32 * NW;
   __shared__ __attribute__((aligned(16))) ClTile32<NW> sh;
   __shared__ float rs_sc[NW][32], rs_w[NW][32];  // per register row: w / Z and w
-  const int z = blockIdx.z;
+  int z = blockIdx.z, mb = blockIdx.y, xb = blockIdx.x;
+  if (a0.xcd_order) {
+    const int per = gridDim.x * gridDim.y;
+    const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), per * gridDim.z);
+    z = lin / per;
+    const int bid = lin - z * per;
+    mb = bid / gridDim.x;
+    xb = bid - mb * gridDim.x;
+  }
   const ClArgs a = head_args(a0, z);
-  const int mb = blockIdx.y, xb = blockIdx.x;
   const Geo g = geo(a, mb);
   const int x0 = xb * XR;
   if (x0 >= g.n) return;
@@ -1732,6 +1741,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.y_dtype = d->y_dtype;
   a.heads_run = d->heads_run > 1 ? d->heads_run : 1;
   a.t_raw = d->t_raw; a.t_dtype = d->t_dtype; a.t_norm = d->t_norm; a.dt = d->dt;
+  a.xcd_order = 0;
   return a;
 }
 
@@ -1838,6 +1848,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
     // forward + the row side of the backward in one pass (row weights from the pad mask first)
     hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
     LTHM_CHECK_LAUNCH();
+    static const int xcd = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : 0;
+    a.xcd_order = xcd;
     hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
