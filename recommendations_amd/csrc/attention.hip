@@ -1596,6 +1596,172 @@ static int attn_launch(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   return (int)hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------
+// Forward on 32x32x16 MFMA (E = 64, T' up to 620, no general mask): one workgroup per
+// (b, h) with the K and V images resident in LDS (2 T' x 128 B: the windowed path is not
+// needed while they fit), 32-row query tiles balanced over the waves, longest first.  Per
+// tile pair: S^T = K . Q^T (the query is the lane; the two lane halves hold alternate key
+// groups, so the running max and sum combine with one lane swap), online softmax in log2
+// units with the bias as pre-shifted log2-scaled copies (as the backward), and
+// O^T += V^T . P^T with P^T straight from the accumulator as bf16 hi + lo (the split keeps
+// the output within 1e-3 of the bf16-rounded fp32 reference).  O leaves as the transposed
+// accumulator (8-byte runs of each query's row), lse per query.
+__host__ __device__ __forceinline__ int fwd32_slack(int T) {
+  const int d = ((T + 31) & ~31) - bwd32_timg(T);
+  return d > 0 ? d : 0;
+}
+static size_t fwd32_lds(int T) {
+  return (size_t)2 * bias_ne(T) * 4 + (size_t)(2 * bwd32_timg(T) + fwd32_slack(T)) * 128;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  const int T = a.T, Tk = (T + 31) & ~31, nt = Tk / 32, ne = bias_ne(T), Ti = bwd32_timg(T);
+  float* brv = reinterpret_cast<float*>(smem);  // [2][ne] descending copies (rows units' layout)
+  unsigned char* IK = smem + 2 * ne * 4;
+  unsigned char* IV = IK + Ti * 128;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, r32 = lane & 31;
+  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+  const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+  const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+  stage_img32(IK, kg, a.k_ts, T, Ti, wave, lane, NW);
+  stage_img32(IV, vg, a.v_ts, T, Ti, wave, lane, NW);
+  for (int c = 0; c < 2; ++c)
+    for (int y = tid; y < ne; y += 64 * NW) {
+      const int xr = ne - 1 - (y + c) - BPAD;
+      brv[c * ne + y] = (a.table && xr >= 0 && xr <= 2 * T) ? a.table[(int64_t)xr * a.H + h] * L2E : 0.f;
+    }
+  for (int i = tid; i < fwd32_slack(T) * 32; i += 64 * NW) reinterpret_cast<float*>(IV + Ti * 128)[i] = 0.f;
+  wait_vm<0>();
+  __syncthreads();
+  const Frag32Off fo = frag32_off(lane);
+  const float c2 = rsqrtf((float)E_BWD32) * L2E;
+  const bool ragged = (T & 31) != 0;
+  // query tiles over the waves, longest first (cost: key tiles visited + 1)
+  uint32_t lo_mask = 0, hi_mask = 0;  // up to 64 tiles
+  {
+    int load[NW] = {};
+    for (int t = nt - 1; t >= 0; --t) {
+      const int cost = (a.causal ? t + 1 : nt) + 1;
+      int w = 0;
+#pragma unroll
+      for (int j = 1; j < NW; ++j)
+        if (load[j] < load[w]) w = j;
+      load[w] += cost;
+      if (w == wave) {
+        if (t < 32) lo_mask |= 1u << t;
+        else hi_mask |= 1u << (t - 32);
+      }
+    }
+  }
+  bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+  float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  for (int t = nt - 1; t >= 0; --t) {
+    if (!((t < 32 ? lo_mask >> t : hi_mask >> (t - 32)) & 1u)) continue;
+    const int i = t, q0 = 32 * i, q = q0 + r32;
+    bf16x8v qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (q < T) v = *reinterpret_cast<const u32x4*>(qg + (int64_t)q * a.q_ts + 16 * s + 8 * hh);
+      qf[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+    f32x16 o[2];
+#pragma unroll
+    for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) o[nd][v] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int kmax = q < T ? (a.causal ? q + 1 : T) : 0;
+    const int z0 = ne - 1 - (q - 4 * hh + T + BPAD);
+    const float* bp = brv + (z0 & 1) * ne + (z0 & ~1);
+    const int jend = a.causal ? i + 1 : nt;
+    for (int j = 0; j < jend; ++j, bp += 32) {
+      const int k0 = 32 * j;
+      f32x16 st;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) st[v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = MFMA32(frag_at(IK + k0 * 128 + fo.row[s]), qf[s], st);
+      // S^T[k][q] -> log2-scaled logits; the key k = k0 + 8 g + 4 hh + jj in register 4 g + jj
+      const bool edge = (a.causal && j == i) || (ragged && (i == nt - 1 || j == nt - 1));
+      float mt = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float2 blo = *reinterpret_cast<const float2*>(bp + 8 * g);
+        const float2 bhi = *reinterpret_cast<const float2*>(bp + 8 * g + 2);
+        const float bv[4] = {blo.x, blo.y, bhi.x, bhi.y};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int v = 4 * g + jj;
+          float tv = fmaf(st[v], c2, bv[jj]);
+          if (edge && !(k0 + 8 * g + 4 * hh + jj < kmax)) tv = -INFINITY;
+          st[v] = tv;
+          mt = fmaxf(mt, tv);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float mu = mn == -INFINITY ? 0.f : mn;  // no live key yet: every p is 0
+      const float sc = __builtin_amdgcn_exp2f(m - mu);  // m = -inf: 0
+      l *= sc;
+#pragma unroll
+      for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) o[nd][v] *= sc;
+      m = mn;
+      f32x16 lo;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float p = __builtin_amdgcn_exp2f(st[v] - mu);
+        l += p;
+        st[v] = p;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8v hf = acc_frag32(st, s2);
+        const u32x4 hb = __builtin_bit_cast(u32x4, hf);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // the remainder p - bf16(p), exact in f32
+          lo[8 * s2 + 2 * e] = st[8 * s2 + 2 * e] - __uint_as_float(hb[e] << 16);
+          lo[8 * s2 + 2 * e + 1] = st[8 * s2 + 2 * e + 1] - __uint_as_float(hb[e] & 0xffff0000u);
+        }
+        const bf16x8v lf = acc_frag32(lo, s2);
+        const unsigned char* vt = IV + (k0 + 16 * s2) * 128;
+#pragma unroll
+        for (int nd = 0; nd < 2; ++nd) {
+          const bf16x8v vf = tr_at(vt + fo.tr[nd][0], vt + fo.tr[nd][1]);
+          o[nd] = MFMA32(vf, hf, o[nd]);
+          o[nd] = MFMA32(vf, lf, o[nd]);
+        }
+      }
+    }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int nd = 0; nd < 2; ++nd) store_accT32(o[nd], inv, og, a.o_ts, q0, nd, T, lane);
+    if (hh == 0 && q < T) lse_g[q] = l > 0.f ? (m + __log2f(l)) * LN2 : -INFINITY;
+  }
+}
+
+// the 32x32x16 forward: E = 64, K and V images within LDS (T' <= 620), not switched off
+static bool fwd32_ok(const AttnArgs& a) {
+  static const bool off = getenv("LTHM_ATTN_FWD_OLD") && atoi(getenv("LTHM_ATTN_FWD_OLD"));  // A/B switch
+  return !off && fwd32_lds(a.T) <= 160 * 1024 && a.T <= 2048;
+}
+static int attn_launch_fwd32(const AttnArgs& a, int B, hipStream_t s) {
+  const size_t sh = fwd32_lds(a.T);
+  // more than 80 KiB of images: one block per CU, so 8 waves (two per SIMD)
+  if (sh > 80 * 1024) hipLaunchKernelGGL(attn_fwd32_k<8>, dim3(B * a.H), dim3(512), sh, s, a);
+  else hipLaunchKernelGGL(attn_fwd32_k<4>, dim3(B * a.H), dim3(256), sh, s, a);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
   if (a.mask) {  // general additive mask: the whole-head VALU kernels
     if (a.T > 256) return (int)hipErrorInvalidValue;
@@ -1608,6 +1774,7 @@ static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t 
     }
   }
   if (attn_windowed(a.T)) {
+    if (E == 64 && !bwd && fwd32_ok(a)) return attn_launch_fwd32(a, B, s);
     switch (E) {
       case 32: return attn_launch_win<32>(a, B, bwd, s);
       case 64: return attn_launch_win<64>(a, B, bwd, s);
@@ -1618,7 +1785,8 @@ static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t 
   switch (E) {
     case 16: return attn_launch<16>(a, B, bwd, s);
     case 32: return attn_launch_mfma<32>(a, B, bwd, s);
-    case 64: return attn_launch_mfma<64>(a, B, bwd, s);
+    case 64: if (!bwd && fwd32_ok(a)) return attn_launch_fwd32(a, B, s);
+             return attn_launch_mfma<64>(a, B, bwd, s);
     case 128: return attn_launch_mfma<128>(a, B, bwd, s);
     default: return (int)hipErrorInvalidValue;
   }

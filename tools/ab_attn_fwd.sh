@@ -1,0 +1,8 @@
+# attention forward 32x32x16 vs the 16x16x32 / windowed kernels: encoder GPU tests, then the
+# probe at the C2 and C5 shapes with LTHM_ATTN_FWD_OLD=1 / 0
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_encoder.py > gpurun_out/af_tests.log 2>&1 || { tail -40 gpurun_out/af_tests.log; exit 1; }
+tail -2 gpurun_out/af_tests.log
+for sh in 4096,129,4 1024,513,8; do
+  for v in 1 0; do SHAPE=$sh TAG="shape=$sh old=$v" LTHM_ATTN_FWD_OLD=$v timeout -k 10 120 python3 tools/attn_probe.py || exit 1; done
+done

@@ -12,7 +12,9 @@ from gemm_bench import timeit  # noqa: E402
 
 def main():
     dev = torch.device("cuda")
-    B, T, H, E = 4096, 129, 4, 64
+    # C2 by default; SHAPE=B,T,H overrides (C5: 1024,513,8)
+    B, T, H = (int(v) for v in os.environ.get("SHAPE", "4096,129,4").split(","))
+    E = 64
     qkv = (torch.randn(B * T, 3 * H * E, device=dev) * 0.5).to(torch.bfloat16)
     tab = torch.randn(2 * T + 1, H, device=dev) * 0.1
     out, lse = K.attn_fwd_qkv(qkv, B, T, H, E, table=tab)
