@@ -17,7 +17,8 @@ import torch  # noqa: F401  (loads torch's libamdhip64 first, so the .so binds t
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(_PKG_DIR)
 HEADER = os.path.join(REPO_ROOT, "include", "lthm.h")
-LIB_PATH = os.path.join(_PKG_DIR, "liblthm_hip.so")
+# LTHM_LIB_PATH: another in-tree build of the same library, for A/B measurements of a kernel change
+LIB_PATH = os.environ.get("LTHM_LIB_PATH") or os.path.join(_PKG_DIR, "liblthm_hip.so")
 
 F32 = 0
 BF16 = 1

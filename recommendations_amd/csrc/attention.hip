@@ -904,6 +904,9 @@ __device__ __forceinline__ void rows_math(f32x16& st, const f32x16& pt, const fl
   }
 }
 
+// G: Q / dO fragments from global memory, once per query tile (the rows kernel of long T'
+// holds only the K / V images); else re-read per tile from the images
+template <bool G = false>
 __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
                                            int i, int lane) {
   constexpr float L2E = 1.4426950408889634f;
@@ -911,6 +914,21 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
   const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
   const bool ragged = (T & 31) != 0;
   const int q0 = 32 * i, q = q0 + r32;
+  bf16x8v gq[4], gd[4];
+  if constexpr (G) {
+    const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
+    const bf16_t* dg = a.dout + b * a.o_bs + h * a.o_hs;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u32x4 u = {0u, 0u, 0u, 0u}, v = u;
+      if (q < T) {
+        u = *reinterpret_cast<const u32x4*>(qg + (int64_t)q * a.q_ts + 16 * s + 8 * hh);
+        v = *reinterpret_cast<const u32x4*>(dg + (int64_t)q * a.o_ts + 16 * s + 8 * hh);
+      }
+      gq[s] = __builtin_bit_cast(bf16x8v, u);
+      gd[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
   const float lq = m.lse[q], dl = m.dlt[q];
   const int kmax = q < T ? (a.causal ? q + 1 : T) : 0;  // keys k < kmax are live for this query
   f32x16 dq[2];
@@ -939,8 +957,8 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
     asm volatile("" : "+v"(qo));
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      st = MFMA32(frag_at(m.IK + k0 * 128 + fo.row[s]), frag_at(m.IQ + qo + fo.row[s]), st);
-      pt = MFMA32(frag_at(m.IV + k0 * 128 + fo.row[s]), frag_at(m.IO + qo + fo.row[s]), pt);
+      st = MFMA32(frag_at(m.IK + k0 * 128 + fo.row[s]), G ? gq[s] : frag_at(m.IQ + qo + fo.row[s]), st);
+      pt = MFMA32(frag_at(m.IV + k0 * 128 + fo.row[s]), G ? gd[s] : frag_at(m.IO + qo + fo.row[s]), pt);
     }
     // S^T[k][q]: the key k = k0 + 8 g + 4 hh + jj in register 4 g + jj, the query q in the lane
     if ((a.causal && j == i) || (ragged && (i == nt - 1 || j == nt - 1)))
@@ -1009,6 +1027,9 @@ __device__ __forceinline__ void cols_math(f32x16& sx, f32x16& px, const float* b
   }
 }
 
+// G: K / V fragments from global memory, once per key tile (the columns kernel of long T'
+// holds only the Q / dO images)
+template <bool G = false>
 __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
                                            int j, int lane) {
   constexpr float L2E = 1.4426950408889634f;
@@ -1016,6 +1037,21 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
   const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
   const bool ragged = (T & 31) != 0;
   const int k0 = 32 * j, k = k0 + r32;
+  bf16x8v gk[4], gv[4];
+  if constexpr (G) {
+    const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
+    const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u32x4 u = {0u, 0u, 0u, 0u}, v = u;
+      if (k < T) {
+        u = *reinterpret_cast<const u32x4*>(kg + (int64_t)k * a.k_ts + 16 * s + 8 * hh);
+        v = *reinterpret_cast<const u32x4*>(vg + (int64_t)k * a.v_ts + 16 * s + 8 * hh);
+      }
+      gk[s] = __builtin_bit_cast(bf16x8v, u);
+      gv[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
   // live queries of this key: [qlo, T)
   const int qlo = k < T ? (a.causal ? k : 0) : T, span = T - qlo;
   f32x16 dk[2], dv[2];
@@ -1042,8 +1078,8 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
     asm volatile("" : "+v"(ko));
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sx = MFMA32(frag_at(m.IQ + q0 * 128 + fo.row[s]), frag_at(m.IK + ko + fo.row[s]), sx);
-      px = MFMA32(frag_at(m.IO + q0 * 128 + fo.row[s]), frag_at(m.IV + ko + fo.row[s]), px);
+      sx = MFMA32(frag_at(m.IQ + q0 * 128 + fo.row[s]), G ? gk[s] : frag_at(m.IK + ko + fo.row[s]), sx);
+      px = MFMA32(frag_at(m.IO + q0 * 128 + fo.row[s]), G ? gv[s] : frag_at(m.IV + ko + fo.row[s]), px);
     }
     // S[q][k]: the query q = q0 + 8 g + 4 hh + jj in register 4 g + jj, the key k in the lane
     const int qb0 = q0 + 4 * hh;
@@ -1518,8 +1554,18 @@ static size_t cols_win_lds(int T, int E) {
 // windowed path: T' beyond what one workgroup keeps in LDS whole
 static bool attn_windowed(int T) { return T > 256; }
 static int attn_row_blocks(int T) { return (T + AW_R - 1) / AW_R; }
+static int64_t attn_win_parts(int B, int T) { return (int64_t)((B + AW_BG - 1) / AW_BG) * attn_row_blocks(T); }
+// bias-gradient partials: the windowed kernels write one per (batch group, row block), the
+// 32x32 long-T' kernels one per batch entry; whichever path runs zeroes the rest
 static int64_t attn_parts(int B, int T) {
-  return attn_windowed(T) ? (int64_t)((B + AW_BG - 1) / AW_BG) * attn_row_blocks(T) : (int64_t)B;
+  return attn_windowed(T) ? std::max<int64_t>(attn_win_parts(B, T), B) : (int64_t)B;
+}
+static int attn_zero_parts(const AttnArgs& a, int64_t used, int64_t parts, hipStream_t s) {
+  if (!a.dtable_part || parts <= used) return 0;
+  const size_t row = (size_t)(2 * a.T + 1) * a.H;
+  return hipMemsetAsync(a.dtable_part + used * row, 0, (size_t)(parts - used) * row * 4, s) == hipSuccess
+             ? 0
+             : (int)hipErrorInvalidValue;
 }
 
 template <int E>
@@ -1541,7 +1587,7 @@ static int attn_launch_win(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   LTHM_CHECK_LAUNCH();
   hipLaunchKernelGGL((attn_bwd_cols_win_k<E>), dim3(B * a.H, nrb), dim3(256), sc, s, a);
   LTHM_CHECK_LAUNCH();
-  return 0;
+  return attn_zero_parts(a, attn_win_parts(B, a.T), attn_parts(B, a.T), s);
 }
 
 static size_t fwd_mfma_lds(int T, int E) {
@@ -1594,6 +1640,86 @@ static int attn_launch(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   LTHM_ATTN_CASE(4)
 #undef LTHM_ATTN_CASE
   return (int)hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------
+// Backward for long T' (E = 64, 256 < T' <= 620): the four images no longer fit together, so
+// two kernels of one 8-wave workgroup per (b, h) each hold two: the rows kernel K and V
+// (rows units, dQ and the bias gradient, Q / dO fragments from global once per query tile),
+// the columns kernel Q and dO (columns units, dK and dV, K / V fragments from global once
+// per key tile); delta = dO . O comes from attn_delta_k.  Same units as attn_bwd32_k.
+__host__ __device__ __forceinline__ int bwd32l_fbytes(int T) {
+  return (2 * bias_ne(T) + 2 * ((T + 31) & ~31) + ((2 * T + 1 + 3) & ~3)) * 4;
+}
+static size_t bwd32l_lds(int T) {
+  return (size_t)bwd32l_fbytes(T) + (size_t)(2 * bwd32_timg(T) + bwd32_slack(T)) * 128;
+}
+
+template <int NW, bool ROWS>
+__global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr float L2E = 1.4426950408889634f;
+  const int T = a.T, Tk = (T + 31) & ~31, nt = Tk / 32, ne = bias_ne(T), Ti = bwd32_timg(T);
+  float* bias = reinterpret_cast<float*>(smem);  // [2][ne]: descending (rows) or ascending (columns) copies
+  float* lse_s = bias + 2 * ne;                  // [Tk]
+  float* dlt_s = lse_s + Tk;                     // [Tk]
+  float* dbias = dlt_s + Tk;                     // [2T + 1] (rows)
+  unsigned char* I0 = smem + bwd32l_fbytes(T);   // rows: K, columns: Q
+  unsigned char* I1 = I0 + Ti * 128;             // rows: V, columns: dO
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (ROWS) {
+    stage_img32(I0, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, T, Ti, wave, lane, NW);
+    stage_img32(I1, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, T, Ti, wave, lane, NW);
+  } else {
+    stage_img32(I0, a.q + b * a.q_bs + h * a.q_hs, a.q_ts, T, Ti, wave, lane, NW);
+    stage_img32(I1, a.dout + b * a.o_bs + h * a.o_hs, a.o_ts, T, Ti, wave, lane, NW);
+  }
+  for (int c = 0; c < 2; ++c)
+    for (int y = tid; y < ne; y += 64 * NW) {
+      const int x = ROWS ? ne - 1 - (y + c) - BPAD : y + c - BPAD;
+      bias[c * ne + y] = (a.table && x >= 0 && x <= 2 * T) ? a.table[(int64_t)x * a.H + h] * L2E : 0.f;
+    }
+  const int64_t rb = ((int64_t)b * a.H + h) * T;
+  for (int i = tid; i < Tk; i += 64 * NW) {
+    lse_s[i] = i < T ? a.lse[rb + i] * L2E : 0.f;
+    dlt_s[i] = i < T ? a.delta[rb + i] : 0.f;
+  }
+  if (ROWS)
+    for (int i = tid; i <= 2 * T; i += 64 * NW) dbias[i] = 0.f;
+  for (int i = tid; i < bwd32_slack(T) * 32; i += 64 * NW) reinterpret_cast<float*>(I1 + Ti * 128)[i] = 0.f;
+  wait_vm<0>();
+  __syncthreads();
+  const Bwd32Smem m = ROWS ? Bwd32Smem{I0, nullptr, nullptr, I1, nullptr, bias, lse_s, dlt_s, dbias, ne}
+                           : Bwd32Smem{nullptr, I0, I1, nullptr, bias, nullptr, lse_s, dlt_s, dbias, ne};
+  const Frag32Off fo = frag32_off(lane);
+  // tiles over the waves, longest first (rows: query tile t visits t + 1 key tiles; columns:
+  // key tile t visits nt - t query tiles)
+  uint32_t mk[2] = {0u, 0u};  // up to 64 tiles
+  {
+    int load[NW] = {};
+    for (int c = nt; c >= 1; --c) {
+      const int t = ROWS ? c - 1 : nt - c;
+      const int cost = (a.causal ? c : nt) + 1;
+      int w = 0;
+#pragma unroll
+      for (int j = 1; j < NW; ++j)
+        if (load[j] < load[w]) w = j;
+      load[w] += cost;
+      if (w == wave) mk[t >> 5] |= 1u << (t & 31);
+    }
+  }
+  for (int c = nt; c >= 1; --c) {
+    const int t = ROWS ? c - 1 : nt - c;
+    if (!((mk[t >> 5] >> (t & 31)) & 1u)) continue;
+    if (ROWS) bwd32_rows<true>(a, m, fo, b, h, t, lane);
+    else bwd32_cols<true>(a, m, fo, b, h, t, lane);
+  }
+  if (ROWS && a.dtable_part) {
+    __syncthreads();
+    for (int i = tid; i <= 2 * T; i += 64 * NW) a.dtable_part[((int64_t)b * (2 * T + 1) + i) * a.H + h] = dbias[i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1762,6 +1888,22 @@ static int attn_launch_fwd32(const AttnArgs& a, int B, hipStream_t s) {
   return 0;
 }
 
+// the long-T' 32x32x16 backward (E = 64): two images of T' rows within LDS
+static bool bwd32l_ok(const AttnArgs& a) {
+  static const bool off = getenv("LTHM_ATTN_BWD_OLD") && atoi(getenv("LTHM_ATTN_BWD_OLD"));  // A/B switch
+  return !off && a.delta && bwd32l_lds(a.T) <= 160 * 1024 && a.T <= 2048;
+}
+static int attn_launch_bwd32l(const AttnArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL((attn_delta_k<64>), dim3(grid_for((int64_t)B * a.H * a.T, 256, 256 * 16)), dim3(256), 0, s, a);
+  LTHM_CHECK_LAUNCH();
+  const size_t sh = bwd32l_lds(a.T);
+  hipLaunchKernelGGL((attn_bwd32l_k<8, true>), dim3(B * a.H), dim3(512), sh, s, a);
+  LTHM_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd32l_k<8, false>), dim3(B * a.H), dim3(512), sh, s, a);
+  LTHM_CHECK_LAUNCH();
+  return attn_zero_parts(a, B, attn_parts(B, a.T), s);
+}
+
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
   if (a.mask) {  // general additive mask: the whole-head VALU kernels
     if (a.T > 256) return (int)hipErrorInvalidValue;
@@ -1775,6 +1917,7 @@ static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t 
   }
   if (attn_windowed(a.T)) {
     if (E == 64 && !bwd && fwd32_ok(a)) return attn_launch_fwd32(a, B, s);
+    if (E == 64 && bwd && bwd32l_ok(a)) return attn_launch_bwd32l(a, B, s);
     switch (E) {
       case 32: return attn_launch_win<32>(a, B, bwd, s);
       case 64: return attn_launch_win<64>(a, B, bwd, s);

@@ -171,7 +171,7 @@ def test_layernorm_golden(dev):
                                             (2, 47, 3, 32, True),
                                             # windowed long-sequence path (T' > 256; C5 has T' = 513)
                                             (2, 513, 2, 64, True), (3, 300, 1, 64, False), (17, 257, 1, 32, True),
-                                            (1, 400, 2, 128, True)])
+                                            (1, 400, 2, 128, True), (20, 520, 1, 64, True)])
 def test_attention_vs_oracle(dev, B, T, H, E, causal):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(B * T + H)
