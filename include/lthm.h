@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 27 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 28 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -157,6 +157,7 @@ typedef struct lthm_gemm_desc {
   int32_t pad1;
   const float* a_scale;
   const float* b_scale;
+  int32_t* amax_out; /* optional: atomic max of |C| (as f32 bits) over the stored values */
 } lthm_gemm_desc;
 
 /* ab_dtype LTHM_BF16 (0 is read as bf16 too) or LTHM_FP8_E4M3: A [M, K] and B [N, K]
@@ -171,6 +172,14 @@ int lthm_gemm(const lthm_gemm_desc* desc, void* stream);
  * (n % 8 == 0, 16-B aligned); q: n bytes; scale: device f32; work: 4-byte scratch. */
 int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_t* q, float* scale, int32_t* work,
                       void* stream);
+/* The same quantisation with amax(|x|) already reduced by the producer (the f32 bits of
+ * the maximum in *amax: lthm_layernorm_fwd_amax, lthm_gemm's amax_out, lthm_amax), so
+ * x is read once: the C5 encoder's fused quantisation. */
+int lthm_quantize_fp8_amax(const void* x, int32_t dtype, int64_t n, const int32_t* amax, uint8_t* q, float* scale,
+                           void* stream);
+/* *amax = max(*amax, amax(|x|)) as f32 bits (x: n f32 / bf16, n % 8 == 0, 16-B aligned);
+ * the caller zeroes *amax before the first producer. */
+int lthm_amax(const void* x, int32_t dtype, int64_t n, int32_t* amax, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Fused encoder MLP: _MLP.forward, commons/transformers/layers.py:279-284      */
@@ -192,6 +201,10 @@ int lthm_mlp_fwd(const void* x, int64_t M, int32_t D, int32_t HID, const void* W
 /* x f32 [M, D] -> y (y_dtype) [M, D], mean/rstd f32 [M]. b may be NULL (bias=False). */
 int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const float* w, const float* b,
                        void* y, int32_t y_dtype, float* mean, float* rstd, void* stream);
+/* lthm_layernorm_fwd that also folds amax(|y|) (of the stored, rounded y) into *amax
+ * (f32 bits, atomic max; the caller zeroes it): the fp8 quantisation's reduction. */
+int lthm_layernorm_fwd_amax(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y,
+                            int32_t y_dtype, float* mean, float* rstd, int32_t* amax, void* stream);
 /* number of row blocks the backward uses (partials is [2, blocks, D] f32) */
 int lthm_layernorm_bwd_blocks(int64_t M);
 /* dx = LN'(dy) + res1 + res2 (f32; res may be NULL), optional bf16 copy of dx;

@@ -92,29 +92,36 @@ class TransformerBlockFn(torch.autograd.Function):
         M = B * T
         x2 = x.contiguous().view(M, d)
         wqkv_b, wp_b, w1_b, w2_b = _bf(wqkv), _bf(wp), _bf(w1), _bf(w2)
+        # am: the activations' max |x| words for the fp8 mode, reduced by their producers
+        # (layernorm_fwd, the c_fc epilogue; the attention output by one amax pass) so
+        # that each quantisation reads its input once
+        am = torch.zeros(4, dtype=torch.int32, device=x.device) if fp8 else None
         if fp8:
             # build-defined C5 mode: the four forward GEMMs take per-tensor-scaled e4m3
             # operands on the fp8 MFMA; the backward runs bf16 on the saved activations
-            def lin(xb, wb, b, **kw):
-                xq, xs = K.quantize_fp8(xb)
+            def lin(xb, wb, b, amax_in=None, **kw):
+                xq, xs = K.quantize_fp8(xb, amax=amax_in)
                 wq, ws = K.quantize_fp8(wb)
                 return K.linear_fwd_fp8(xq, xs, wq, ws, b, **kw)
         else:
-            def lin(xb, wb, b, **kw):
+            def lin(xb, wb, b, amax_in=None, **kw):
                 return K.linear_fwd(xb, wb, b, **kw)
         pa, pr, seed = drop if drop is not None else (0.0, 0.0, 0)
-        h1, mu1, rs1 = K.layernorm_fwd(x2, ln1w.detach(), _f(ln1b))
-        qkv = lin(h1, wqkv_b, _f(bqkv))
+        h1, mu1, rs1 = K.layernorm_fwd(x2, ln1w.detach(), _f(ln1b), amax=am[0:1] if fp8 else None)
+        qkv = lin(h1, wqkv_b, _f(bqkv), amax_in=am[0:1] if fp8 else None)
         if pa > 0.0:
             K.dropout_rows_(qkv, 3, pa, seed)  # the attention sees (and the backward saves) the scaled q / k / v
         tab = None if table is None else table.detach().contiguous()
         mop = K.attn_mask_operand(mask, B, H, T)
         o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop)
+        if fp8:
+            K.amax_(o, am[1:2])
         if pr > 0.0:
-            x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32), pr, seed + 1, res1=x2)
+            x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None), pr,
+                           seed + 1, res1=x2)
         else:
-            x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32)
-        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+            x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None)
+        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
         if infer and not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]):
             # inference (no backward will run): the fused MLP keeps the [M, 4d] hidden on chip
             out = K.mlp_fwd(h2, w1_b, _f(b1), w2_b.t().contiguous(), _f(b2), res1=x1,
@@ -122,12 +129,17 @@ class TransformerBlockFn(torch.autograd.Function):
             return out.view(B, T, d)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
-        g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre)
+        if fp8:
+            g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre, amax_in=am[2:3], amax_out=am[3:4])
+        else:
+            g = lin(h2, w1_b, _f(b1), act=K.ACT_GELU_D, aux_out=pre)
+        gam = am[3:4] if fp8 else None
         if pr > 0.0:
-            out = K.dropout(lin(g, w2_b, _f(b2), out_dtype=torch.float32), pr, seed + 2, res1=x1,
+            out = K.dropout(lin(g, w2_b, _f(b2), out_dtype=torch.float32, amax_in=gam), pr, seed + 2, res1=x1,
                             res2=x2 if double_residual else None)
         else:
-            out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32)
+            out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32,
+                      amax_in=gam)
         ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,

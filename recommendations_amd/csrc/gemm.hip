@@ -45,6 +45,7 @@ struct GemmArgs {
   bool fast_ok;        // 16-B aligned operands and leading dims (interior-tile fast path)
   const float* sa;     // fp8 per-tensor scales (device scalars), or null
   const float* sb;
+  unsigned* amax;      // atomic max of |C| as f32 bits (gemm_ps_k epilogues), or null
 };
 
 __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
@@ -503,6 +504,13 @@ __device__ __forceinline__ void ps_epi_load(const GemmArgs& g, PsIn<EPI>& in, in
   }
 }
 
+// running max of |C| over one lane's 8 stored values (rounded as stored)
+__device__ __forceinline__ float ps_amax8(float m, const float* v, int dt) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(dt == LTHM_F32 ? v[e] : bf2f(f2bf(v[e]))));
+  return m;
+}
+
 typedef int i32x8v __attribute__((ext_vector_type(8)));
 // fp8 A/B fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row rbase + (l & 15),
 // k bytes 32 (l >> 4) .. + 31 = the two 16-B chunks 2 (l >> 4), 2 (l >> 4) + 1 of a 128-B row
@@ -589,6 +597,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float* stg = sh.stg[wave];
   const float alpha = F8 ? g.alpha * *g.sa * *g.sb : g.alpha;
+  float amx = 0.f;  // max |C| of this lane's stores (g.amax)
 
   // Forward forms (K-contiguous B) defer their epilogue; the dgrad forms and the
   // two-residual epilogue keep the in-line one (the deferred accumulator spills them).
@@ -660,6 +669,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += q.y[u][e];
       }
+      if (g.amax && ok) amx = ps_amax8(amx, v, g.out_dt);
       if (ok) {
         if (g.out_dt == LTHM_F32) {
           float* o = reinterpret_cast<float*>(g.C) + row * g.ldc + col0;
@@ -844,6 +854,7 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += q.y[u][e];
         }
+        if (g.amax && ok) amx = ps_amax8(amx, v, g.out_dt);
         if (ok) {
           if (g.out_dt == LTHM_F32) {
             float* o = reinterpret_cast<float*>(g.C) + row * g.ldc + col0;
@@ -858,6 +869,10 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
       asm volatile("" ::: "memory");
     }
   }
+  }
+  if (g.amax) {
+    amx = wave_max(amx);
+    if (lane == 0) atomicMax(g.amax, __float_as_uint(amx));
   }
 }
 
@@ -1013,6 +1028,13 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   g.ws = (splits > 1) ? d->workspace : nullptr;
   g.sa = nullptr;
   g.sb = nullptr;
+  g.amax = reinterpret_cast<unsigned*>(d->amax_out);
+  // the kernels other than gemm_ps_k leave amax_out to a pass over C afterwards
+  LTHM_REQUIRE(!d->amax_out || (d->batch == 1 && d->ldc == d->N && (d->M * d->N) % 8 == 0 &&
+                                ((uintptr_t)d->C % 16) == 0));
+  auto amax_after = [&]() -> int {
+    return d->amax_out ? lthm_amax(d->C, d->out_dtype, d->M * d->N, d->amax_out, stream) : 0;
+  };
   g.fast_ok = ((uintptr_t)d->A % 16) == 0 && ((uintptr_t)d->B % 16) == 0 && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
               d->sA % 8 == 0 && d->sB % 8 == 0;
   if (splits > 1) {
@@ -1042,7 +1064,7 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
       const int64_t total = d->M * d->N;
       hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, gr, spl, 1);
       LTHM_CHECK_LAUNCH();
-      return 0;
+      return amax_after();
     }
   }
   const int per_xcd = lthm_cu_count() / 8;
@@ -1127,5 +1149,5 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, g, splits, d->batch);
     LTHM_CHECK_LAUNCH();
   }
-  return 0;
+  return amax_after();
 }

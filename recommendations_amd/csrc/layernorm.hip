@@ -131,7 +131,7 @@ template <int NK, typename TY>
 __global__ __launch_bounds__(256) void ln_fwd_v4_k(const float* __restrict__ x, int64_t M, int D,
                                                    const float* __restrict__ w, const float* __restrict__ b,
                                                    TY* __restrict__ y, float* __restrict__ mean,
-                                                   float* __restrict__ rstd, float eps) {
+                                                   float* __restrict__ rstd, float eps, unsigned* __restrict__ amax) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void ln_fwd_v4_k(const float* __restrict__ x, 
       if (b) ld4(b + c, bv[k]);
     }
   }
+  float amx = 0.f;  // max |y| of this lane's stores, as stored (amax)
   for (int64_t r = wave; r < M; r += nw) {
     const float* xr = x + r * D;
     float v[NK][4];
@@ -181,12 +182,19 @@ __global__ __launch_bounds__(256) void ln_fwd_v4_k(const float* __restrict__ x, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
         store_vec<TY, 4>(y + r * D + c, o);
+        if (amax)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) amx = fmaxf(amx, fabsf(sizeof(TY) == 2 ? bf2f(f2bf(o[i])) : o[i]));
       }
     }
     if (lane == 0) {
       mean[r] = mu;
       rstd[r] = rs;
     }
+  }
+  if (amax) {
+    amx = wave_max(amx);
+    if (lane == 0) atomicMax(amax, __float_as_uint(amx));
   }
 }
 
@@ -301,8 +309,8 @@ static int ln_bwd_launch(const void* dy, int dydt, const float* x, int64_t M, in
 
 using namespace lthm;
 
-extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y,
-                                  int32_t y_dtype, float* mean, float* rstd, void* stream) {
+static int ln_fwd(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y, int32_t y_dtype,
+                  float* mean, float* rstd, unsigned* amax, void* stream) {
   LTHM_REQUIRE(M >= 0 && D > 0 && D <= 1024 && w != nullptr);
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -312,10 +320,10 @@ extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const fl
     if (D <= 256 * NK) {                                                                                       \
       if (y_dtype == LTHM_BF16)                                                                                \
         hipLaunchKernelGGL((ln_fwd_v4_k<NK, bf16_t>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (bf16_t*)y,   \
-                           mean, rstd, 1e-5f);                                                                 \
+                           mean, rstd, 1e-5f, amax);                                                                 \
       else                                                                                                     \
         hipLaunchKernelGGL((ln_fwd_v4_k<NK, float>), dim3(grid), dim3(256), 0, s, x, M, D, w, b, (float*)y,     \
-                           mean, rstd, 1e-5f);                                                                 \
+                           mean, rstd, 1e-5f, amax);                                                                 \
       LTHM_CHECK_LAUNCH();                                                                                     \
       return 0;                                                                                                \
     }
@@ -324,12 +332,28 @@ extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const fl
     LTHM_LN_FWD_V4(4)
 #undef LTHM_LN_FWD_V4
   }
+  // D % 4 != 0: the scalar kernel, then amax in a pass over y
+  LTHM_REQUIRE(!amax || (M * D) % 8 == 0);
   const int npl = (D + 63) / 64;
-  if (npl <= 1) return ln_fwd_launch<1>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
-  if (npl <= 2) return ln_fwd_launch<2>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
-  if (npl <= 4) return ln_fwd_launch<4>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
-  if (npl <= 8) return ln_fwd_launch<8>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
-  return ln_fwd_launch<16>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  int rc;
+  if (npl <= 1) rc = ln_fwd_launch<1>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  else if (npl <= 2) rc = ln_fwd_launch<2>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  else if (npl <= 4) rc = ln_fwd_launch<4>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  else if (npl <= 8) rc = ln_fwd_launch<8>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  else rc = ln_fwd_launch<16>(x, M, D, w, b, y, y_dtype, mean, rstd, s);
+  if (rc || !amax) return rc;
+  return lthm_amax(y, y_dtype, M * D, reinterpret_cast<int32_t*>(amax), stream);
+}
+
+extern "C" int lthm_layernorm_fwd(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y,
+                                  int32_t y_dtype, float* mean, float* rstd, void* stream) {
+  return ln_fwd(x, M, D, w, b, y, y_dtype, mean, rstd, nullptr, stream);
+}
+
+extern "C" int lthm_layernorm_fwd_amax(const float* x, int64_t M, int32_t D, const float* w, const float* b, void* y,
+                                       int32_t y_dtype, float* mean, float* rstd, int32_t* amax, void* stream) {
+  LTHM_REQUIRE(amax != nullptr);
+  return ln_fwd(x, M, D, w, b, y, y_dtype, mean, rstd, reinterpret_cast<unsigned*>(amax), stream);
 }
 
 extern "C" int lthm_layernorm_bwd_blocks(int64_t M) { return grid_for(M, 4, 256 * 4); }

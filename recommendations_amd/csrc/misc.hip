@@ -596,6 +596,39 @@ extern "C" int lthm_quantize_fp8(const void* x, int32_t dtype, int64_t n, uint8_
   return 0;
 }
 
+extern "C" int lthm_amax(const void* x, int32_t dtype, int64_t n, int32_t* amax, void* stream) {
+  LTHM_REQUIRE(n >= 0 && n % 8 == 0 && amax && ((uintptr_t)x % 16) == 0);
+  LTHM_REQUIRE(dtype == LTHM_F32 || dtype == LTHM_BF16);
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(n8, 256, 256 * 8);
+  if (dtype == LTHM_BF16)
+    hipLaunchKernelGGL((amax_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, n8, (unsigned*)amax);
+  else
+    hipLaunchKernelGGL((amax_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, n8, (unsigned*)amax);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_quantize_fp8_amax(const void* x, int32_t dtype, int64_t n, const int32_t* amax, uint8_t* q,
+                                      float* scale, void* stream) {
+  LTHM_REQUIRE(n >= 0 && n % 8 == 0 && q && scale && amax);
+  LTHM_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
+  LTHM_REQUIRE(dtype == LTHM_F32 || dtype == LTHM_BF16);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n8 = n / 8;
+  const int grid = grid_for(n8 > 0 ? n8 : 1, 256, 256 * 8);
+  if (dtype == LTHM_BF16)
+    hipLaunchKernelGGL((quant_fp8_k<bf16_t>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, n8,
+                       (const unsigned*)amax, q, scale);
+  else
+    hipLaunchKernelGGL((quant_fp8_k<float>), dim3(grid), dim3(256), 0, s, (const float*)x, n8,
+                       (const unsigned*)amax, q, scale);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------- MoELinear gates / expert scaling
 namespace lthm {
 __global__ __launch_bounds__(256) void moe_gate_fwd_k(const float* __restrict__ logits, int64_t M, int E, float scale,

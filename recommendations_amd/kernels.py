@@ -303,9 +303,10 @@ def _workspace(dev, nbytes: int) -> torch.Tensor:
 
 def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, out=None,
          out_dtype=torch.bfloat16, ldc=None, alpha=1.0, bias=None, act=ACT_NONE, aux=None, aux_out=None,
-         res1=None, res2=None, batch=1, sA=0, sB=0, sC=0, splits=1, a_scale=None, b_scale=None):
+         res1=None, res2=None, batch=1, sA=0, sB=0, sC=0, splits=1, a_scale=None, b_scale=None, amax_out=None):
     """C = epi(alpha * A.B) on the MFMA GEMM kernel (include/lthm.h lthm_gemm).  uint8
-    A / B are fp8 e4m3 bytes with per-tensor device scales a_scale / b_scale."""
+    A / B are fp8 e4m3 bytes with per-tensor device scales a_scale / b_scale; amax_out
+    (int32 [1] device word) receives the running max of |C| as f32 bits."""
     from ._lib import STRUCTS
     require_gpu(A, B)
     dev = A.device
@@ -345,6 +346,9 @@ def gemm(A, B, M, N, K, *, a_kcontig=True, b_kcontig=True, lda=None, ldb=None, o
         ws = _workspace(dev, splits * batch * M * N * 4)
         d.workspace, d.workspace_bytes = ptr(ws), ws.numel() * 4
     d.splits = splits
+    if amax_out is not None:
+        _check(amax_out.dtype == torch.int32 and amax_out.is_cuda, "amax_out is an int32 device word")
+        d.amax_out = ptr(amax_out)
     fp8 = A.dtype == torch.uint8
     if fp8:
         _check(B.dtype == torch.uint8 and a_scale is not None and b_scale is not None,
@@ -383,27 +387,43 @@ class gemm_tag:
 FP8_E4M3 = 2
 
 
-def quantize_fp8(x):
+def quantize_fp8(x, amax=None):
     """Per-tensor e4m3 quantisation (include/lthm.h lthm_quantize_fp8): -> (q uint8 of
-    x's shape, scale f32 [1] on the device) with x = q * scale up to e4m3 rounding."""
+    x's shape, scale f32 [1] on the device) with x = q * scale up to e4m3 rounding.
+    amax: the int32 [1] word a producer already reduced max |x| into (layernorm_fwd /
+    gemm amax_out / amax_): x is then read once (lthm_quantize_fp8_amax)."""
     require_gpu(x)
     n = x.numel()
     _check(n % 8 == 0, "quantize_fp8 takes n % 8 == 0")
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     scale = torch.empty(1, dtype=torch.float32, device=x.device)
+    if amax is not None:
+        _check(amax.dtype == torch.int32 and amax.is_cuda, "amax is an int32 device word")
+        call("lthm_quantize_fp8_amax", ptr(x), dcode(x), n, ptr(amax), ptr(q), ptr(scale), stream(),
+             _key="quantize_fp8", _work=n * (x.element_size() + 1), _unit="byte")
+        return q, scale
     work = torch.empty(1, dtype=torch.int32, device=x.device)
     call("lthm_quantize_fp8", ptr(x), dcode(x), n, ptr(q), ptr(scale), ptr(work), stream(), _key="quantize_fp8",
          _work=n * (x.element_size() * 2 + 1), _unit="byte")
     return q, scale
 
 
+def amax_(x, amax):
+    """amax (int32 [1] device word) = max(amax, max |x|) as f32 bits (lthm_amax)."""
+    require_gpu(x, amax)
+    _check(x.numel() % 8 == 0 and amax.dtype == torch.int32, "amax_ takes n % 8 == 0 and an int32 word")
+    call("lthm_amax", ptr(x), dcode(x), x.numel(), ptr(amax), stream(), _key="amax",
+         _work=x.numel() * x.element_size(), _unit="byte")
+    return amax
+
+
 def linear_fwd_fp8(xq, xs, wq, ws, bias=None, act=ACT_NONE, aux_out=None, res1=None, res2=None,
-                   out_dtype=torch.bfloat16):
+                   out_dtype=torch.bfloat16, amax_out=None):
     """y = act(xs ws (xq wq^T) + b) (+ res1 + res2) on the fp8 MFMA: xq [M, K], wq [N, K] e4m3 bytes."""
     M, K_ = xq.shape
     N = wq.shape[0]
     return gemm(xq, wq, M, N, K_, bias=bias, act=act, aux_out=aux_out, res1=res1, res2=res2, out_dtype=out_dtype,
-                a_scale=xs, b_scale=ws)
+                a_scale=xs, b_scale=ws, amax_out=amax_out)
 
 
 def _splits_for(M: int, N: int, K: int) -> int:
@@ -476,7 +496,9 @@ def mlp_fwd(x2d, w1_b, b1, w2t_b, b2, res1=None, res2=None):
 
 
 # ----------------------------------------------------------------- LayerNorm
-def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
+def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
+    """amax: optional int32 [1] device word (zeroed by the caller) that receives the
+    running max of |y| as f32 bits -- the fp8 quantisation's reduction, fused."""
     require_gpu(x2d, w)
     M, D = x2d.shape
     _need(w, D, "ln weight")
@@ -484,7 +506,12 @@ def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16):
     y = torch.empty((M, D), dtype=y_dtype, device=x2d.device)
     mean = torch.empty(M, dtype=torch.float32, device=x2d.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x2d.device)
-    call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream())
+    if amax is not None:
+        _check(amax.dtype == torch.int32 and amax.is_cuda, "amax is an int32 device word")
+        call("lthm_layernorm_fwd_amax", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd),
+             ptr(amax), stream())
+    else:
+        call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream())
     return y, mean, rstd
 
 

@@ -45,6 +45,54 @@ def test_quantize_fp8_bit_exact(dev, dtype):
     assert torch.equal(q.cpu(), exp)
 
 
+def _amax_word(t):
+    return int(t.float().abs().max().view(torch.int32))
+
+
+@pytest.mark.parametrize("D,ydt", [(512, torch.bfloat16), (256, torch.float32), (70, torch.bfloat16)])
+def test_layernorm_amax_fused(dev, D, ydt):
+    """layernorm_fwd(amax=) folds max |y| (of the stored y) into the word, and
+    quantize_fp8(amax=) then equals the two-pass quantize_fp8 bit for bit."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(D)
+    M = 3001 if D != 70 else 4000
+    x = (torch.randn(M, D, generator=g) * 2 + 0.5).to(dev)
+    w = (1 + 0.3 * torch.randn(D, generator=g)).to(dev)
+    b = (0.2 * torch.randn(D, generator=g)).to(dev)
+    am = torch.zeros(1, dtype=torch.int32, device=dev)
+    y, mu, rs = K.layernorm_fwd(x, w, b, y_dtype=ydt, amax=am)
+    y0, _, _ = K.layernorm_fwd(x, w, b, y_dtype=ydt)
+    assert torch.equal(y, y0)
+    assert int(am.cpu()) == _amax_word(y0.cpu())
+    q, s = K.quantize_fp8(y, amax=am)
+    q0, s0 = K.quantize_fp8(y0)
+    assert torch.equal(q.cpu(), q0.cpu()) and float(s.cpu()) == float(s0.cpu())
+
+
+@pytest.mark.parametrize("M,N,K,act,odt", [(40000, 2048, 512, 5, torch.bfloat16), (5000, 512, 512, 0, torch.float32),
+                                           (333, 256, 128, 1, torch.bfloat16)])
+def test_fp8_gemm_amax_out(dev, M, N, K, act, odt):
+    """The GEMM epilogue's amax_out equals max |C| of the stored C (fp8 GEMM, persistent
+    kernel; and the bf16 one-tile kernel's pass over C for a small M)."""
+    from recommendations_amd import kernels as K_
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if act else None
+    am = torch.zeros(1, dtype=torch.int32, device=dev)
+    xq, xs = K_.quantize_fp8(x)
+    wq, ws = K_.quantize_fp8(w)
+    out = K_.linear_fwd_fp8(xq, xs, wq, ws, bias, act=act, aux_out=pre, out_dtype=odt, amax_out=am)
+    assert int(am.cpu()) == _amax_word(out.cpu())
+    am2 = torch.zeros(1, dtype=torch.int32, device=dev)
+    out2 = K_.gemm(x, w, M, N, K, bias=bias, act=act, aux_out=pre, out_dtype=odt, amax_out=am2)
+    assert int(am2.cpu()) == _amax_word(out2.cpu())
+    am3 = torch.zeros(1, dtype=torch.int32, device=dev)
+    K_.amax_(out2, am3)
+    assert int(am3.cpu()) == int(am2.cpu())
+
+
 @pytest.mark.parametrize("M,N,K,act,res", [(40000, 1536, 512, 0, 0), (333, 2048, 512, 1, 0),
                                            (20000, 512, 2048, 0, 2), (5000, 512, 512, 0, 1),
                                            (70001, 768, 256, 2, 0)])
