@@ -35,8 +35,8 @@ PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call 
     "cl_bwd_k": ["cl_bwd_k<", "cl_bwd32_k<", "cl_shift_k", "cl_dyscale_k<"],
     "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_fr32_k", "cl_used_k", "cl_stats_k", "cl_rowstats_k", "cl_wscale_k"],
     "attn_bwd_k": ["attn_bwd_mfma_k<", "attn_bwd32_k<", "attn_bwd_rows_win_k<", "attn_bwd_cols_win_k<",
-                   "attn_delta_k<"],
-    "attn_fwd_k": ["attn_fwd_mfma_k<", "attn_fwd_win_k<"],
+                   "attn_delta_k<", "attn_bwd32l_k<"],
+    "attn_fwd_k": ["attn_fwd_mfma_k<", "attn_fwd_win_k<", "attn_fwd32_k<"],
     "gemm_k<1,1>": ["gemm_k<true, true>", "gemm_ps_k<true, "],
     "gemm_k<1,0>": ["gemm_k<true, false>", "gemm_ps_k<false, "],
     "gemm_k<0,0>": ["gemm_k<false, false>", "gemm_wg_k", "splitk_reduce_k"],
