@@ -141,8 +141,14 @@ def load_torch_ops() -> None:
         raise RuntimeError(
             f"{TORCH_OPS_PATH} not found: the TORCH_LIBRARY(lthm) op layer is not built "
             "(run `python -c 'import __graft_entry__ as g; g.build()'`).")
-    load()  # liblthm_hip.so first (RTLD_GLOBAL), the op library links against it
+    lib = load()  # liblthm_hip.so first (RTLD_GLOBAL), the op library links against it
     torch.ops.load_library(TORCH_OPS_PATH)
+    # the op library fills the descriptors of include/lthm.h: a stale build (older header)
+    # would hand the kernels a shorter struct, so refuse it
+    built, want = int(torch.ops.lthm.built_abi_version()), int(lib.lthm_abi_version())
+    if built != want:
+        raise RuntimeError(f"{TORCH_OPS_PATH} was built against ABI {built}, liblthm_hip.so is ABI {want}: "
+                           "rebuild it (`python recommendations_amd/csrc/torch_ops/build.py`)")
     _TORCH_OPS = True
 
 

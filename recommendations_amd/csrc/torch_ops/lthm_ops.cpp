@@ -408,11 +408,14 @@ Tensor item_artifact_cuda(const Tensor& ids_, const Tensor& W, int64_t K, int64_
 }
 
 int64_t abi_version() { return lthm_abi_version(); }
+// the include/lthm.h this op library was compiled against (descriptor layouts)
+int64_t built_abi_version() { return LTHM_ABI_VERSION; }
 
 }  // namespace
 
 TORCH_LIBRARY(lthm, m) {
   m.def("abi_version() -> int", &abi_version);
+  m.def("built_abi_version() -> int", &built_abi_version);
   m.def("kshift(Tensor ids, Tensor weight, int P, int K, int mode, int F=1, ScalarType? out_dtype=None) -> Tensor");
   m.def("kshift_rows(Tensor ids, int P, int K) -> Tensor");
   m.def("gather_pool(Tensor rows, Tensor weight, int mode, ScalarType out_dtype=float) -> Tensor");
