@@ -141,7 +141,7 @@ def build(cfgd, dev):
     cfg = lthm_config(T=cfgd["T"], d=cfgd["d"], n_layers=cfgd["L"], n_head=cfgd["H"], cat_features=cfgd["n_cat"],
                       cat_vocab=cfgd["cat_vocab"], item_vocab=cfgd["item_vocab"],
                       item_table_sharded=cfgd.get("item_table_sharded", False), fp8=cfgd.get("fp8", False),
-                      train_mini_batch_size=cfgd.get("mbs", 32))
+                      train_mini_batch_size=cfgd.get("mbs", 32), gradient_checkpointing=cfgd.get("ckpt", False))
     model = LTHMModelBuilder(None, cfg).build().to(dev)
     return cfg, model
 
@@ -278,6 +278,10 @@ def main():
                     help="C3 at N > 1: look the row-sharded item table up inside each step instead of one "
                          "step ahead on a side stream")
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--checkpointing", action="store_true",
+                    help="recompute block activations in the backward (the reference yaml's "
+                         "enable_gradient_checkpointing, a memory knob; off by default: the "
+                         "activations fit in 288 GB of HBM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -314,6 +318,7 @@ def main():
     cfgd = dict(CONFIGS[args.config])
     if args.batch:
         cfgd["B"] = args.batch
+    cfgd["ckpt"] = bool(args.checkpointing)
     cfg, model = build(cfgd, dev)
     B = cfgd["B"]
     ranker = cfgd.get("kind") == "ranker"
@@ -422,6 +427,7 @@ def main():
                                 + (", fp8 e4m3 forward encoder GEMMs" if cfgd.get("fp8") else "")
                                 + (f", {cfgd['mbs']}-sequence loss mini-batches" if cfgd.get("mbs") else "")),
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
+                   "activation_checkpointing": cfgd["ckpt"],
                    "item_lookup": ("one step ahead on a side stream (Encoder.prefetch after the forward), "
                                    "inside the timed loop"
                                    if pipelined else "inline"),

@@ -18,6 +18,7 @@ import math
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
+import torch.utils.checkpoint
 import torch.nn as nn
 
 from ... import kernels as K
@@ -538,12 +539,22 @@ class TransformerBlock(nn.Module):
             return TransformerBlockFn.apply(x.float(), *args, self.attn.n_head, self.is_causal,
                                             double_residual, self.fp8_gemm, drop, attn_mask, infer)
 
+    def _checkpointing(self) -> bool:
+        return bool(self.enable_gradient_checkpointing and self.training and torch.is_grad_enabled())
+
     def forward(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        # Activation checkpointing (:375-380) changes memory, not numbers: at 288 GB HBM
-        # the fused op keeps its bf16 activations instead of recomputing them.
-        if not self.is_sparse:
-            return self._fused(x, False, attn_mask)
-        return self._sparse_forward(x, attn_mask)
+        """:374-380: with enable_gradient_checkpointing in training the block's activations
+        are dropped after the forward and recomputed in the backward (non-reentrant
+        checkpoint; the CPU generator the dropout seeds come from is restored for the
+        recompute, so the masks match)."""
+        fn = self._fused_single if not self.is_sparse else self._sparse_forward
+        if self._checkpointing():
+            return torch.utils.checkpoint.checkpoint(fn, x, attn_mask, use_reentrant=False,
+                                                     preserve_rng_state=True)
+        return fn(x, attn_mask)
+
+    def _fused_single(self, x: torch.Tensor, attn_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self._fused(x, False, attn_mask)
 
     def _null(self, x):
         from ...models.lthm.sequence.query_tower import LinearFn
@@ -571,7 +582,11 @@ class TransformerBlock(nn.Module):
         return x_final
 
     def forward_double_residual(self, x: torch.Tensor) -> torch.Tensor:
-        """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137)."""
+        """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137); checkpointed
+        like forward (the reference checkpoints block(x) and adds x outside)."""
+        if self._checkpointing():
+            return torch.utils.checkpoint.checkpoint(self._fused, x, True, use_reentrant=False,
+                                                     preserve_rng_state=True)
         return self._fused(x, True)
 
 

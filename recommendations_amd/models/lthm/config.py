@@ -115,12 +115,13 @@ class LTHMModelConfig(BaseModel):
 
 def lthm_config(T: int, d: int, n_layers: int, n_head: int, cat_features: int = 0, cat_vocab: int = 1_000_000,
                 item_vocab: int = 1_000_000, out_emb_dim: Optional[int] = None, fp8: bool = False,
-                **kw) -> LTHMModelConfig:
+                gradient_checkpointing: bool = True, **kw) -> LTHMModelConfig:
     """Convenience constructor for the BASELINE configurations (C1-C5; fp8 = C5's
-    fp8 encoder GEMMs)."""
+    fp8 encoder GEMMs). gradient_checkpointing follows the reference yaml
+    (hydra-configs/model/lthm.yaml:53, on): activations recomputed in the backward."""
     tc = EncoderTransformerConfig(
         rotator_config={"ff_mult": 4}, is_causal=True, num_layers=n_layers, dropout=0.0,
-        enable_gradient_checkpointing=True, fp8_gemm=fp8,
+        enable_gradient_checkpointing=gradient_checkpointing, fp8_gemm=fp8,
         attn_config=SelfAttentionConfig(attn_dropout=0.0, bias=False, dropout=0.0, n_head=n_head, n_embd=d,
                                         attn_type="multi_query", pos_bias={"context_window": T + 1}))
     pt = ProductTowerConfig(out_emb_dim=out_emb_dim or d,

@@ -56,3 +56,49 @@ def test_overlapped_allreduce_world1(dev, rccl1):
     g = lin.weight.grad.clone()
     ar()
     assert torch.equal(g, lin.weight.grad)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_full_step_world2_matches_world1(dev, tmp_path):
+    """The whole data-parallel training step at world 2 (both ranks on this box's one GPU,
+    gloo over CUDA tensors; tests/dist_step_worker.py): table-sharded categorical tables
+    (all_to_all of ids, pooled rows and gradients), the row-sharded item table (device
+    routing, count exchange, two all_to_alls), the bucketed dense all-reduce launched from
+    the backward's gradient hooks, sparse row-wise and dense AdamW, activation
+    checkpointing.  Each rank holds half of a 64-sequence batch (one loss mini-batch), so
+    the rank-averaged loss and every update equal a world-1 step on the whole batch (two
+    mini-batches, loss averaged over them): losses of three steps to 1e-4, dense weights
+    and the categorical tables after them to 1e-3 of the update."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    worker = os.path.join(root, "tests", "dist_step_worker.py")
+    prefix = str(tmp_path / "step")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    steps = "3"
+    subprocess.run([sys.executable, worker, prefix, steps], env=env, check=True, timeout=300)
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), worker, prefix, steps],
+                   env=env, check=True, timeout=300)
+    w1 = torch.load(prefix + "_w1_r0.pt", weights_only=True)
+    w2 = [torch.load(prefix + f"_w2_r{r}.pt", weights_only=True) for r in range(2)]
+    torch.testing.assert_close(w2[0]["losses"], w1["losses"], rtol=1e-4, atol=0)
+    assert torch.equal(w2[0]["losses"], w2[1]["losses"])
+    for k, v in w1.items():
+        if not k.startswith("dense."):
+            continue
+        assert torch.equal(w2[0][k], w2[1][k]), f"replicas diverged: {k}"
+        err = float((w2[0][k] - v).abs().max())
+        assert err <= 1e-3 * max(float(v.abs().max()), 1e-2), (k, err)
+    P = w1["tables"].shape[0] // 2
+    for r in range(2):
+        f0 = int(w2[r]["tables_f0"])
+        ref_rows = w1["tables"][f0 * P:f0 * P + w2[r]["tables"].shape[0]]
+        err = float((w2[r]["tables"] - ref_rows).abs().max())
+        assert err <= 1e-3, (r, err)

@@ -468,6 +468,40 @@ def test_block_dropout_vs_oracle(dev, p):
     check(f"dropout {p} eval fwd", relerr(y0.cpu() - x, yr0 - x), 1e-3)
 
 
+@pytest.mark.parametrize("dbl", [False, True])
+def test_block_gradient_checkpointing(dev, dbl):
+    """enable_gradient_checkpointing (commons/transformers/layers.py:374-380): in training
+    the block's saved activations are recomputed in the backward. With dropout on (seeds
+    drawn from the CPU generator, restored for the recompute) outputs and gradients equal
+    the non-checkpointed block's (outputs bit for bit), and the activations kept between forward and
+    backward shrink to the block input."""
+    B, T, d, H = 8, 129, 256, 4
+    blk, sd, x, dy = _rand_block(dev, B, T, d, H, seed=5, dropout=0.1)
+    blk.train()
+    res = {}
+    for ck in (False, True):
+        blk.enable_gradient_checkpointing = ck
+        blk.zero_grad(set_to_none=True)
+        xd = x.to(dev).requires_grad_(True)
+        torch.cuda.synchronize()
+        m0 = torch.cuda.memory_allocated(dev)
+        torch.manual_seed(123)
+        y = blk.forward_double_residual(xd) if dbl else blk(xd)
+        torch.cuda.synchronize()
+        kept = torch.cuda.memory_allocated(dev) - m0 - y.numel() * y.element_size()
+        torch.manual_seed(999)  # the recompute must not depend on the generator's state here
+        y.backward(dy.to(dev))
+        res[ck] = (y.detach().cpu(), xd.grad.cpu(), {n: p.grad.cpu() for n, p in blk.named_parameters()}, kept)
+    (y0, dx0, g0, kept0), (y1, dx1, g1, kept1) = res[False], res[True]
+    assert torch.equal(y0, y1)
+    # same kernels on the same operands; the bias gradient's LDS float atomics may sum
+    # in another order, so the gradients are held to 1e-5 rather than bit equality
+    check("ckpt dx", relerr(dx1, dx0), 1e-5)
+    for n in g0:
+        check(f"ckpt d{n}", relerr(g1[n], g0[n]), 1e-5)
+    assert kept1 < kept0 / 4, (kept0, kept1)
+
+
 @pytest.mark.parametrize("idx", [0, 1])
 def test_transformer_block_attn_mask_golden(dev, idx):
     """TransformerBlock.forward(x, attn_mask) with a general additive [B, 1, T, T] mask
