@@ -56,6 +56,7 @@ def main():
         full[k][0::B_RANK] = longest[k]
     lo, hi = (0, 2 * B_RANK) if world == 1 else (rank * B_RANK, (rank + 1) * B_RANK)
     batch = {k: v[lo:hi].contiguous().to(dev) for k, v in full.items()}
+    init = {n: p.detach().float().cpu().clone() for n, p in dense}
     losses = []
     for _ in range(steps):
         out = model(batch)
@@ -75,7 +76,7 @@ def main():
         print(f"world {world} losses {losses}", flush=True)
     res = {"losses": torch.tensor(losses, dtype=torch.float64)}
     for n, p in dense:
-        res["dense." + n] = p.detach().float().cpu()
+        res["dense." + n] = p.detach().float().cpu() - init[n]  # the update over the steps
     tabs = enc.user_context.tables
     w = tabs.weight.detach().float().cpu()
     if world > 1:  # this rank's tables [f0, f1) of the full stack
