@@ -27,6 +27,9 @@ def main():
     dev = torch.device("cuda")
     M = 4096 * 129
     shapes = [("qkv", M, 768, 256), ("proj", M, 256, 256), ("fc", M, 1024, 256), ("fc2", M, 256, 1024)]
+    if os.environ.get("GEMM_BENCH_CFG") == "c5":  # C5: B 1024 x T' 513, d 512, MQA (q 512 + kv 128)
+        M = 1024 * 513
+        shapes = [("qkv", M, 640, 512), ("proj", M, 512, 512), ("fc", M, 2048, 512), ("fc2", M, 512, 2048)]
     if os.environ.get("GEMM_BENCH_SQUARE"):
         shapes.append(("sq4096", 4096, 4096, 4096))
     for name, m, n, k in shapes:
@@ -38,12 +41,16 @@ def main():
         t2 = timeit(lambda: torch.matmul(a, w.T))
         dy = torch.randn(m, n, device=dev).to(torch.bfloat16)
         t3 = timeit(lambda: K.linear_dgrad(dy, w))
+        # the same dgrad product with a K-contiguous B (W^T materialised): the forward kernel form
+        wt = w.t().contiguous()
+        t3t = timeit(lambda: K.linear_fwd(dy, wt))
         t4 = timeit(lambda: K.linear_wgrad(dy, a), iters=5)
         t5 = timeit(lambda: torch.matmul(dy.T, a), iters=5)
         byts = 2.0 * (m * k + n * k + m * n)  # bf16 A + W + C, each once
         print(f"{name:7s} M={m} N={n} K={k}: fwd {t0:.3f} ms ({fl / t0 / 1e9:.0f} TF, "
               f"{byts / t0 / 1e6:.0f} GB/s)  +gelu {t1:.3f}  "
-              f"hipblaslt {t2:.3f} ({fl / t2 / 1e9:.0f} TF) | dgrad {t3:.3f} ({fl / t3 / 1e9:.0f} TF) | "
+              f"hipblaslt {t2:.3f} ({fl / t2 / 1e9:.0f} TF) | dgrad {t3:.3f} ({fl / t3 / 1e9:.0f} TF) "
+              f"via W^T {t3t:.3f} ({fl / t3t / 1e9:.0f} TF) | "
               f"wgrad {t4:.3f} ({fl / t4 / 1e9:.0f} TF) hipblaslt {t5:.3f}", flush=True)
 
 
