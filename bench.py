@@ -511,7 +511,14 @@ def main():
         else:
             peak = pk_mfma
             ach, unit, bound = per_launch / avg_s / 1e12, "TFLOP/s", "mfma"
-        traffic = pmc_traffic(dom, s["calls"] / args.steps)
+        if ":" in dom and prof is not None:
+            # a tagged GEMM form (enc:...): the counters see the kernel, not the tag, so the
+            # traffic is the form's average over all its launches (tagged or not)
+            base = dom.split(":")[-1]
+            fam = sum(v["calls"] for k, v in prof.items() if k.split(":")[-1] == base) / PROF_STEPS
+            traffic = pmc_traffic(base, fam)
+        else:
+            traffic = pmc_traffic(dom, s["calls"] / args.steps)
         res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                            "frac": round(ach / peak, 4),
                            "traffic": round(traffic) if traffic is not None else None,

@@ -83,6 +83,20 @@ __global__ __launch_bounds__(256) void adagrad_k(float* __restrict__ p, float* _
   }
 }
 
+// per-element row-wise updates, shared by the per-element and the 16-byte kernels so both
+// round identically
+__device__ __forceinline__ float adamw_elem(float p, float g, float& m, float& v, float lr, float b1, float b2,
+                                           float eps, float wd, float bc1, float bc2_sqrt) {
+  p = p * (1.f - lr * wd);
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  return p - (lr / bc1) * m / (sqrtf(v) / bc2_sqrt + eps);
+}
+__device__ __forceinline__ float adagrad_elem(float p, float g, float& s, float clr, float eps) {
+  s = s + g * g;
+  return p - clr * g / (sqrtf(s) + eps);
+}
+
 // rows[0 .. *count) touched rows of a [R, D] table; the gradient row is consumed and re-zeroed,
 // the row's touched flag reset.  One wave per row.
 __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
@@ -100,19 +114,85 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
     const int64_t r = rows[k];
     for (int d = d0; d < D; d += 64) {
       const int64_t i = r * D + d;
-      const float gi = g[i];
-      float pi = p[i] * (1.f - lr * wd);
-      const float mi = b1 * m[i] + (1.f - b1) * gi;
-      const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+      float mi = m[i], vi = v[i];
+      const float pi = adamw_elem(p[i], g[i], mi, vi, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
       m[i] = mi;
       v[i] = vi;
-      pi = pi - (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
     }
     if (d0 == 0) flags[r] = 0;
   }
+}
+
+// 16-byte form of sparse_adamw_k / sparse_adagrad_k for D % 4 == 0 with D / 4 dividing 64:
+// D / 4 lanes per row, 256 / D rows per wave (C4's D = 32: 8 rows, each array's row one
+// 128-B access by 8 lanes), the next row index loaded before the current row's update,
+// so a wave keeps several rows of every array in flight (the row-per-wave form is
+// latency-bound: one row's loads at a time behind the index load).  Same per-element
+// arithmetic, bit-identical results.
+__device__ __forceinline__ void ld4f(const float* p, float (&v)[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+__device__ __forceinline__ void st4f(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ void st4bf(bf16_t* p, const float (&v)[4]) {
+  u32x2 w;
+  w[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  w[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<u32x2*>(p) = w;
+}
+
+template <bool ADAM>
+__global__ __launch_bounds__(256) void sparse_opt_v4_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
+                                                       int64_t max_rows, int D, float* __restrict__ p,
+                                                       float* __restrict__ g, float* __restrict__ m,
+                                                       float* __restrict__ v, int32_t* __restrict__ flags, float lr,
+                                                       float b1, float b2, float eps, float wd, float bc1,
+                                                       float bc2_sqrt, bf16_t* __restrict__ shadow) {
+  const int64_t cnt = min(*count, max_rows);
+  const int lane = threadIdx.x & 63;
+  const int L = D >> 2, rpw = 64 / L;
+  const int sub = lane / L, d0 = (lane - sub * L) * 4;
+  const int64_t stride = (int64_t)gridDim.x * 4 * rpw;
+  int64_t k = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + sub;
+  int64_t r = k < cnt ? rows[k] : 0;
+  for (; k < cnt; k += stride) {
+    const int64_t kn = k + stride;
+    const int64_t rn = kn < cnt ? rows[kn] : 0;  // the next row index in flight
+    const int64_t i = r * D + d0;
+    float gi[4], pi[4], mi[4];
+    ld4f(g + i, gi);
+    ld4f(p + i, pi);
+    ld4f(m + i, mi);  // ADAM: first moment; Adagrad: the state sum
+    if constexpr (ADAM) {
+      float vi[4];
+      ld4f(v + i, vi);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pi[e] = adamw_elem(pi[e], gi[e], mi[e], vi[e], lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+      st4f(v + i, vi);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pi[e] = adagrad_elem(pi[e], gi[e], mi[e], lr, eps);
+    }
+    st4f(m + i, mi);
+    st4f(p + i, pi);
+    if (shadow) st4bf(shadow + i, pi);
+    const float z[4] = {0.f, 0.f, 0.f, 0.f};
+    st4f(g + i, z);
+    if (d0 == 0) flags[r] = 0;
+    r = rn;
+  }
+}
+
+static bool sparse_v4_ok(int D, const void* a, const void* b, const void* c, const void* d, const void* sh) {
+  if (D % 4 != 0 || D > 256 || 64 % (D / 4) != 0) return false;
+  for (const void* q : {a, b, c, d})
+    if (q && ((uintptr_t)q % 16) != 0) return false;
+  return !sh || ((uintptr_t)sh % 8) == 0;
 }
 
 __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
@@ -128,10 +208,9 @@ __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restric
     const int64_t r = rows[k];
     for (int d = d0; d < D; d += 64) {
       const int64_t i = r * D + d;
-      const float gi = g[i];
-      const float si = s[i] + gi * gi;
+      float si = s[i];
+      const float pi = adagrad_elem(p[i], g[i], si, clr, eps);
       s[i] = si;
-      const float pi = p[i] - clr * gi / (sqrtf(si) + eps);
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
@@ -228,8 +307,15 @@ extern "C" int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int6
   if (max_rows == 0) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
-  hipLaunchKernelGGL(sparse_adamw_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
-                     p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+  if (sparse_v4_ok(D, p, g, m, v, bf16_shadow)) {
+    const int rpw = 256 / D;
+    hipLaunchKernelGGL(sparse_opt_v4_k<true>, dim3(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16)), dim3(256), 0,
+                       (hipStream_t)stream, rows, count, max_rows, D, p, g, m, v, flags, lr, beta1, beta2, eps,
+                       weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+  } else {
+    hipLaunchKernelGGL(sparse_adamw_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
+                       p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+  }
   LTHM_CHECK_LAUNCH();
   return 0;
 }
@@ -240,8 +326,15 @@ extern "C" int lthm_sparse_adagrad(const int64_t* rows, const int64_t* count, in
   LTHM_REQUIRE(D > 0 && step >= 1 && max_rows >= 0);
   if (max_rows == 0) return 0;
   const float clr = lr / (1.f + (float)(step - 1) * lr_decay);
-  hipLaunchKernelGGL(sparse_adagrad_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count,
-                     max_rows, D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow);
+  if (sparse_v4_ok(D, p, g, state_sum, nullptr, bf16_shadow)) {
+    const int rpw = 256 / D;
+    hipLaunchKernelGGL(sparse_opt_v4_k<false>, dim3(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16)), dim3(256), 0,
+                       (hipStream_t)stream, rows, count, max_rows, D, p, g, state_sum, nullptr, flags, clr, 0.f, 0.f,
+                       eps, 0.f, 1.f, 1.f, (bf16_t*)bf16_shadow);
+  } else {
+    hipLaunchKernelGGL(sparse_adagrad_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count,
+                       max_rows, D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow);
+  }
   LTHM_CHECK_LAUNCH();
   return 0;
 }

@@ -126,3 +126,74 @@ def test_block_reads_current_weights(dev, how):
         fresh.load_state_dict(blk.state_dict())
         want = fresh(x)
     assert torch.equal(got, want)
+
+
+def _misaligned(t):
+    """A copy of t whose storage starts 4 bytes past a 16-byte boundary (the per-element
+    kernel's path)."""
+    big = torch.empty(t.numel() + 1, dtype=t.dtype, device=t.device)
+    out = big[1:].view(t.shape)
+    out.copy_(t)
+    return out
+
+
+@pytest.mark.parametrize("D", [32, 64, 128, 16])
+@pytest.mark.parametrize("adam", [True, False])
+def test_sparse_row_optimizers_16b_form(dev, D, adam):
+    """lthm_sparse_adamw / lthm_sparse_adagrad in the 16-byte form (D / 4 lanes per row,
+    256 / D rows per wave) against the per-element form on the same touched rows
+    (misaligned copies take that one): p and the moments to 1 ulp, the bf16 shadow equal to
+    the rounded p, the gradient rows zeroed and the touched flags reset; untouched rows unchanged; and
+    against the row-wise update written in torch."""
+    from recommendations_amd import kernels as K
+    torch.manual_seed(D + adam)
+    R, n = 5000, 1733
+    rows = torch.randperm(R, device=dev)[:n].to(torch.int64)
+    cap = n + 64
+    rows_buf = torch.zeros(cap, dtype=torch.int64, device=dev)
+    rows_buf[:n] = rows
+    count = torch.tensor([n], dtype=torch.int64, device=dev)
+    p0 = torch.randn(R, D, device=dev)
+    g0 = torch.zeros(R, D, device=dev)
+    g0[rows] = torch.randn(n, D, device=dev)
+    m0 = torch.randn(R, D, device=dev).abs() if not adam else torch.randn(R, D, device=dev) * 0.1
+    v0 = torch.rand(R, D, device=dev) * 0.01
+    res = []
+    for mis in (False, True):
+        f = _misaligned if mis else (lambda t: t.clone())
+        p, g, m, v = f(p0), f(g0), f(m0), f(v0)
+        sh = torch.zeros(R, D, dtype=torch.bfloat16, device=dev)
+        sh = _misaligned(sh) if mis else sh
+        flags = torch.zeros(R, dtype=torch.int32, device=dev)
+        flags[rows] = 1
+        if adam:
+            K.sparse_adamw_(rows_buf, count, cap, p, g, m, v, flags, 1e-2, (0.9, 0.999), 1e-8, 0.01, 3, shadow=sh)
+        else:
+            K.sparse_adagrad_(rows_buf, count, cap, p, g, m, flags, 1e-2, 0.0, 1e-10, 3, shadow=sh)
+        torch.cuda.synchronize()
+        res.append((p.clone(), g.clone(), m.clone(), v.clone(), sh.clone(), flags.clone()))
+    (p1, g1, m1, v1, s1, f1), (p2, g2, m2, v2, s2, f2) = res
+    # the two forms share the per-element update; their code generation may still round
+    # the last step differently (1 ulp measured on p)
+    for nm, a, b in (("p", p1, p2), ("m", m1, m2), ("v", v1, v2)):
+        err = float(((a - b).abs() - 2.4e-7 * torch.maximum(a.abs(), b.abs())).max())
+        assert err <= 1e-7, (nm, err)  # 2 ulp of the larger, or 1e-7 where the update cancels p
+    assert torch.equal(f1, f2)
+    assert torch.equal(s2[rows], p2[rows].to(torch.bfloat16))
+    assert int(g1.abs().sum()) == 0 and int(f1.sum()) == 0
+    untouched = torch.ones(R, dtype=torch.bool, device=dev)
+    untouched[rows] = False
+    assert torch.equal(p1[untouched], p0[untouched]) and torch.equal(m1[untouched], m0[untouched])
+    gi, pi, mi, vi = g0[rows], p0[rows], m0[rows], v0[rows]
+    if adam:
+        b1, b2, lr, wd, t = 0.9, 0.999, 1e-2, 0.01, 3
+        me = b1 * mi + (1 - b1) * gi
+        ve = b2 * vi + (1 - b2) * gi * gi
+        pe = pi * (1 - lr * wd) - (lr / (1 - b1 ** t)) * me / (ve.sqrt() / (1 - b2 ** t) ** 0.5 + 1e-8)
+        torch.testing.assert_close(v1[rows], ve, rtol=1e-5, atol=1e-6)
+    else:
+        me = mi + gi * gi
+        pe = pi - 1e-2 * gi / (me.sqrt() + 1e-10)
+    torch.testing.assert_close(m1[rows], me, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p1[rows], pe, rtol=1e-5, atol=1e-6)
+    assert torch.equal(s1[rows], p1[rows].to(torch.bfloat16))
