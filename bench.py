@@ -519,6 +519,8 @@ def main():
             traffic = pmc_traffic(base, fam)
         else:
             traffic = pmc_traffic(dom, s["calls"] / args.steps)
+        if args.config != "c2" or args.batch or world > 1:
+            traffic = None  # the committed counter passes profile the default (C2, one GPU) run only
         res["roofline"] = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                            "frac": round(ach / peak, 4),
                            "traffic": round(traffic) if traffic is not None else None,
