@@ -169,7 +169,7 @@ class TransformerBlockFn(torch.autograd.Function):
         dw1 = K.linear_wgrad(dpre, h2)
         db1 = K.colsum(dpre) if has_b1 else None
         dh2 = K.linear_dgrad(dpre, w1_b)
-        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy)
+        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b)
         # attention half (dx1r: the gradient behind the residual dropout)
         if pr > 0.0:
             dx1r = K.dropout(dx1, pr, seed + 1)
@@ -185,7 +185,7 @@ class TransformerBlockFn(torch.autograd.Function):
         dwqkv = K.linear_wgrad(dqkv, h1)
         dbqkv = K.colsum(dqkv) if has_bqkv else None
         dh1 = K.linear_dgrad(dqkv, wqkv_b)
-        dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1,
+        dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1, need_bias=has_ln1b,
                                                 res2=dy if dbl else None)
         _stash_grad_bf16(dx, dxb)
         dtable = None
