@@ -383,6 +383,31 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs g, int tiles_n) {
   }
 }
 
+// split-K combine, 4 adjacent columns per thread (N % 4 == 0): 16-B partial loads, eight
+// splits' loads in flight ahead of the adds; each element still sums s = 0, 1, ... in order
+// (bit-identical to splitk_reduce_k)
+__global__ __launch_bounds__(256) void splitk_reduce4_k(GemmArgs g, int splits) {
+  const int64_t MN = g.M * g.N, total4 = MN / 4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total4; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rc = t * 4;
+    const int64_t row = rc / g.N, col = rc - row * g.N;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    const float* p = g.ws + rc;
+#pragma unroll 8
+    for (int s = 0; s < splits; ++s) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(p + (int64_t)s * MN);
+      v[0] += w[0]; v[1] += w[1]; v[2] += w[2]; v[3] += w[3];
+    }
+    const int64_t o = row * g.ldc + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float r = epilogue(g, v[e], row, col + e, 0);
+      if (g.out_dt == LTHM_F32) reinterpret_cast<float*>(g.C)[o + e] = r;
+      else reinterpret_cast<bf16_t*>(g.C)[o + e] = f2bf(r);
+    }
+  }
+}
+
 // split-K combine: C = epi(sum_s ws[s])
 __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs g, int splits, int batch) {
   const int64_t MN = g.M * g.N;
@@ -1062,7 +1087,10 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
       gr.ws = d->workspace;
       gr.alpha = 1.f;  // alpha already applied to the partials
       const int64_t total = d->M * d->N;
-      hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, gr, spl, 1);
+      if (d->N % 4 == 0 && ((uintptr_t)d->workspace % 16) == 0)
+        hipLaunchKernelGGL(splitk_reduce4_k, dim3(grid_for(total / 4, 256, 256 * 8)), dim3(256), 0, s, gr, spl);
+      else
+        hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, gr, spl, 1);
       LTHM_CHECK_LAUNCH();
       return amax_after();
     }
@@ -1146,7 +1174,10 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   LTHM_CHECK_LAUNCH();
   if (splits > 1) {
     const int64_t total = d->M * d->N * d->batch;
-    hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, g, splits, d->batch);
+    if (d->batch == 1 && d->N % 4 == 0 && ((uintptr_t)d->workspace % 16) == 0)
+      hipLaunchKernelGGL(splitk_reduce4_k, dim3(grid_for(total / 4, 256, 256 * 8)), dim3(256), 0, s, g, splits);
+    else
+      hipLaunchKernelGGL(splitk_reduce_k, dim3(grid_for(total, 256, 256 * 8)), dim3(256), 0, s, g, splits, d->batch);
     LTHM_CHECK_LAUNCH();
   }
   return amax_after();
