@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 28 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 29 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -462,7 +462,8 @@ int lthm_outcome_fwd(const float* x, const int64_t* labels, int64_t B, int32_t T
  * send_counts [world] and owner_base [world + 1] (owner_base[world] = the request total) stay on
  * the device; inv [n_items * K] holds, for every pair, the position of its row's value in the
  * buffer the exchange returns (owner-major, the send order).  Replaces torch.unique / argsort /
- * bincount of the reference-style exchange; workspace: lthm_shard_route_ws_bytes bytes. */
+ * bincount of the reference-style exchange; workspace: lthm_shard_route_ws_bytes bytes.
+ * 1 <= world <= 256 (the per-owner counts live in LDS); larger worlds are refused. */
 int64_t lthm_shard_route_ws_bytes(int64_t n_pairs, int32_t world);
 int lthm_shard_route(const int64_t* ids, int64_t n_items, int32_t K, int64_t P, int32_t world, int64_t* send_rows,
                      int64_t* send_counts, int64_t* owner_base, int64_t* inv, void* workspace, int64_t ws_bytes,
@@ -536,6 +537,10 @@ typedef struct lthm_contrastive_desc {
   int32_t rows_done;      /* backward: the forward already wrote dy (it was given y_raw / y_norm / dy at the fixed
                              shift: the fused forward + ROWS pass) for a unit upstream gradient; the backward
                              then runs the COLS side only and scales dy by *gscale */
+  void* main_ev0;         /* optional hipEvent_t pair recorded on the stream around the call's main pass alone
+                             (forward: cl_fr32_k / cl_fwd_k; backward: the cl_bwd32_k columns / rows passes),
+                             for live per-kernel timing (bench.py); NULL: not recorded */
+  void* main_ev1;
 } lthm_contrastive_desc;
 
 /* bytes of lthm_contrastive_desc.stats_ws for one forward launch (-1: invalid sizes) */
@@ -609,19 +614,22 @@ int lthm_dropout_rows(void* x, int32_t dtype, int64_t rows, int32_t cols, int32_
                       void* stream);
 int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed, void* stream);
 /* Streaming logQ for the LTHM loss (commons/layers.py:189-237 CascadedStreamingLogQ-
- * CorrectionModule, as wrapper.py:126-130 drives it per mini-batch of mb_size sequences):
+ * CorrectionModule, as wrapper.py:126-136 drives it per mini-batch of mb_size sequences):
  * for mini-batch k in order, train_step on its non-pad ids at batch index batch_idx0 + k,
  * then out[b, t] = -beta * min_m(-log b_m[(id + hash_offsets[m]) mod num_buckets]) for
  * all its ids.  b_tables / a_tables: f32 [n_modules, num_buckets] (the modules' b / a
- * buffers stacked), updated in place.  ids [B, ids_stride], mask [B, mask_stride]
- * (1 = pad; NULL = no pads), out f32 [B, T] or NULL.  update = 0 skips the train_step
- * (the module's plain forward; beta = -1 then returns min_m -log b). */
+ * buffers stacked), updated in place, bit-identical to the reference's sequence of
+ * train_steps.  ids [B, ids_stride], mask [B, mask_stride] (1 = pad; NULL = no pads), out
+ * f32 [B, T] or NULL (update only: the β = 0 case, where the reference trains the
+ * estimates but the correction vanishes).  update = 0 skips the train_step (the module's
+ * plain forward; beta = -1 then returns min_m -log b).  With update, workspace holds
+ * lthm_logq_ws_bytes(B, T, mb_size, n_modules) bytes (a per-call bucket table; every
+ * mini-batch's updates run in parallel over buckets).  n_modules * num_buckets < 2^32 - 1. */
+int64_t lthm_logq_ws_bytes(int64_t B, int32_t T, int32_t mb_size, int32_t n_modules);
 int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride, int64_t B,
                      int32_t T, int32_t mb_size, float* b_tables, float* a_tables, const int64_t* hash_offsets,
                      int32_t n_modules, int64_t num_buckets, float alpha, int64_t batch_idx0, float beta,
-                     int32_t update, float* out, float* scratch, void* stream);
-/* (scratch: with update, f32 [min(mb_size, B) * T]: every token of a mini-batch computes its
- * bucket's new value before any is written, the semantics of the reference's index_put) */
+                     int32_t update, float* out, void* workspace, int64_t ws_bytes, void* stream);
 /* History-trim statistics of mask [B, T] (uint8, 1 = pad) for query_tower.py:73-86:
  * work[0] = first column holding a non-pad entry (T if none), work[1] = number of
  * all-pad columns; work is a device int32 buffer of T + 2 entries (work[2..] scratch). */

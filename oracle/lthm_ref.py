@@ -10,9 +10,11 @@ reference's source (it cannot be imported: SURVEY.md §3.5 #1):
 
 with the same bug resolutions as the product (DESIGN.md §"Bug resolutions").
 Components with reference goldens (KShift, CVE, TransformerBlock, MLP,
-cap_gradients) are pinned by tests/test_oracle_golden.py; the composition
-itself is "parity unpinned" by the reference (it never ran) and is checked
-only for self-consistency against the HIP path.
+cap_gradients) are pinned by tests/test_oracle_golden.py; the composition is
+pinned by tests/test_lthm_step_golden_cpu.py against one training step of the
+reference's own Encoder / ProductTower / QueryTower forward code and loss
+(tests/golden/lthm_step_*.npz; build-defined stand-ins only where the reference
+cannot be constructed): the loss is bit-equal, the gradients within 2e-7.
 
 Parameters are read from the product model's state_dict (same names), so the
 two paths run identical weights.

@@ -195,6 +195,22 @@ def call(name: str, *args, _key: str = None, _work: float = None, _unit: str = N
         raise RuntimeError(f"{name} failed with hip error {rc}")
 
 
+def sub_events(key: str, work: float = None, unit: str = None, nbytes: float = None):
+    """(start, end) HIP events for ONE kernel launched inside a C-ABI call, which records them
+    around that launch (e.g. lthm_contrastive_desc.main_ev0 / main_ev1), or None when the live
+    timer is off or does not want ``key``.  Both events are recorded here once first, so their
+    handles exist; the call re-records them at the kernel's boundaries."""
+    t = TIMER
+    if t is None or (t.only is not None and key not in t.only):
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    e1.record()
+    t.records.append((key, e0, e1, work, unit, nbytes))
+    return e0, e1
+
+
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 

@@ -344,6 +344,8 @@ class RowShardedKShiftEmbedding(nn.Module):
         import torch.distributed as dist
         self._world = world if world is not None else world_size()
         self._rank = rank if rank is not None else (dist.get_rank() if dist.is_initialized() else 0)
+        if not 0 < self._world <= 256:  # lthm_shard_route's per-owner counts (csrc/shard.hip)
+            raise ValueError(f"RowShardedKShiftEmbedding supports 1..256 ranks, got world={self._world}")
         self._num_embeddings = num_embeddings
         self._num_shifts = num_shifts
         self._mode = K.KSHIFT_NORMALIZE if normalize_output else K.KSHIFT_SCALE
@@ -536,10 +538,15 @@ def _logq_call(mods, ids, mask, mb_size, batch_idx0, beta, update, want_out=True
     offs = torch.tensor([int(m.hash_offset) for m in mods], dtype=torch.int64).to(ids.device, non_blocking=True)
     B, T = ids2.shape
     out = torch.empty((B, T), dtype=torch.float32, device=ids.device) if want_out else None
-    scratch = torch.empty(min(mb_size, B) * T, dtype=torch.float32, device=ids.device) if update else None
+    ws, wsb = None, 0
+    if update:  # the per-call bucket table of the parallel update (lthm_logq_ws_bytes)
+        from .._lib import load
+        wsb = int(load().lthm_logq_ws_bytes(B, T, mb_size, len(mods)))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=ids.device)
     call("lthm_logq_stream", ptr(ids2), ids2.stride(0), ptr(mask), 0 if mask is None else mask.stride(0), B, T,
          mb_size, ptr(bt), ptr(at), ptr(offs), len(mods), nb, float(mods[0].alpha), int(batch_idx0), float(beta),
-         int(update), ptr(out), ptr(scratch), stream())
+         int(update), ptr(out), ptr(ws), wsb, stream(), _key="logq_stream",
+         _work=float(B * T) * (8 + 1 + (len(mods) * 16 if update else 0) + (4 if want_out else 0)), _unit="byte")
     return out.view(shp) if want_out else None
 
 
@@ -558,9 +565,11 @@ class CascadedStreamingLogQCorrectionModule(nn.Module):
         _logq_call(list(self.models), products.reshape(1, -1), None, 1, batch_idx, 0.0, True, want_out=False)
 
     def stream_correction(self, ids: torch.Tensor, mask: torch.Tensor, mb_size: int, batch_idx0: int,
-                          beta: float) -> torch.Tensor:
-        """The LTHM loss's use (wrapper.py:126-130, 204-208) over all mini-batches of mb_size
+                          beta: float, want_out: bool = True) -> Optional[torch.Tensor]:
+        """The LTHM loss's use (wrapper.py:126-136, 204-208) over all mini-batches of mb_size
         sequences in order: train_step on each mini-batch's non-pad ids at batch index
-        batch_idx0 + k, then -beta * logQ of its ids.  ids int64 [B, T], mask [B, T] (1 = pad)."""
+        batch_idx0 + k, then -beta * logQ of its ids.  ids int64 [B, T], mask [B, T] (1 = pad).
+        want_out=False runs the train_steps only (beta = 0: the correction is zero) and
+        returns None."""
         m = (mask if mask.dtype == torch.uint8 else mask.to(torch.uint8)).contiguous()
-        return _logq_call(list(self.models), ids.contiguous(), m, mb_size, batch_idx0, beta, True)
+        return _logq_call(list(self.models), ids.contiguous(), m, mb_size, batch_idx0, beta, True, want_out=want_out)

@@ -69,61 +69,145 @@ static inline uint32_t dropout_thresh(float p) {
 
 // ---------------------------------------------------------------- streaming logQ
 // CascadedStreamingLogQCorrectionModule (commons/layers.py:189-237, train_step as fixed
-// in SURVEY §3.5 #7-8) driven the way the LTHM loss drives it (wrapper.py:126-130): for
-// each mini-batch in order, first the train_step on its non-pad ids at batch index
-// batch_idx0 + mb (b[h] <- (1 - alpha) b[h] + alpha (idx - a[h]); a[h] <- idx, every
-// duplicate computing from the pre-update state, as the reference's index_put does),
-// then the correction of all its ids: out = -beta * min_m (-log b_m[(id + off_m) mod N]).
-// One workgroup walks the mini-batches in order (the updates chain through b and a).
+// in SURVEY §3.5 #7-8) driven the way the LTHM loss drives it (wrapper.py:126-136): for
+// each mini-batch k in order, first the train_step on its non-pad ids at batch index
+// batch_idx0 + k (b[h] <- (1 - alpha) b[h] + alpha (idx - a[h]); a[h] <- idx, every
+// duplicate of a mini-batch computing from the pre-update state, as the reference's
+// index_put does), then the correction of all its ids:
+// out = -beta * min_m (-log b_m[(id + off_m) mod N]).
+//
+// The chain through b and a runs per bucket, and a bucket's chain depends only on WHICH
+// mini-batches touched it.  So, all in parallel:
+//   logq_insert_k  every (non-pad token, module) inserts its key m * N + h into an
+//                  open-addressing table and sets bit k of the entry's mini-batch mask;
+//   logq_apply_k   every entry keeps the bucket's state from before the call and walks its
+//                  mask bits in increasing k, applying the update -- the same fp32 operations
+//                  in the same order as the reference's sequence of train_steps (no
+//                  contraction: __fmul_rn / __fadd_rn), so b and a come out bit-identical;
+//   logq_out_k     (with out) every token's value after ITS mini-batch: untouched buckets read
+//                  the table, touched ones replay their chain up to k from the saved state.
+// The table holds 2x the (token, module) pairs, so probing always ends.
+constexpr uint32_t LQ_EMPTY = 0xFFFFFFFFu;
+
 __device__ __forceinline__ int64_t logq_bucket(int64_t id, int64_t off, int64_t nb) {
   const int64_t h = (int64_t)((uint64_t)id + (uint64_t)off) % nb;  // int64 wrap, then torch remainder
   return h < 0 ? h + nb : h;
 }
 
-__global__ __launch_bounds__(1024) void logq_stream_k(const int64_t* __restrict__ ids, const uint8_t* __restrict__ mask,
-                                                      int64_t B, int T, int64_t ids_stride, int64_t mask_stride, int mbs,
-                                                      float* __restrict__ btab, float* __restrict__ atab,
-                                                      const int64_t* __restrict__ offs, int n_mod, int64_t nb,
-                                                      float alpha, int64_t batch_idx0, float beta, int update,
-                                                      float* __restrict__ out, float* __restrict__ scratch) {
-  const int n_mb = (int)((B + mbs - 1) / mbs);
-  for (int mb = 0; mb < n_mb; ++mb) {
-    const int64_t b0 = (int64_t)mb * mbs;
-    const int64_t cnt = min((int64_t)mbs, B - b0) * T;
-    const float idx = (float)(batch_idx0 + mb);
-    for (int m = 0; m < (update ? n_mod : 0); ++m) {
-      float* bt = btab + (int64_t)m * nb;
-      float* at = atab + (int64_t)m * nb;
-      // every token of the mini-batch computes its bucket's new value from the state before
-      // the mini-batch (the reference's index_put: duplicates agree, whichever writes last),
-      // then all of them write: two passes over the whole mini-batch with a barrier between
-      for (int64_t i = threadIdx.x; i < cnt; i += 1024) {
-        const int64_t bb = b0 + i / T, t = i % T;
-        if (!mask || !mask[bb * mask_stride + t]) {
-          const int64_t h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
-          scratch[i] = (1.f - alpha) * bt[h] + alpha * (idx - at[h]);
-        }
+__device__ __forceinline__ uint32_t logq_slot0(uint32_t key, uint32_t cap_mask) {
+  uint32_t x = key * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  return x & cap_mask;
+}
+
+struct LogqArgs {
+  const int64_t* ids;
+  const uint8_t* mask;
+  int64_t B, ids_stride, mask_stride;
+  int T, mbs, n_mod, n_w;
+  const int64_t* offs;
+  int64_t nb;
+  float* bt;
+  float* at;
+  float alpha, oma, beta;
+  int64_t batch_idx0;
+  uint32_t* keys;   // [cap]
+  uint32_t* bits;   // [cap, n_w]
+  float* b0;        // [cap]
+  float* a0;        // [cap]
+  uint32_t cap_mask;
+  float* out;
+};
+
+__device__ __forceinline__ void logq_step(float& b, float& a, float idx, float alpha, float oma) {
+  // (1 - alpha) * b[h] + (alpha * (batch_idx - a[h])).float(): three rounded fp32 ops and the add
+  b = __fadd_rn(__fmul_rn(oma, b), __fmul_rn(alpha, __fsub_rn(idx, a)));
+  a = idx;
+}
+
+__global__ __launch_bounds__(256) void logq_insert_k(LogqArgs p) {
+  const int64_t n = p.B * p.T;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t bb = i / p.T, t = i % p.T;
+    if (p.mask && p.mask[bb * p.mask_stride + t]) continue;
+    const int64_t id = p.ids[bb * p.ids_stride + t];
+    const int mb = (int)(bb / p.mbs);
+    for (int m = 0; m < p.n_mod; ++m) {
+      const uint32_t key = (uint32_t)((int64_t)m * p.nb + logq_bucket(id, p.offs[m], p.nb));
+      uint32_t s = logq_slot0(key, p.cap_mask);
+      while (true) {
+        const uint32_t old = atomicCAS(p.keys + s, LQ_EMPTY, key);
+        if (old == LQ_EMPTY || old == key) break;
+        s = (s + 1) & p.cap_mask;
       }
-      __syncthreads();
-      for (int64_t i = threadIdx.x; i < cnt; i += 1024) {
-        const int64_t bb = b0 + i / T, t = i % T;
-        if (!mask || !mask[bb * mask_stride + t]) {
-          const int64_t h = logq_bucket(ids[bb * ids_stride + t], offs[m], nb);
-          bt[h] = scratch[i];
-          at[h] = idx;
-        }
-      }
-      __syncthreads();
+      atomicOr(p.bits + (int64_t)s * p.n_w + (mb >> 5), 1u << (mb & 31));
     }
-    for (int64_t i = threadIdx.x; out && i < cnt; i += 1024) {
-      const int64_t bb = b0 + i / T, t = i % T;
-      const int64_t id = ids[bb * ids_stride + t];
-      float q = INFINITY;
-      for (int m = 0; m < n_mod; ++m) q = fminf(q, -__logf(btab[(int64_t)m * nb + logq_bucket(id, offs[m], nb)]));
-      out[bb * T + t] = -beta * q;
-    }
-    __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void logq_apply_k(LogqArgs p) {
+  const int64_t cap = (int64_t)p.cap_mask + 1;
+  for (int64_t s = blockIdx.x * (int64_t)256 + threadIdx.x; s < cap; s += (int64_t)gridDim.x * 256) {
+    const uint32_t key = p.keys[s];
+    if (key == LQ_EMPTY) continue;
+    float b = p.bt[key], a = p.at[key];
+    p.b0[s] = b;
+    p.a0[s] = a;
+    for (int w = 0; w < p.n_w; ++w) {
+      uint32_t m = p.bits[s * p.n_w + w];
+      while (m) {
+        const int k = w * 32 + __builtin_ctz(m);
+        m &= m - 1;
+        logq_step(b, a, (float)(p.batch_idx0 + k), p.alpha, p.oma);
+      }
+    }
+    p.bt[key] = b;
+    p.at[key] = a;
+  }
+}
+
+// update = 0: the plain forward (no table; cap_mask unused)
+__global__ __launch_bounds__(256) void logq_out_k(LogqArgs p, int update) {
+  const int64_t n = p.B * p.T;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t bb = i / p.T, t = i % p.T;
+    const int64_t id = p.ids[bb * p.ids_stride + t];
+    const int mb = (int)(bb / p.mbs);
+    float q = INFINITY;
+    for (int m = 0; m < p.n_mod; ++m) {
+      const uint32_t key = (uint32_t)((int64_t)m * p.nb + logq_bucket(id, p.offs[m], p.nb));
+      float b = p.bt[key];
+      if (update) {
+        uint32_t s = logq_slot0(key, p.cap_mask);
+        uint32_t k0;
+        while ((k0 = p.keys[s]) != LQ_EMPTY && k0 != key) s = (s + 1) & p.cap_mask;
+        if (k0 == key) {  // replay this bucket's chain up to (and including) mini-batch mb
+          float a = p.a0[s];
+          b = p.b0[s];
+          for (int w = 0; w <= (mb >> 5); ++w) {
+            uint32_t bits = p.bits[(int64_t)s * p.n_w + w];
+            if (w == (mb >> 5)) bits &= (mb & 31) == 31 ? 0xFFFFFFFFu : ((2u << (mb & 31)) - 1u);
+            while (bits) {
+              const int k = w * 32 + __builtin_ctz(bits);
+              bits &= bits - 1;
+              logq_step(b, a, (float)(p.batch_idx0 + k), p.alpha, p.oma);
+            }
+          }
+        }
+      }
+      q = fminf(q, -logf(b));
+    }
+    p.out[bb * p.T + t] = -p.beta * q;
+  }
+}
+
+static inline int64_t logq_cap(int64_t B, int T, int n_mod) {
+  const int64_t pairs = B * (int64_t)T * n_mod;
+  int64_t cap = 1024;
+  while (cap < 2 * pairs) cap <<= 1;
+  return cap;
 }
 
 // Multi-tensor f32 -> bf16 cast (lthm_cast_multi_bf16): a block per 1024-element
@@ -264,19 +348,51 @@ extern "C" int lthm_dropout_mask(uint8_t* out, int64_t n, float p, uint64_t seed
   return 0;
 }
 
+extern "C" int64_t lthm_logq_ws_bytes(int64_t B, int32_t T, int32_t mb_size, int32_t n_modules) {
+  if (B < 0 || T <= 0 || mb_size <= 0 || n_modules <= 0) return -1;
+  const int64_t cap = logq_cap(B, T, n_modules);
+  const int64_t n_w = ((B + mb_size - 1) / mb_size + 31) / 32;
+  return cap * (4 + 4 * n_w + 8) + 256;
+}
+
 extern "C" int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const uint8_t* mask, int64_t mask_stride,
                                 int64_t B, int32_t T, int32_t mb_size, float* b_tables, float* a_tables,
                                 const int64_t* hash_offsets, int32_t n_modules, int64_t num_buckets, float alpha,
-                                int64_t batch_idx0, float beta, int32_t update, float* out, float* scratch,
-                                void* stream) {
+                                int64_t batch_idx0, float beta, int32_t update, float* out, void* workspace,
+                                int64_t ws_bytes, void* stream) {
   LTHM_REQUIRE(B >= 0 && T > 0 && mb_size > 0 && n_modules > 0 && num_buckets > 0);
   LTHM_REQUIRE(ids_stride >= T && (!mask || mask_stride >= T));
-  LTHM_REQUIRE(!update || scratch);
-  if (B == 0) return 0;
-  hipLaunchKernelGGL(logq_stream_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, ids, mask, B, T, ids_stride,
-                     mask_stride, mb_size, b_tables, a_tables, hash_offsets, n_modules, num_buckets, alpha, batch_idx0,
-                     beta, update, out, scratch);
-  LTHM_CHECK_LAUNCH();
+  LTHM_REQUIRE((int64_t)n_modules * num_buckets < (int64_t)LQ_EMPTY);  // keys m * N + h fit 32 bits
+  LTHM_REQUIRE(batch_idx0 >= 0 && batch_idx0 + (B + mb_size - 1) / mb_size <= (1ll << 24));  // exact in fp32
+  LTHM_REQUIRE(!update || (workspace && ws_bytes >= lthm_logq_ws_bytes(B, T, mb_size, n_modules)));
+  if (B == 0 || (!update && !out)) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  LogqArgs p{};
+  p.ids = ids; p.mask = mask; p.B = B; p.ids_stride = ids_stride; p.mask_stride = mask_stride;
+  p.T = T; p.mbs = mb_size; p.n_mod = n_modules; p.offs = hash_offsets; p.nb = num_buckets;
+  p.bt = b_tables; p.at = a_tables; p.alpha = alpha; p.oma = (float)(1.0 - (double)alpha); p.beta = beta;
+  p.batch_idx0 = batch_idx0; p.out = out;
+  const int64_t n = B * (int64_t)T;
+  if (update) {
+    const int64_t cap = logq_cap(B, T, n_modules);
+    p.n_w = (int)(((B + mb_size - 1) / mb_size + 31) / 32);
+    char* w = (char*)workspace;
+    p.keys = (uint32_t*)w;
+    p.bits = (uint32_t*)(w + cap * 4);
+    p.b0 = (float*)(w + cap * (4 + 4 * (int64_t)p.n_w));
+    p.a0 = p.b0 + cap;
+    p.cap_mask = (uint32_t)(cap - 1);
+    if (hipMemsetAsync(p.keys, 0xFF, cap * 4, s) != hipSuccess) return (int)hipGetLastError();
+    if (hipMemsetAsync(p.bits, 0, cap * 4 * (int64_t)p.n_w, s) != hipSuccess) return (int)hipGetLastError();
+    hipLaunchKernelGGL(logq_insert_k, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, s, p);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL(logq_apply_k, dim3(grid_for(cap, 256, 256 * 32)), dim3(256), 0, s, p);
+    LTHM_CHECK_LAUNCH();
+  }
+  if (out) {
+    hipLaunchKernelGGL(logq_out_k, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, s, p, update);
+    LTHM_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -21,13 +21,14 @@ namespace lthm {
 
 constexpr int SR_NP = 2048;  // (row, pair) keys per workgroup
 constexpr int SR_PB = 11;    // bits of the pair index inside a key
+constexpr int SR_MAXW = 256; // owners: shard_dedup_k counts per owner in __shared__ s_own[SR_MAXW]
 
 __global__ __launch_bounds__(256) void shard_dedup_k(const int64_t* __restrict__ ids, int64_t n_pairs, int K,
                                                      int64_t P, int W, int64_t* __restrict__ u_row,
                                                      int32_t* __restrict__ u_slot, int32_t* __restrict__ u_cnt,
                                                      int32_t* __restrict__ blk_cnt, int32_t* __restrict__ inv_local) {
   __shared__ uint64_t keys[SR_NP];
-  __shared__ int s_own[256];
+  __shared__ int s_own[SR_MAXW];
   __shared__ int s_wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * SR_NP;
@@ -190,7 +191,7 @@ extern "C" int64_t lthm_shard_route_ws_bytes(int64_t n_pairs, int32_t world) {
 extern "C" int lthm_shard_route(const int64_t* ids, int64_t n_items, int32_t K, int64_t P, int32_t world,
                                 int64_t* send_rows, int64_t* send_counts, int64_t* owner_base, int64_t* inv,
                                 void* workspace, int64_t ws_bytes, void* stream) {
-  LTHM_REQUIRE(n_items >= 0 && K > 0 && K <= 64 && P > 0 && world > 0 && world <= 32768);
+  LTHM_REQUIRE(n_items >= 0 && K > 0 && K <= 64 && P > 0 && world > 0 && world <= SR_MAXW);
   LTHM_REQUIRE(P <= (1ll << (64 - SR_PB - 1)));
   const int64_t n_pairs = n_items * K;
   LTHM_REQUIRE(workspace && ws_bytes >= lthm_shard_route_ws_bytes(n_pairs, world));

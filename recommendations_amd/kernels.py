@@ -129,7 +129,9 @@ def shard_route(ids: torch.Tensor, P: int, K: int, world: int):
     require_gpu(ids)
     flat = ids.reshape(-1).contiguous()
     n = flat.numel()
-    _check(flat.dtype == torch.int64 and 0 < K <= 64 and P > 0 and world > 0, "shard_route: int64 ids, 0 < K <= 64")
+    # world <= 256: the dedup kernel counts requests per owner in a 256-entry LDS array (csrc/shard.hip)
+    _check(flat.dtype == torch.int64 and 0 < K <= 64 and P > 0 and 0 < world <= 256,
+           "shard_route: int64 ids, 0 < K <= 64, 0 < world <= 256")
     dev = ids.device
     npairs = n * K
     send = torch.empty(max(npairs, 1), dtype=torch.int64, device=dev)

@@ -88,10 +88,11 @@ class Encoder(nn.Module):
         routing, the count exchange the host reads and both all_to_alls (on a communicator
         of their own, distributed.row_exchange_group) -- runs on a side stream of the device.
         ``ready`` marks when the ids are valid (default: everything issued so far on the
-        current stream).  Issue it early, e.g. right after the current step's forward with
-        ``ready`` recorded when the next batch landed: the host then waits only for the side
-        stream's routing and count exchange while the current step's backward is queued.
-        Every rank must issue it at the same program point (collective order)."""
+        current stream).  At world > 1 the call blocks the host until the count exchange
+        has landed, so issue it once the current step's backward has been enqueued (with
+        ``ready`` recorded when the next batch landed): the host's wait then overlaps the
+        queued backward.  Every rank must issue it at the same program point (collective
+        order)."""
         raw = batch["product_ids"]
         K.require_gpu(raw)
         side = _side_stream(raw.device)

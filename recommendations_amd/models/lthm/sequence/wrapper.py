@@ -11,15 +11,18 @@ lookahead offsets drawn per mini-batch exactly as wrapper.py:147-153 does
 Bug resolutions: #11 ``self._model_config`` -> ``self.model_config``;
 #12 ``current_token_id`` -> ``current_token_ids``; #13 ``sparse`` /
 ``log_q_config`` / ``loss_type`` declared in the config.  The logQ streaming
-estimates are trained on every helper call as in the reference; the correction
-enters the loss kernels only when ``log_q_config.beta != 0`` (the shipped YAML has
-beta = 0, where the correction is exactly zero).
+estimates are trained on every helper call whatever beta is, as in the reference
+(wrapper.py:131-136); the correction enters the loss kernels only when
+``log_q_config.beta != 0`` (the shipped YAML has beta = 0, where it is exactly zero).
+``train_step`` / ``val_step`` return ``(loss, metrics)`` with the reference's metric
+dict (``StepMetrics``: materialised from the device statistics on first read).
 """
 from __future__ import annotations
 
 import ctypes
 import os
 import random
+from collections.abc import MutableMapping
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -27,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
-from ...._lib import STRUCTS, call, dcode, load, ptr, stream
+from ...._lib import STRUCTS, call, dcode, load, ptr, stream, sub_events
 from ....commons.base_model_wrapper import BaseModelWrapper
 from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
@@ -86,6 +89,10 @@ class ContrastiveLossFn(torch.autograd.Function):
             dy = torch.empty_like(yc)
             d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
         # algorithmic work: 2 n^2 De per head (S); with the row side also dS . in (2 n^2 De)
+        ev = sub_events("cl_fr32_k" if rows else "cl_fwd_main", (2.0 if rows else 1.0) * float(sum(cfg["flops"])),
+                        "flop")
+        if ev is not None:  # the fused pass alone, timed inside the call (bench.py's roofline kernel)
+            d.main_ev0, d.main_ev1 = ev[0].cuda_event, ev[1].cuda_event
         call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
              1.0 / n_mb, stream(), _key="cl_fwd_k", _work=(2.0 if rows else 1.0) * float(sum(cfg["flops"])),
              _unit="flop")
@@ -123,6 +130,12 @@ class ContrastiveLossFn(torch.autograd.Function):
         # every head in one call: the ROWS kernel writes dy per head through F.normalize (or the
         # forward already did: rows_done, dy scaled by g here), the COLS kernel sums dIn over the
         # six heads on chip and writes dt once through F.normalize
+        if dy_f is not None and getattr(ctx, "dy_consumed", False):
+            # a second backward through this graph (retain_graph): the first one scaled the
+            # forward's dy in place and returned it, so run the ROWS side again into a fresh dy
+            dy_f = None
+        if dy_f is not None:
+            ctx.dy_consumed = True
         dy = dy_f if dy_f is not None else torch.empty_like(yc)
         dt = torch.empty_like(tc)
         d = ContrastiveLossFn._desc(yn, tn, mask, B, T, NH, 0, De, mbs, n_mb, n_max, tau, offsets_dev,
@@ -133,6 +146,10 @@ class ContrastiveLossFn(torch.autograd.Function):
         d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
         d.t_raw, d.t_norm, d.dt, d.t_dtype = ptr(tc), ptr(tnorm), ptr(dt), dcode(tc)
         d.rows_done = 1 if dy_f is not None else 0
+        if dy_f is not None:  # the columns pass alone: S recompute + dS^T . out, 4 n^2 De per head
+            ev = sub_events("cl_bwd32_k", 2.0 * float(sum(ctx.flops)), "flop")
+            if ev is not None:
+                d.main_ev0, d.main_ev1 = ev[0].cuda_event, ev[1].cuda_event
         # algorithmic work per head: one S recompute + dS^T . out (2 x 2 n^2 De) with the row side
         # done in the forward; else also dS . in (3 x; the ROWS and COLS kernels each recompute S)
         call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
@@ -278,18 +295,17 @@ class LTHMModelWrapper(BaseModelWrapper):
         # non-pad ids, then the correction -beta * logQ of its ids (zeroed on the positive
         # in-kernel).  The streaming estimates advance whatever beta is, as the reference's do;
         # the correction enters the loss only when beta != 0 (with beta = 0 it is exactly zero)
-        logq = None
-        if self._log_q_beta != 0.0:
-            logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
-                                                      self._log_q_beta)
+        want = self._log_q_beta != 0.0
+        logq = self._log_q_calc.stream_correction(output["current_token_ids"], mask, mbs, self.batch_idx,
+                                                  self._log_q_beta, want_out=want)
         loss, stats = contrastive_step(y, tgt, mask, offs, mbs, self._softmax_temperature, self._metrics_k_all, logq)
         self.batch_idx += n_mb  # the reference counts helper calls, one per mini-batch
         self.last_stats = (stats, offs, step_type, B, T, mbs, whole)
-        return loss, {}
+        return loss, StepMetrics(stats, offs, step_type, self._metrics_k_all, B, T, mbs, whole)
 
     def metrics(self) -> Dict[str, float]:
-        """Metric dict of the last train_step / val_step, with the reference's keys and
-        values (wrapper.py:95-111, 139-142, 221-242; one device->host copy)."""
+        """Metric dict of the last train_step / val_step as a plain dict (the same values
+        train_step / val_step return)."""
         if self.last_stats is None:
             return {}
         stats, offs, step_type, B, T, mbs, whole = self.last_stats
@@ -317,6 +333,58 @@ class LTHMModelWrapper(BaseModelWrapper):
         for name, p in self.named_parameters():
             groups.setdefault(self.optim_group(self, name, p.numel()), []).append(p)
         return groups
+
+
+class StepMetrics(MutableMapping):
+    """The metric dict ``train_step`` / ``val_step`` return (wrapper.py:71-112, 139-142,
+    221-245: same keys, same values), built lazily from the loss kernels' device statistics.
+
+    Construction issues one non-blocking device->host copy of the [NH, n_mb, 7 + len(ks)]
+    statistics into pinned memory on the current stream and records an event; nothing
+    waits for the GPU until a key, the length or the repr is first read, so a training
+    loop that never reads the dict pays no synchronisation.  After that it behaves as a
+    plain mutable dict (the reference trainer adds into the first step's dict in place,
+    accelerate_training_strategy.py:405-409)."""
+
+    __slots__ = ("_pending", "_d")
+
+    def __init__(self, stats: torch.Tensor, offs: np.ndarray, step_type: str, ks: List[int], B: int, T: int,
+                 mbs: int, whole: bool):
+        host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
+        host.copy_(stats, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending = (host, ev, offs, step_type, list(ks), B, T, mbs, whole)
+        self._d: Optional[Dict[str, float]] = None
+
+    def _dict(self) -> Dict[str, float]:
+        if self._d is None:
+            host, ev, offs, step_type, ks, B, T, mbs, whole = self._pending
+            ev.synchronize()
+            self._d = lthm_metrics(host.numpy(), offs, step_type, ks, B, T, mbs, whole)
+            self._pending = None
+        return self._d
+
+    def __getitem__(self, k):
+        return self._dict()[k]
+
+    def __setitem__(self, k, v):
+        self._dict()[k] = v
+
+    def __delitem__(self, k):
+        del self._dict()[k]
+
+    def __iter__(self):
+        return iter(self._dict())
+
+    def __len__(self):
+        return len(self._dict())
+
+    def __repr__(self):
+        return repr(self._dict())
+
+    def copy(self) -> Dict[str, float]:
+        return dict(self._dict())
 
 
 def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[int], B: int, T: int, mbs: int,

@@ -1,0 +1,60 @@
+"""The HIP LTHM training step against the REFERENCE's own forward code and loss.
+
+tests/golden/lthm_step_*.npz (make_goldens.py::gen_lthm_step): one step of the reference's
+Encoder.forward / ProductTower.forward / QueryTower.forward and _mini_batch_mapper, fp32 on the
+CPU, with the build-defined stand-ins for the pieces the reference cannot construct (listed in
+the generator).  Here the build's LTHMModelWrapper gets the same weights (reference names),
+the same batch and the offsets the reference drew, and runs forward -> train_step -> backward
+through the HIP kernels.  tests/test_lthm_step_golden_cpu.py pins the oracle to the same
+fixtures on the CPU (loss bit-equal, gradients 2e-7).
+
+Bounds (bf16 operands through the encoder GEMMs and attention against fp32; measured errors
+are recorded through tests/parity.py): next_token_emb 3e-2 relative Frobenius over the rows
+the loss reads; the loss and the per-offset CE 2e-2; counts exact; every trainable
+parameter's gradient 8e-2 relative Frobenius (the same bound as the C5-shape step against
+the oracle, test_gpu_lthm.py)."""
+import numpy as np
+import pytest
+import torch
+
+from lthm_step_case import STEP_CASES, build_wrapper, load_case
+from parity import check, relerr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_hip_step_vs_reference(dev, name, monkeypatch):
+    fx, params, grads, batch = load_case(name)
+    m = build_wrapper(fx, params, dev)
+    offs = np.asarray(fx["offsets"], dtype=np.int32)
+    monkeypatch.setattr(m, "draw_offsets", lambda n_mb: offs[:n_mb].copy())
+    m.train()
+    b = {k: v.to(dev) for k, v in batch.items()}
+    out = m(b)
+    loss, metrics = m.train_step(b, out)
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_y = torch.from_numpy(fx["next_token_emb"])
+    y = out["next_token_emb"].float().cpu()
+    assert y.shape == ref_y.shape, (y.shape, ref_y.shape)
+    mask = torch.from_numpy(fx["current_token_mask"]).reshape(ref_y.shape[0], -1)
+    assert torch.equal(out["current_token_mask"].cpu().reshape(mask.shape).bool(), mask.bool())
+    check(f"{name} next_token_emb", relerr(y, ref_y), 3e-2)
+    check(f"{name} current_token_emb", relerr(out["current_token_emb"].float().cpu(),
+                                             torch.from_numpy(fx["current_token_emb"])), 1e-2)
+    ref_loss = float(fx["loss"][0])
+    check(f"{name} loss", abs(float(loss) - ref_loss) / abs(ref_loss), 2e-2)
+    ref_m = dict(zip([str(k) for k in fx["metric_keys"]], fx["metric_values"].tolist()))
+    assert set(metrics) == set(ref_m), sorted(set(metrics) ^ set(ref_m))
+    for k, rv in ref_m.items():
+        v = metrics[k]
+        if any(s in k for s in ("batch_size", "seq_len", "used_tokens", "average_negatives")):
+            assert abs(v - rv) <= 1e-6 * max(1.0, abs(rv)), (k, v, rv)
+        elif "loss" in k:
+            check(f"{name} {k}", abs(v - rv) / max(abs(rv), 1e-6), 2e-2)
+    named = dict(m.named_parameters())
+    for k, g in grads.items():
+        got = named[k].grad
+        assert got is not None, k
+        check(f"{name} grad {k}", relerr(got.float().cpu(), g), 8e-2)

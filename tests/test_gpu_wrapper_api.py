@@ -1,0 +1,218 @@
+"""The BaseModelWrapper contract of LTHMModelWrapper, driven the way the reference trainer
+drives it (/root/reference/commons/training_strategy/accelerate_training_strategy.py):
+
+  * train loop (:353-368, :405-409): ``loss, metrics = train_step_fn(batch, output)``, the first
+    step's dict becomes ``metrics_agg`` and later steps add into it in place, then the
+    aggregate is divided by the step count (:413-414);
+  * ``val()`` (:506-516): ``loss.item()``, the NaN scan over every metric value, and the
+    per-key sum over batches.
+
+The loss inputs are the contrastive goldens' (tests/golden/contrastive_*.npz, written by
+the reference's own _mini_batch_mapper / _train_or_val_step_helper); the wrapper is given
+the offsets the reference drew (its own draw is a seeded stream) and, for the logQ case,
+the reference run's fixed correction.  The metric dict returned by train_step / val_step
+themselves must equal the reference's (bounds as tests/test_gpu_loss_golden.py).
+
+Also: the logQ streaming estimates advance at beta = 0 (wrapper.py:131-136 trains them
+on every helper call whatever beta is), bit-identical to the reference's train_step
+sequence restated on the CPU.
+"""
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+from parity import check
+from test_gpu_loss_golden import check_metrics
+
+sys.path.insert(0, GOLDEN)
+from contrastive_inputs import CASES, make_inputs  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _wrapper(case, dev, **kw):
+    from recommendations_amd.models.lthm.config import lthm_config
+    from recommendations_amd.models.lthm.sequence.wrapper import LTHMModelWrapper
+    cfg = lthm_config(T=case["T"], d=64, n_layers=1, n_head=2, item_vocab=1000, lookahead=list(case["lookahead"]),
+                      train_mini_batch_size=case["mbs"], softmax_temperature=case["tau"],
+                      metrics_k_all=list(case["ks"]), log_q_beta=case["beta"], gradient_checkpointing=False,
+                      **kw)
+    return LTHMModelWrapper(cfg).to(dev)
+
+
+def _output(case, dev, ydt):
+    inp = make_inputs(case)
+    B, T = case["B"], case["T"]
+    g = torch.Generator().manual_seed(case["seed"])
+    return {
+        "next_token_emb": torch.from_numpy(inp["y"]).to(dev).to(ydt).requires_grad_(True),
+        "current_token_emb": torch.from_numpy(inp["tgt"]).to(dev).requires_grad_(True),
+        "current_token_mask": torch.from_numpy(inp["mask"]).to(dev),
+        "current_token_ids": torch.randint(0, 2 ** 40, (B, T), generator=g, dtype=torch.int64).to(dev),
+    }, inp
+
+
+def _fix_offsets(m, fx, monkeypatch):
+    offs = np.asarray(fx["offsets"], dtype=np.int32)
+    monkeypatch.setattr(m, "draw_offsets", lambda n_mb: offs[:n_mb].copy())
+
+
+def _fix_logq(m, case, inp, monkeypatch):
+    if case["beta"] == 0.0:
+        return
+    corr = (-case["beta"] * torch.from_numpy(inp["logq"]))
+    orig = m._log_q_calc.stream_correction
+
+    def stream_correction(ids, mask, mbs, idx0, beta, want_out=True):
+        orig(ids, mask, mbs, idx0, beta, want_out=False)  # the estimates still advance
+        return corr.to(ids.device)
+    monkeypatch.setattr(m._log_q_calc, "stream_correction", stream_correction)
+
+
+@pytest.mark.parametrize("name", [n for n, c in CASES.items() if c["mode"] == "train"])
+def test_train_step_metrics_through_reference_loop(dev, name, monkeypatch):
+    case = CASES[name]
+    fx = golden("contrastive_" + name)
+    exact = case["kind"] == "exact"
+    m = _wrapper(case, dev)
+    _fix_offsets(m, fx, monkeypatch)
+    steps = 2
+    metrics_agg, metrics_agg_num = {}, 0
+    for step in range(steps):
+        out, inp = _output(case, dev, torch.float32)
+        _fix_logq(m, case, inp, monkeypatch)
+        loss, metrics = m.train_step({}, out)  # :354
+        loss.backward()
+        if step == 0:  # the dict is lazy: nothing has waited for the GPU yet
+            assert metrics._d is None
+        # :405-409, verbatim shape: the first dict becomes the aggregate, later ones add in place
+        if len(metrics_agg.keys()) == 0:
+            metrics_agg = metrics
+        else:
+            for k in metrics:
+                metrics_agg[k] += metrics[k]
+        metrics_agg_num += 1
+        if step == 0:
+            lb = 1e-5 if exact else 2e-3
+            check(f"{name} train_step loss", abs(float(loss) - float(fx["loss"][0])) / abs(float(fx["loss"][0])), lb)
+            # the values train_step returned, before the aggregation mutates them
+            check_metrics(f"{name} train_step", dict(metrics), fx, exact, lb)
+            print(f"METRICS: {metrics}")  # :371-372 prints the dict
+    for k in metrics_agg:  # :413-414
+        metrics_agg[k] = metrics_agg[k] / metrics_agg_num
+    check_metrics(f"{name} trainer aggregate", dict(metrics_agg), fx, exact, 1e-5 if exact else 2e-3)
+
+
+@pytest.mark.parametrize("name", [n for n, c in CASES.items() if c["mode"] == "val"])
+def test_val_step_metrics_through_reference_val(dev, name, monkeypatch):
+    case = CASES[name]
+    fx = golden("contrastive_" + name)
+    m = _wrapper(case, dev)
+    _fix_offsets(m, fx, monkeypatch)
+    m.eval()
+    val_loss, num_batches, skipped, metrics_agg = 0.0, 0, 0, {}
+    with torch.no_grad():
+        for _ in range(2):
+            out, inp = _output(case, dev, torch.float32)
+            loss, metrics = m.val_step({}, out)  # :506
+            val_loss += loss.item()
+            if any(np.isnan(metrics[k]) for k in metrics):  # :508-512
+                skipped += 1
+                continue
+            for k in metrics:
+                metrics_agg[k] = metrics_agg.setdefault(k, 0) + metrics[k]
+            num_batches += 1
+    assert skipped == 0 and num_batches == 2
+    check(f"{name} val loss", abs(val_loss / 2 - float(fx["loss"][0])) / abs(float(fx["loss"][0])), 1e-5)
+    check_metrics(f"{name} val()", {k: v / num_batches for k, v in metrics_agg.items()}, fx, True, 1e-5)
+
+
+def test_val_nan_scan_skips_bad_batch(dev, monkeypatch):
+    """A non-finite next_token_emb gives NaN metrics, and the val() scan skips the batch."""
+    case = CASES["val_whole"]
+    fx = golden("contrastive_val_whole")
+    m = _wrapper(case, dev)
+    _fix_offsets(m, fx, monkeypatch)
+    out, _ = _output(case, dev, torch.float32)
+    with torch.no_grad():
+        out["next_token_emb"][0, -1, 0, 0] = float("nan")
+        out["next_token_emb"][5, 30, 1, 3] = float("nan")
+        loss, metrics = m.val_step({}, out)
+    assert any(np.isnan(metrics[k]) for k in metrics)
+
+
+def test_logq_estimates_advance_at_beta_zero(dev):
+    """wrapper.py:131-136: _log_q_calc.train_step runs on every helper call whatever beta is.
+    After two train_steps at beta = 0 the a / b buffers equal the reference's sequence of
+    train_steps (commons/layers.py:210-213, fixed per SURVEY §3.5 #7) bit for bit."""
+    case = dict(CASES["train_ragged"])
+    m = _wrapper(case, dev)
+    assert m._log_q_beta == 0.0
+    lq = m._log_q_calc
+    nb = lq.models[0].num_buckets
+    offs = [int(md.hash_offset) for md in lq.models]
+    alpha = lq.models[0].alpha
+    bt = [md.b.detach().cpu().clone() for md in lq.models]
+    at = [md.a.detach().cpu().clone() for md in lq.models]
+    idx = 0
+    B, mbs = case["B"], case["mbs"]
+    g = torch.Generator().manual_seed(3)
+    for _ in range(2):
+        out, _ = _output(case, dev, torch.float32)
+        ids = torch.randint(0, 500, (B, case["T"]), generator=g, dtype=torch.int64)  # repeats across mini-batches
+        out["current_token_ids"] = ids.to(dev)
+        loss, _ = m.train_step({}, out)
+        mask = out["current_token_mask"].cpu()
+        for b0 in range(0, B, mbs):  # the reference: one helper call (one train_step) per mini-batch
+            sl = slice(b0, min(b0 + mbs, B))
+            valid = ids[sl][~mask[sl]]
+            for j, o in enumerate(offs):
+                h = torch.remainder(valid + o, nb)
+                bt[j][h] = (1 - alpha) * bt[j][h] + (alpha * (idx - at[j][h])).float()
+                at[j][h] = float(idx)
+            idx += 1
+    torch.cuda.synchronize()
+    assert m.batch_idx == idx
+    for j, md in enumerate(lq.models):
+        assert torch.equal(md.a.cpu(), at[j]), j
+        assert torch.equal(md.b.cpu(), bt[j]), j
+    assert float((lq.models[0].a > 0).sum()) > 0
+
+
+@pytest.mark.parametrize("B,T,mbs,nmod,nb", [(64, 128, 32, 7, 2 ** 24), (300, 40, 7, 3, 1009)])
+def test_logq_parallel_update_bit_exact(dev, B, T, mbs, nmod, nb):
+    """lthm_logq_stream's parallel bucket update and per-mini-batch outputs against the
+    reference's per-mini-batch loop, bit for bit: the shipped yaml's 7 modules x 2^24 buckets,
+    and a small table with > 32 mini-batches (multi-word masks) and heavy collisions."""
+    from recommendations_amd.commons.layers import CascadedStreamingLogQCorrectionModule
+    offs = [0, 34144, 7465477, 64363466, 4234551, 245435435, 143244556][:nmod]
+    alpha, p_init, beta = 0.05, 0.001, 0.7
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(0, 5000, (B, T), generator=g, dtype=torch.int64)
+    mask = torch.rand((B, T), generator=g) < 0.15
+    m = CascadedStreamingLogQCorrectionModule(nb, offs, alpha, p_init).to(dev)
+    got = m.stream_correction(ids.to(dev), mask.to(dev), mbs, 5, beta).cpu()
+    bt = [torch.full((nb,), 1.0 / p_init, dtype=torch.float32) for _ in offs]
+    at = [torch.zeros(nb) for _ in offs]
+    want = torch.empty(B, T)
+    for k, b0 in enumerate(range(0, B, mbs)):
+        sl = slice(b0, min(b0 + mbs, B))
+        idx = 5 + k
+        valid = ids[sl][~mask[sl]]
+        for j, o in enumerate(offs):
+            h = torch.remainder(valid + o, nb)
+            bt[j][h] = (1 - alpha) * bt[j][h] + (alpha * (idx - at[j][h])).float()
+            at[j][h] = float(idx)
+        q = None
+        for j, o in enumerate(offs):
+            v = -bt[j][torch.remainder(ids[sl] + o, nb)].log()
+            q = v if q is None else torch.minimum(q, v)
+        want[sl] = -beta * q
+    for j in range(len(offs)):
+        assert torch.equal(m.models[j].b.cpu(), bt[j]), j
+        assert torch.equal(m.models[j].a.cpu(), at[j]), j
+    # -log b on the GPU (logf) vs torch's CPU log: within an ulp or two
+    check(f"logq out B={B}", float((got - want).abs().max() / want.abs().max()), 1e-6)

@@ -1541,11 +1541,13 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
     cur.stage(sh.r.img[buf], g.n, w, lane);
     glds4(y0 + lane < a.n_max ? a.colb + base + y0 + lane : &cl_ninf, sh.r.m0[buf][w]);
   };
-  retire_loads();
-  stage(0);
-  if (ntile > 1) stage(1);
-  if (ntile > 2) stage(2);
-  for (int tI = 0; tI < ntile; ++tI) {
+  // one tile: S^T = img . rows^T on MFMA, then p, Z, counts and ranks, then dacc += p . img.
+  // SPEC: the tile holds image rows of the register rows' own sequences (diagonal and
+  // same-sequence exclusion, per element); the others are "clean" (every valid column kept).
+  // The tiles of the special range are contiguous, so three loops run the clean / special /
+  // clean tiles and the clean body is straight-line code with no per-element tests.
+  auto tile = [&](int tI, auto spec_tag) {
+    constexpr bool SPEC = decltype(spec_tag)::value;
     const int cb = tI % CL_NB32, y0 = tI * 64;
     if (tI + 2 < ntile) wait_vm<2 * PT>();
     else if (tI + 1 < ntile) wait_vm<PT>();
@@ -1565,61 +1567,39 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
         acc[ib] = mfma32(af, qf[s], acc[ib]);
       }
     }
-#if defined(CL_EXP) && CL_EXP >= 2
-    const bool special = false;
-#else
-    const bool special = y0 < spec_hi && y0 + 64 > spec_lo;
-#endif
-    if (!special) {
+    if (!SPEC) {
       // every valid column is kept; pad / beyond-n columns are zero image rows (S = 0) with a
       // -inf bias: counted out of cn, and out of the rank when 0 > thr
       const int np = __popcll(__ballot(colb[lane] == -INFINITY) & hmask);
       cn += 32 - np;
       rk -= (0.f > thr) ? np : 0;
     }
+    int ys0 = y0;  // laundered (see cl_bwd32_head)
+    if (SPEC) asm volatile("" : "+s"(ys0));
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) {
         const float4 c4 = *reinterpret_cast<const float4*>(colb + 32 * ib + 8 * qd + 4 * hh);
         const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
-        if (!special) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int v = 4 * qd + j;
-            const float sv = acc[ib][v];
-#if defined(CL_EXP) && CL_EXP >= 5
-            const float p = sv;
-#elif defined(CL_EXP) && CL_EXP >= 4
-            const float p = __builtin_fmaf(sv, c1, cv[j]);
-#else
+        for (int j = 0; j < 4; ++j) {
+          const int v = 4 * qd + j;
+          const float sv = acc[ib][v];
+          if (!SPEC) {
             const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j]));
-#endif
-#if !defined(CL_EXP) || CL_EXP < 5
             Z += p;
-#endif
-#if !defined(CL_EXP) || CL_EXP < 3
             rk += sv > thr ? 1 : 0;
-#endif
             acc[ib][v] = p;
-          }
-        } else {
-          int ys0 = y0;  // laundered (see cl_bwd32_head)
-          asm volatile("" : "+s"(ys0));
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int v = 4 * qd + j, yl = 32 * ib + 8 * qd + 4 * hh + j, y = ys0 + yl;
-            const float sv = acc[ib][v];
+          } else {
+            const int y = ys0 + 32 * ib + 8 * qd + 4 * hh + j;
             if (y == x) pv = sv * it;
             const int ysq = y < g.n ? seq_of(g, y) : -1;
             const bool keep = live && cv[j] != -INFINITY && (ysq != xsq || y == x);
-            float p = 0.f;
-            if (keep) {
-              p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j]));
-              Z += p;
-              cn += 1;
-              rk += (y != x && sv > thr) ? 1 : 0;
-            }
+            const float p = keep ? __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j])) : 0.f;
+            Z += p;
+            cn += keep ? 1 : 0;
+            rk += (keep && y != x && sv > thr) ? 1 : 0;
             acc[ib][v] = p;
           }
         }
@@ -1629,8 +1609,8 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
       for (int hf = 0; hf < 2; ++hf) {
         const int ks = 2 * ib + hf, o = 8 * hf;
         const f32x16& pvv = acc[ib];
-        const u32x4 hpk = {pk_bf16(pvv[o], pvv[o + 1]), pk_bf16(pvv[o + 2], pvv[o + 3]), pk_bf16(pvv[o + 4], pvv[o + 5]),
-                           pk_bf16(pvv[o + 6], pvv[o + 7])};
+        const u32x4 hpk = {pk_bf16(pvv[o], pvv[o + 1]), pk_bf16(pvv[o + 2], pvv[o + 3]),
+                           pk_bf16(pvv[o + 4], pvv[o + 5]), pk_bf16(pvv[o + 6], pvv[o + 7])};
         const bf16x8v af = __builtin_bit_cast(bf16x8v, hpk);
 #pragma unroll
         for (int nd = 0; nd < 4; ++nd) {
@@ -1639,7 +1619,17 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
         }
       }
     }
-  }
+  };
+  // tiles [t_lo, t_hi) overlap [spec_lo, spec_hi)
+  const int t_lo = min(spec_lo / 64, ntile), t_hi = max(min((spec_hi + 63) / 64, ntile), t_lo);
+  retire_loads();
+  stage(0);
+  if (ntile > 1) stage(1);
+  if (ntile > 2) stage(2);
+  int tI = 0;
+  for (; tI < t_lo; ++tI) tile(tI, std::false_type{});
+  for (; tI < t_hi; ++tI) tile(tI, std::true_type{});
+  for (; tI < ntile; ++tI) tile(tI, std::false_type{});
 }
 
 // grid ((n_max + 127) / 128, n_mb, heads): 4 waves x 32 register rows
@@ -1864,10 +1854,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
     LTHM_CHECK_LAUNCH();
     static const int xcd = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : 0;
     a.xcd_order = xcd;
-    if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
     hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
-    if (d->main_ev1 && hipEventRecord((hipEvent_t)d->main_ev1, s) != hipSuccess) return (int)hipGetLastError();
     if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
     a.colb = d->w;
   } else {
@@ -1875,11 +1863,9 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
     // fixed shift: 3 blocks per CU (3 waves per SIMD hide more of the exp / count VALU
     // latency: 0.91 -> 0.78-0.82 ms per C2 head; a 2-deep ring at 3 blocks measured the
     // same, 4 blocks spill); running shift: 2
-    if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
     if (fixed) hipLaunchKernelGGL((cl_fwd_k<true, 3, 3>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((cl_fwd_k<false, 3, 2>), grid, dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
-    if (d->main_ev1 && hipEventRecord((hipEvent_t)d->main_ev1, s) != hipSuccess) return (int)hipGetLastError();
   }
   const int nblk = (int)cl_stats_blocks(d->n_max);
   hipLaunchKernelGGL(cl_rowstats_k, dim3(nblk, d->n_mb, nrun), dim3(256), 0, s, a, hist, part);
@@ -1914,10 +1900,8 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
     hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, ash);
     LTHM_CHECK_LAUNCH();
     const dim3 gcols((int)(((int64_t)d->mb_size * d->T + 127) / 128), d->n_mb, 1);
-    if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
     hipLaunchKernelGGL((cl_bwd32_k<false, true, 4>), gcols, dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
-    if (d->main_ev1 && hipEventRecord((hipEvent_t)d->main_ev1, s) != hipSuccess) return (int)hipGetLastError();
     if (d->gscale) {
       const int64_t n = (int64_t)d->B * (d->T + 1) * d->n_heads * DE;
       const dim3 gs((unsigned)std::min<int64_t>((n / 8 + 255) / 256, 2048));
