@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 29 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 30 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -194,6 +194,14 @@ int lthm_mlp_supported(int32_t D, int32_t HID);
 int lthm_mlp_fwd(const void* x, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
                  const void* W2T, const float* b2, const float* res1, const float* res2, float* out,
                  void* stream);
+/* The training backward with the hidden RECOMPUTED (never stored by the forward):
+ * pre = x W1^T + b1; G = GELU(pre); dP = (dY W2) * GELU'(pre); dX = dP W1.  dY bf16 [M, D]
+ * (gradient of the MLP output), dX [M, D] in dx_dtype (LTHM_F32 / LTHM_BF16), G and dP bf16
+ * [M, HID]: the operands of dW2 = dY^T G and dW1 = dP^T x (db1 = colsum dP), which the
+ * weight-gradient GEMM computes.  Replaces the c_proj / c_fc dgrad pair of
+ * commons/transformers/layers.py:279-284's backward. */
+int lthm_mlp_bwd(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
+                 const void* W2T, void* dX, int32_t dx_dtype, void* G, void* dP, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm (commons/transformers/layers.py:142-149, eps 1e-5)               */

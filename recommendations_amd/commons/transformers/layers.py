@@ -15,6 +15,7 @@ are bf16 (GEMM operands), the residual stream and all accumulations fp32.
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -63,6 +64,11 @@ def _grad_bf16(g32: torch.Tensor) -> torch.Tensor:
             and src.dtype == g32.dtype and ver == src._version and g32.is_contiguous()):
         return bf.view(g32.shape)
     return K.cast(g32, torch.bfloat16)
+
+
+# training through the fused MLP (forward hidden on chip, backward recomputes it); LTHM_MLP_TRAIN=0
+# restores the stored-hidden chain (c_fc GEMM with the GELU' aux, c_proj GEMM, two dgrad GEMMs)
+_MLP_TRAIN = os.environ.get("LTHM_MLP_TRAIN", "1") == "1"
 
 
 class TransformerBlockFn(torch.autograd.Function):
@@ -123,10 +129,19 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
-        if infer and not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]):
-            # inference (no backward will run): the fused MLP keeps the [M, 4d] hidden on chip
-            out = K.mlp_fwd(h2, w1_b, _f(b1), w2_b.t().contiguous(), _f(b2), res1=x1,
-                            res2=x2 if double_residual else None)
+        if not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]) and (infer or _MLP_TRAIN):
+            # the fused MLP keeps the [M, 4d] hidden on chip; in training the backward
+            # recomputes it (K.mlp_bwd), so neither the hidden nor GELU' is stored
+            w2t_b = w2_b.t().contiguous()
+            out = K.mlp_fwd(h2, w1_b, _f(b1), w2t_b, _f(b2), res1=x1, res2=x2 if double_residual else None)
+            if infer:
+                return out.view(B, T, d)
+            ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, _f(b1), w2t_b,
+                                  wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
+            ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
+                       b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
+            ctx.mop = mop
+            ctx.fused_mlp = True
             return out.view(B, T, d)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
@@ -146,6 +161,7 @@ class TransformerBlockFn(torch.autograd.Function):
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
                    b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
         ctx.mop = mop
+        ctx.fused_mlp = False
         return out.view(B, T, d)
 
     @staticmethod
@@ -163,12 +179,21 @@ class TransformerBlockFn(torch.autograd.Function):
             dyb = K.cast(dym, torch.bfloat16)
         else:
             dym, dyb = dy, _grad_bf16(dy)
-        dw2 = K.linear_wgrad(dyb, g)
-        db2 = K.colsum(dym) if has_b2 else None
-        dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_MUL_AUX, aux=pre)
-        dw1 = K.linear_wgrad(dpre, h2)
-        db1 = K.colsum(dpre) if has_b1 else None
-        dh2 = K.linear_dgrad(dpre, w1_b)
+        if ctx.fused_mlp:
+            # saved: pre -> b1 (f32 or None), g -> c_proj.weight^T (bf16); the hidden is recomputed
+            b1f, w2t_b = pre, g
+            dh2, g, dpre = K.mlp_bwd(h2, dyb, w1_b, b1f, w2t_b)
+            dw2 = K.linear_wgrad(dyb, g)
+            db2 = K.colsum(dym) if has_b2 else None
+            dw1 = K.linear_wgrad(dpre, h2)
+            db1 = K.colsum(dpre) if has_b1 else None
+        else:
+            dw2 = K.linear_wgrad(dyb, g)
+            db2 = K.colsum(dym) if has_b2 else None
+            dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_MUL_AUX, aux=pre)
+            dw1 = K.linear_wgrad(dpre, h2)
+            db1 = K.colsum(dpre) if has_b1 else None
+            dh2 = K.linear_dgrad(dpre, w1_b)
         dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b)
         # attention half (dx1r: the gradient behind the residual dropout)
         if pr > 0.0:

@@ -45,6 +45,21 @@ struct MlpArgs {
   int ntiles;
 };
 
+struct MlpBwdArgs {
+  const bf16_t* X;    // [M, D] ln_2 output (bf16)
+  const bf16_t* dY;   // [M, D] gradient of the MLP output (bf16)
+  const bf16_t* W1;   // [HID, D] c_fc.weight (bf16)
+  const bf16_t* W2T;  // [HID, D] c_proj.weight^T (bf16)
+  const float* b1;    // [HID] or null
+  bf16_t* G;          // [M, HID] GELU(pre) (bf16)
+  bf16_t* dP;         // [M, HID] d pre (bf16)
+  float* dXf;         // [M, D] dX (f32), or
+  bf16_t* dXb;        // [M, D] dX (bf16)
+  int dx_f32;
+  int64_t M;
+  int HID;
+};
+
 typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
 typedef short s16x4m __attribute__((ext_vector_type(4)));
 typedef short s16x8m __attribute__((ext_vector_type(8)));
@@ -245,6 +260,142 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- backward (recompute)
+// The training backward of the fused MLP: the hidden is recomputed, never read from HBM.
+// Per token row x (ln_2 output, bf16) and upstream gradient dy (bf16):
+//   pre  = x W1^T + b1        g = GELU(pre)          (hidden unit i: c_fc row i)
+//   dH   = dy W2              dpre = dH * GELU'(pre)
+//   dX   = dpre W1                                    (-> the ln_2 backward)
+// and the two [M, HID] operands of the weight gradients, g (for dW2 = dy^T g) and dpre
+// (for dW1 = dpre^T x, db1 = colsum dpre), are written once (bf16).  Same structure as
+// the forward: a wave owns 32 token rows with x and dy held in registers as B operands,
+// the hidden is walked in 32-unit chunks whose W1 / W2T images ride a 2-slot LDS-DMA
+// ring; per chunk
+//   S^T  = W1_j . x^T,  dH^T = W2T_j . dy^T        (hidden on registers, tokens on lanes)
+//   dp   = dH * GELU'(S + b1), g = GELU(S + b1)     (one v_exp + v_rcp per element)
+//   dX  += dp . W1_j                                (dp packed to bf16 IS the A operand; B:
+//                                                    transposed reads of the same W1_j image)
+// g and dp leave through the wave's LDS strip as 64-B row pieces.  One wave per SIMD (the
+// x / dy fragments and the dX accumulator are 256 registers).
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
+  constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave strips
+  __shared__ float b1s[8192];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  float* stg = stg_all[wave];
+  bf16_t* stb = reinterpret_cast<bf16_t*>(stg);  // bf16 view: [32 rows][32 units] g, then dp
+  retire_loads();
+  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
+  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  __syncthreads();  // b1s
+  int g = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform
+    bf16x8m xf[KS], df[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    const bool more_tiles = t0 + TR < re;
+    for (int j = 0; j < NC; ++j, ++g) {
+      wait_vm<0>();
+      __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
+      asm volatile("" ::: "memory");
+      if (j + 1 < NC || more_tiles) {
+        const int jn = j + 1 < NC ? j + 1 : 0;
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      }
+      if (!active) continue;
+      const unsigned char* w1 = img[g & 1][0];
+      const unsigned char* w2 = img[g & 1][1];
+      f32x16 S = f32x16{}, dH = f32x16{};
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        S = mfma32(mlp_row_frag<D>(w1, lane, k), xf[k], S);
+        dH = mfma32(mlp_row_frag<D>(w2, lane, k), df[k], dH);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // g straight into the strip (8-B writes of 4 consecutive units), dp kept for the MFMA
+      float dp[16];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+        float gv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float gd;
+          gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
+          dp[4 * m + e] = dH[4 * m + e] * gd;
+        }
+        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * m + 4 * h) =
+            uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
+      }
+      const bf16x8m d0 = mlp_pack(dp), d1 = mlp_pack(dp + 8);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] = mfma32(d0, mlp_tr_frag<D>(w1, lane, 0, t), acc[t]);
+        acc[t] = mfma32(d1, mlp_tr_frag<D>(w1, lane, 1, t), acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // g and dp of the chunk: [32 tokens][32 units] bf16 through the strip (8-B writes of
+      // 4 consecutive units), then 16-B row pieces: lane -> row l / 4 (+ 16), piece l % 4
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * m + 4 * h) =
+            uint2{pack_bf16x2(dp[4 * m], dp[4 * m + 1]), pack_bf16x2(dp[4 * m + 2], dp[4 * m + 3])};
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
+        const int64_t row = rb + rl;
+        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + pc);
+        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + pc);
+        if (row < lim) {
+          *reinterpret_cast<u32x4*>(a.G + row * a.HID + 32 * j + pc) = vg;
+          *reinterpret_cast<u32x4*>(a.dP + row * a.HID + 32 * j + pc) = vd;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (!active) continue;
+    // dX [32 tokens][D]: each 32-column tile through the strip, 16-B pieces out
+    const int pr = lane >> 3, pc = 4 * (lane & 7);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) stg[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r32] = acc[t][i];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t row = rb + pr + 8 * m;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stg + (pr + 8 * m) * 32 + pc);
+        if (row < lim) {
+          if (a.dx_f32) {
+            *reinterpret_cast<f32x4*>(a.dXf + row * D + 32 * t + pc) = v;
+          } else {
+            *reinterpret_cast<uint2*>(a.dXb + row * D + 32 * t + pc) =
+                uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -297,6 +448,31 @@ extern "C" int lthm_mlp_fwd(const void* X, int64_t M, int32_t D, int32_t HID, co
   if (D == 256) { if (nw == 8) LTHM_MLPF(256, 8); else LTHM_MLPF(256, 4); }
   else { if (nw == 8) LTHM_MLPF(128, 8); else LTHM_MLPF(128, 4); }
 #undef LTHM_MLPF
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_mlp_bwd(const void* X, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                            const float* b1, const void* W2T, void* dX, int32_t dx_dtype, void* G, void* dP,
+                            void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && M >= 0);
+  LTHM_REQUIRE(X && dY && W1 && W2T && dX && G && dP && (dx_dtype == LTHM_F32 || dx_dtype == LTHM_BF16));
+  LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)dY % 16) == 0 && ((uintptr_t)W1 % 16) == 0 &&
+               ((uintptr_t)W2T % 16) == 0 && ((uintptr_t)b1 % 16) == 0 && ((uintptr_t)dX % 16) == 0 &&
+               ((uintptr_t)G % 16) == 0 && ((uintptr_t)dP % 16) == 0);
+  if (M == 0) return 0;
+  MlpBwdArgs a;
+  a.X = (const bf16_t*)X; a.dY = (const bf16_t*)dY; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1; a.G = (bf16_t*)G; a.dP = (bf16_t*)dP;
+  a.dx_f32 = dx_dtype == LTHM_F32;
+  a.dXf = (float*)dX; a.dXb = (bf16_t*)dX;
+  a.M = M; a.HID = HID;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int NW = 4;
+  const int64_t ntiles = (M + 32 * NW - 1) / (32 * NW);
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());
+  if (D == 256) hipLaunchKernelGGL((mlp_bwd_k<256, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((mlp_bwd_k<128, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

@@ -508,6 +508,30 @@ def mlp_fwd(x2d, w1_b, b1, w2t_b, b2, res1=None, res2=None):
     return out
 
 
+def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
+    """Backward of the fused MLP with the hidden recomputed (lthm_mlp_bwd): -> (dx [M, D],
+    g [M, HID] = GELU(pre) bf16, dpre [M, HID] bf16).  x2d / dy2d [M, D] bf16."""
+    require_gpu(x2d, dy2d, w1_b, w2t_b)
+    M, D = x2d.shape
+    HID = w1_b.shape[0]
+    _check(x2d.dtype == torch.bfloat16 and dy2d.dtype == torch.bfloat16 and w1_b.dtype == torch.bfloat16
+           and w2t_b.dtype == torch.bfloat16, "mlp_bwd takes bf16 x / dy / weights")
+    _check(mlp_supported(D, HID), f"fused MLP does not take D={D} HID={HID}")
+    _check(tuple(dy2d.shape) == (M, D) and tuple(w1_b.shape) == (HID, D) and tuple(w2t_b.shape) == (HID, D),
+           "mlp_bwd: shapes")
+    for t in (x2d, dy2d, w1_b, w2t_b, b1):
+        _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_bwd: contiguous 16-B aligned operands")
+    _check(b1 is None or (b1.dtype == torch.float32 and b1.numel() == HID), "mlp_bwd: f32 b1")
+    dev = x2d.device
+    dx = torch.empty((M, D), dtype=dx_dtype, device=dev)
+    g = torch.empty((M, HID), dtype=torch.bfloat16, device=dev)
+    dpre = torch.empty((M, HID), dtype=torch.bfloat16, device=dev)
+    call("lthm_mlp_bwd", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dx), dcode(dx),
+         ptr(g), ptr(dpre), stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd",
+         _work=6.0 * M * D * HID, _unit="flop")
+    return dx, g, dpre
+
+
 # ----------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
     """amax: optional int32 [1] device word (zeroed by the caller) that receives the

@@ -1854,6 +1854,7 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
     LTHM_CHECK_LAUNCH();
     static const int xcd = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : 0;
     a.xcd_order = xcd;
+    if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
     hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
