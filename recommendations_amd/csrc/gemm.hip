@@ -995,6 +995,116 @@ __global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int
       }
 }
 
+// ---------------------------------------------------------------- 256 x 256 forward / dgrad GEMM
+// Both operands K-contiguous (Y = X W^T, dX = dY W^T on a W^T copy) at K > 256, where the
+// persistent kernel's resident B slab no longer fits and its 128 x 128 tile re-reads the
+// LDS per flop at one compute wave per SIMD: the ranker MLPs (K = 2,176 / 1,024 / 512,
+// M = 65,536) and the C5 encoder forms (K 512 / 2,048).  A workgroup of 8 waves owns one
+// 256 x 256 tile of C (4 x 2 waves, 64 x 128 each: 128 accumulator registers per lane);
+// all 8 waves stream 32-k stages of A and B (256 rows x 64 B each, 16 KiB) into a 4-deep
+// LDS ring by LDS-DMA, retired by counted vmcnt waits + one barrier per stage.  Image rows
+// are 64 B with the 16-B chunk c of row r at slot c ^ (3 (r >> 2) & 3): conflict-free for
+// the 16x16x32 operand reads (ds_read_b128 lane groups).  The epilogue restages each
+// wave's 16-row slices through the (drained) ring and runs the generic 8-wide epilogue
+// (bias, activations / their gradients, aux, residuals).  Grid order: XCD-contiguous tiles,
+// the tiles of one row panel adjacent (each A panel fetched once per XCD).
+constexpr int BT_NST = 4, BT_BK = 32;
+constexpr int BT_SUB = 256 * 64;  // one operand stage (256 rows x 32 k), 16 KiB
+struct BtSmem {
+  unsigned char ring[BT_NST][2][BT_SUB];  // 128 KiB: [stage][A, B]
+};
+
+__device__ __forceinline__ int bt_off(int r, int c) { return r * 64 + ((c ^ ((3 * (r >> 2)) & 3)) << 4); }
+
+__global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) BtSmem sh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nblk = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int64_t m0 = (int64_t)(lid / tiles_n) * 256, n0 = (int64_t)(lid % tiles_n) * 256;
+  const int S = (int)(g.K / BT_BK);
+  // stage st: A pieces 0..15, B pieces 0..15 (1 KiB = 16 rows x 64 B each); wave w issues
+  // A w, w + 8 and B w, w + 8.  Lane l lands at row 16 d + l / 4, slot l % 4 and so loads
+  // chunk slot ^ f(row) (the swizzle is an involution in the chunk index).
+  auto issue = [&](int st) {
+    const int64_t k = (int64_t)st * BT_BK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool isA = u < 2;
+      const int d = wave + 8 * (u & 1);
+      const int row = 16 * d + (lane >> 2);
+      const int ch = (lane & 3) ^ ((3 * (row >> 2)) & 3);
+      const bf16_t* P = isA ? g.A : g.B;
+      const int64_t ld = isA ? g.lda : g.ldb, rows = isA ? g.M : g.N;
+      const int64_t gr = (isA ? m0 : n0) + row;
+      const void* src = gr < rows ? (const void*)(P + gr * ld + k + ch * 8) : (const void*)gemm_zero16;
+      glds16(src, sh.ring[st % BT_NST][isA ? 0 : 1] + d * 1024);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;  // rows wm * 64 .., cols wn * 128 ..
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  retire_loads();
+  for (int st = 0; st < BT_NST - 1 && st < S; ++st) issue(st);
+  const int r16 = lane & 15, c4 = lane >> 4;
+  for (int s = 0; s < S; ++s) {
+    // issued: 0 .. min(S-1, s+NST-2); step s must have landed (4 DMAs per wave and stage)
+    const int behind = min(S - 1, s + BT_NST - 2) - s;
+    if (behind >= 2) wait_vm<8>();
+    else if (behind == 1) wait_vm<4>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the stage being freed are done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + BT_NST - 1 < S) issue(s + BT_NST - 1);  // into the stage step s-1 freed
+    const unsigned char* sa = sh.ring[s % BT_NST][0];
+    const unsigned char* sb = sh.ring[s % BT_NST][1];
+    bf16x8v af[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af[i] = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(sa + bt_off(wm * 64 + i * 16 + r16, c4)));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8v bfr =
+          __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(sb + bt_off(wn * 128 + j * 16 + r16, c4)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: every wave's ring reads are done before the ring becomes the staging area
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  constexpr int LDP = 132;  // staging row pitch (floats)
+  float* stg = reinterpret_cast<float*>(&sh.ring[0][0][0]) + wave * 16 * LDP;
+  const int cq = (lane & 15) * 8;  // this lane's 8 columns of the wave's 128
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[((lane >> 4) * 4 + r) * LDP + j * 16 + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int lr = (lane >> 4) + 4 * u;
+      const int64_t row = m0 + wm * 64 + i * 16 + lr;
+      const int64_t col0 = n0 + wn * 128 + cq;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + lr * LDP + cq);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + lr * LDP + cq + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
+      if (row < g.M && col0 < g.N) epilogue8(g, v, row, col0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -1015,6 +1125,16 @@ static int lthm_gemm_ps_mode() {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("LTHM_GEMM_PS");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode;
+}
+
+// 256 x 256 big-K kernel: 1 when eligible (default), 0 never (LTHM_GEMM_BT=0, A/B)
+static int lthm_gemm_bt_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("LTHM_GEMM_BT");
     mode = (e && e[0] == '0') ? 0 : 1;
   }
   return mode;
@@ -1140,6 +1260,16 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
 #undef LTHM_PS8
     LTHM_CHECK_LAUNCH();
     return 0;
+  }
+  if (lthm_gemm_bt_mode() && d->ab_dtype != LTHM_FP8_E4M3 && ka && kb && splits == 1 && d->batch == 1 &&
+      g.fast_ok && d->K > 4 * BK &&
+      d->K % BT_BK == 0 && d->M >= 4096 && d->N >= 256) {
+    const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
+    GemmArgs gb = g;
+    gb.ws = nullptr;
+    hipLaunchKernelGGL(gemm_bt_k, dim3(tm * tn), dim3(512), 0, s, gb, tm, tn);
+    LTHM_CHECK_LAUNCH();
+    return amax_after();
   }
   if (lthm_gemm_ps_mode() && epi >= 0 && ka && splits == 1 && d->batch == 1 && g.fast_ok && d->K % BK == 0 &&
       d->K > 0 && d->N % 8 == 0 && tiles_n <= per_xcd && (int64_t)tiles_m * tiles_n >= 4 * 8 * per_xcd) {

@@ -2,7 +2,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PARITY_LOG=gpurun_out/r04b_parity.json
-timeout -k 10 900 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_encoder.py tests/test_gpu_wrapper_api.py tests/test_gpu_lthm_step_golden.py tests/test_gpu_loss.py tests/test_gpu_loss_golden.py tests/test_gpu_lthm.py -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r04b_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_gemm_bigk.py tests/test_gpu_mlp.py tests/test_gpu_encoder.py tests/test_gpu_wrapper_api.py tests/test_gpu_lthm_step_golden.py tests/test_gpu_loss.py tests/test_gpu_loss_golden.py tests/test_gpu_lthm.py -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r04b_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r04b_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest exit $rc: stopping"; exit $rc; fi
 [ $rc -eq 1 ] && grep -E "^FAILED|Error" gpurun_out/r04b_tests.log | head -20
