@@ -1534,6 +1534,7 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
   const int hh = lane >> 5;
   const float it = 1.f / a.tau, c1 = it * LOG2E;
   const bool live = x < g.n;
+  const int xlo = live ? xsq * g.L : -(1 << 30);  // first column of x's sequence
   const uint64_t hmask = hh ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full;  // this half's columns
   const int ntile = (g.n + 63) / 64;
   auto stage = [&](int t) {
@@ -1610,6 +1611,17 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
           for (int j = 0; j < 4; ++j) {
             const int v = 4 * qd + j, yl = 32 * ib + 8 * qd + 4 * hh + j, y = ys0 + yl;
             const float sv = acc[ib][v];
+#if defined(CL_SP2)
+            // branch-free: x's own sequence is [xlo, xlo + L); pads / beyond-n carry cv = -inf
+            if (y == x) pv = sv * it;
+            const bool same = (unsigned)(y - xlo) < (unsigned)g.L;
+            const bool keep = live && cv[j] != -INFINITY && (!same || y == x);
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, cv[j]));
+            const float p = keep ? e : 0.f;
+            Z += p;
+            cn += keep ? 1 : 0;
+            rk += (keep && y != x && sv > thr) ? 1 : 0;
+#else
             if (y == x) pv = sv * it;
             const int ysq = y < g.n ? seq_of(g, y) : -1;
             const bool keep = live && cv[j] != -INFINITY && (ysq != xsq || y == x);
@@ -1620,6 +1632,7 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
               cn += 1;
               rk += (y != x && sv > thr) ? 1 : 0;
             }
+#endif
             acc[ib][v] = p;
           }
         }
