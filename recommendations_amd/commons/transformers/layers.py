@@ -656,18 +656,26 @@ class CVEFn(torch.autograd.Function):
         d.emb_out, d.rows_out, d.emb_dtype = ptr(emb32), ptr(rows), dcode(emb32)
         call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
         ctx.save_for_backward(rows)
-        segs, so = [], 0
+        segs, cmods, so = [], [], 0
         for j, m in enumerate(mods):
             segs += K.cve_segments(m.n_proj, m.num_bins + 1, so, d.mod_row_off[j])
+            cmods.append((so, m.n_proj, d.mod_row_off[j], m.num_bins + 1))
             so += m.n_proj
-        ctx.meta = ([t.shape for t in tables], R, shp, segs)
+        ctx.meta = ([t.shape for t in tables], R, shp, segs, cmods)
         return emb32.view(*shp[:-1], Dout)
 
     @staticmethod
     def backward(ctx, dy):
         (rows,) = ctx.saved_tensors
-        shapes, R, shp, segs = ctx.meta
-        dtab = K.segmented_table_bwd(rows, dy.contiguous().view(rows.shape[0], -1).float(), R, segs)
+        shapes, R, shp, segs, cmods = ctx.meta
+        dyc = dy.contiguous().view(rows.shape[0], -1).float()
+        D = dyc.shape[1]
+        if (D in (16, 32, 64, 128, 256) or D % 256 == 0) and len(cmods) <= 16:
+            # the one-hot MFMA reduction (the product tower's; C4 DenseMapper: 65,536 rows x 16
+            # projections into 336 rows, where the LDS scatter-add ran at 36 GB/s)
+            dtab = K.cve_table_bwd(rows, dyc, R, cmods)
+        else:
+            dtab = K.segmented_table_bwd(rows, dyc, R, segs)
         out, r = [], 0
         for s in shapes:
             out.append(dtab[r:r + s[0]])

@@ -1177,6 +1177,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32<NW>& sh, f32x16 (&dacc)[4
   const float it = 1.f / a.tau, c1 = it * LOG2E;
   const float* shift = a.diag;
   const int ntile = (g.n + 63) / 64;
+  const int xlo = xr.sq >= 0 ? xr.sq * g.L : -(1 << 30);  // first image row of the register row's sequence
   auto stage = [&](int t) {
     const int buf = t % CL_NB32, y0 = t * 64;
     cur.stage(sh.r.img[buf], g.n, w, lane);
@@ -1238,6 +1239,27 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32<NW>& sh, f32x16 (&dacc)[4
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const int yl = 32 * ib + 8 * (v >> 2) + 4 * hh + (v & 3), y = ys0 + yl;
+#if defined(CL_SP2)
+          // branch-free: the register row's own sequence is [xlo, xlo + L); beyond-n image rows
+          // are zero (ROWS) or carry weight 0 (COLS)
+          const bool same = (unsigned)(y - xlo) < (unsigned)g.L;
+          const bool keep = xr.live && (!same || xr.x == y);
+          const bool dg = xr.x == y;
+          float ds;
+          if (ROWS) {
+            const float yq = FIXED ? 0.f : sh.r.m0[cb][w][yl] * LOG2E;
+            float t = __builtin_fmaf(acc[ib][v], c1, xr.sh + (dg ? 0.f : yq));
+            if (!FIXED) t = fminf(t, xr.cap);
+            const float e = __builtin_amdgcn_exp2f(t) - (dg ? xr.w : 0.f);
+            ds = (keep && xr.w != 0.f) ? e : 0.f;
+          } else {
+            const float ysh = sh.r.m0[cb][w][yl], yw = sh.r.m1[cb][w][yl];
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][v], c1, ysh + (dg ? 0.f : xr.q))) -
+                            (dg ? yw : 0.f);
+            ds = (keep && yw != 0.f) ? e : 0.f;
+          }
+          acc[ib][v] = ds;
+#else
           const int ysq = y < g.n ? seq_of(g, y) : -1;
           const bool keep = xr.live && (ysq != xr.sq || xr.x == y);
           float ds = 0.f;
@@ -1255,6 +1277,7 @@ __device__ __forceinline__ void cl_bwd32_head(ClTile32<NW>& sh, f32x16 (&dacc)[4
                    (xr.x == y ? yw : 0.f);
           }
           acc[ib][v] = ds;
+#endif
         }
       }
       // dacc[32 x 128] += dS[32 x 32] . img[32 x 128] of this image block: k-step ks = 2 ib + hf
