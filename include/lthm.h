@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 30 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 31 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -194,6 +194,13 @@ int lthm_mlp_supported(int32_t D, int32_t HID);
 int lthm_mlp_fwd(const void* x, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
                  const void* W2T, const float* b2, const float* res1, const float* res2, float* out,
                  void* stream);
+/* lthm_mlp_fwd with ln_2 fused into the prologue: the input rows are LayerNorm(x) (x f32 [M, D],
+ * ln_w / ln_b f32 [D], eps 1e-5, ln_b NULL for bias=False); h_out (bf16 [M, D]), mean and rstd
+ * (f32 [M]) receive the LayerNorm output and statistics for the backward (each may be NULL).
+ * Replaces the block's x + mlp(ln_2(x)) (commons/transformers/layers.py:371, :142-149). */
+int lthm_mlp_fwd_ln(const float* x, const float* ln_w, const float* ln_b, int64_t M, int32_t D, int32_t HID,
+                    const void* W1, const float* b1, const void* W2T, const float* b2, const float* res1,
+                    const float* res2, float* out, void* h_out, float* mean, float* rstd, void* stream);
 /* The training backward with the hidden RECOMPUTED (never stored by the forward):
  * pre = x W1^T + b1; G = GELU(pre); dP = (dY W2) * GELU'(pre); dX = dP W1.  dY bf16 [M, D]
  * (gradient of the MLP output), dX [M, D] in dx_dtype (LTHM_F32 / LTHM_BF16), G and dP bf16

@@ -128,12 +128,12 @@ class TransformerBlockFn(torch.autograd.Function):
                            seed + 1, res1=x2)
         else:
             x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None)
-        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
         if not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]) and (infer or _MLP_TRAIN):
-            # the fused MLP keeps the [M, 4d] hidden on chip; in training the backward
-            # recomputes it (K.mlp_bwd), so neither the hidden nor GELU' is stored
+            # ln_2 and the MLP in one kernel: the [M, 4d] hidden stays on chip; in training the
+            # backward recomputes it (K.mlp_bwd), so neither the hidden nor GELU' is stored
             w2t_b = w2_b.t().contiguous()
-            out = K.mlp_fwd(h2, w1_b, _f(b1), w2t_b, _f(b2), res1=x1, res2=x2 if double_residual else None)
+            out, h2, mu2, rs2 = K.mlp_fwd_ln(x1, ln2w.detach(), _f(ln2b), w1_b, _f(b1), w2t_b, _f(b2), res1=x1,
+                                             res2=x2 if double_residual else None, save=not infer)
             if infer:
                 return out.view(B, T, d)
             ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, _f(b1), w2t_b,
@@ -143,6 +143,7 @@ class TransformerBlockFn(torch.autograd.Function):
             ctx.mop = mop
             ctx.fused_mlp = True
             return out.view(B, T, d)
+        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
         if fp8:

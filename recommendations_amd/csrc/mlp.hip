@@ -43,6 +43,13 @@ struct MlpArgs {
   int64_t M;
   int HID;
   int ntiles;
+  // ln_2 fused in the prologue (ln_w non-null): X is unused, the input rows are LN(x32)
+  const float* x32;   // [M, D] f32 (the block's x1; usually also res1)
+  const float* ln_w;  // [D]
+  const float* ln_b;  // [D] or null
+  bf16_t* h_out;      // [M, D] bf16: the LN output, saved for the backward (or null)
+  float* mean;        // [M] (or null)
+  float* rstd;        // [M] (or null)
 };
 
 struct MlpBwdArgs {
@@ -181,30 +188,100 @@ __device__ __forceinline__ void mlp_load_x(const bf16_t* X, int64_t row, bool ok
     xf[s] = __builtin_bit_cast(bf16x8m, ok ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0u, 0u, 0u, 0u});
 }
 
+// ln_2 in the prologue: lane (row r, half h) holds columns 16 s + 8 h .. + 7 of its row (the B
+// operand layout); the row's statistics combine the two halves through one lane exchange.
+// Same two-pass arithmetic as ln_fwd_v4_k (mean, then the mean squared deviation, eps 1e-5).
+template <int D, int KS>
+__device__ __forceinline__ void mlp_ld8f(const float* p, bool ok, float (&v)[8]) {
+  const f32x4 lo = ok ? *reinterpret_cast<const f32x4*>(p) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 hi = ok ? *reinterpret_cast<const f32x4*>(p + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+}
+// ln_2 in the prologue: lane (row r, half h) holds columns 16 s + 8 h .. + 7 of its row (the B
+// operand layout); the row's statistics combine the two halves through one lane exchange.
+// Same two-pass arithmetic as ln_fwd_v4_k (mean, then the mean squared deviation, eps 1e-5);
+// the lane's half-row is streamed three times (sum, deviations, normalise: L1 / L2 hits after
+// the first) instead of held in 128 registers.
+template <int D, int KS>
+__device__ __forceinline__ void mlp_load_ln(const MlpArgs& a, const float* lw, const float* lb, int64_t row, bool ok,
+                                            int h, bf16x8m (&xf)[KS]) {
+  const float* p = a.x32 + (ok ? row : 0) * D + 8 * h;
+  float s = 0.f;
+#pragma unroll 4
+  for (int k = 0; k < KS; ++k) {
+    float v[8];
+    mlp_ld8f<D, KS>(p + 16 * k, ok, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[e];
+  }
+  s += __shfl_xor(s, 32, 64);
+  const float mu = s / (float)D;
+  float q = 0.f;
+#pragma unroll 4
+  for (int k = 0; k < KS; ++k) {
+    float v[8];
+    mlp_ld8f<D, KS>(p + 16 * k, ok, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dd = v[e] - mu;
+      q += dd * dd;
+    }
+  }
+  q += __shfl_xor(q, 32, 64);
+  const float rs = 1.f / sqrtf(q / (float)D + 1e-5f);
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    float v[8], y[8];
+    mlp_ld8f<D, KS>(p + 16 * k, ok, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 16 * k + 8 * h + e;
+      y[e] = (v[e] - mu) * rs * lw[c] + (lb ? lb[c] : 0.f);
+    }
+    u32x4 w4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w4[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]);
+    xf[k] = __builtin_bit_cast(bf16x8m, w4);
+    if (ok && a.h_out) *reinterpret_cast<u32x4*>(a.h_out + row * D + 16 * k + 8 * h) = w4;
+  }
+  if (ok && h == 0) {
+    if (a.mean) a.mean[row] = mu;
+    if (a.rstd) a.rstd[row] = rs;
+  }
+}
+
 template <int D, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
   __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
   __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave epilogue strips
-  extern __shared__ float b1s[];                                         // [HID] b1, then [D] b2
+  extern __shared__ float b1s[];                                         // [HID] b1, [D] b2, [D] ln w, [D] ln b
   float* b2s = b1s + a.HID;
+  float* lws = b2s + D;
+  float* lbs = lws + D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int NC = a.HID / 32;
   const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
   if (rs >= re) return;  // uniform
   for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
   for (int i = tid; i < D; i += NTH) b2s[i] = a.b2 ? a.b2[i] : 0.f;
+  if (a.ln_w)
+    for (int i = tid; i < D; i += NTH) {
+      lws[i] = a.ln_w[i];
+      lbs[i] = a.ln_b ? a.ln_b[i] : 0.f;
+    }
   float* stg = stg_all[wave];
   retire_loads();
   mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
   mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
-  __syncthreads();  // b1s / b2s
+  __syncthreads();  // b1s / b2s / ln
   int g = 0;
   for (int64_t t0 = rs; t0 < re; t0 += TR) {
     const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
     const bool active = rb < lim;  // wave-uniform: a wave past the tile's rows only streams weights
     bf16x8m xf[KS];
-    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    if (a.ln_w) mlp_load_ln<D, KS>(a, lws, a.ln_b ? lbs : nullptr, rb + r32, rb + r32 < lim, h, xf);
+    else mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
@@ -426,6 +503,25 @@ extern "C" int lthm_mlp_supported(int32_t D, int32_t HID) {
   return (D == 128 || D == 256) && HID >= 32 && HID % 32 == 0 && HID <= 8192;
 }
 
+static int mlp_fwd_launch(MlpArgs a, int D, void* stream);
+
+extern "C" int lthm_mlp_fwd_ln(const float* x, const float* ln_w, const float* ln_b, int64_t M, int32_t D,
+                               int32_t HID, const void* W1, const float* b1, const void* W2T, const float* b2,
+                               const float* res1, const float* res2, float* out, void* h_out, float* mean,
+                               float* rstd, void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && M >= 0);
+  LTHM_REQUIRE(x && ln_w && W1 && W2T && out);
+  LTHM_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)W1 % 16) == 0 && ((uintptr_t)W2T % 16) == 0 &&
+               ((uintptr_t)b1 % 16) == 0 && ((uintptr_t)h_out % 16) == 0);
+  if (M == 0) return 0;
+  MlpArgs a{};
+  a.X = nullptr; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1; a.b2 = b2; a.res1 = res1; a.res2 = res2; a.out = out;
+  a.M = M; a.HID = HID;
+  a.x32 = x; a.ln_w = ln_w; a.ln_b = ln_b; a.h_out = (bf16_t*)h_out; a.mean = mean; a.rstd = rstd;
+  return mlp_fwd_launch(a, D, stream);
+}
+
 extern "C" int lthm_mlp_fwd(const void* X, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
                             const void* W2T, const float* b2, const float* res1, const float* res2, float* out,
                             void* stream) {
@@ -434,12 +530,18 @@ extern "C" int lthm_mlp_fwd(const void* X, int64_t M, int32_t D, int32_t HID, co
   LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)W1 % 16) == 0 && ((uintptr_t)W2T % 16) == 0 &&
                ((uintptr_t)b1 % 16) == 0);
   if (M == 0) return 0;
-  MlpArgs a;
+  MlpArgs a{};
   a.X = (const bf16_t*)X; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
   a.b1 = b1; a.b2 = b2; a.res1 = res1; a.res2 = res2; a.out = out;
   a.M = M; a.HID = HID;
+  return mlp_fwd_launch(a, D, stream);
+}
+
+static int mlp_fwd_launch(MlpArgs a, int D, void* stream) {
+  const int64_t M = a.M;
+  const int HID = a.HID;
   hipStream_t s = (hipStream_t)stream;
-  const size_t dyn = (size_t)(HID + D) * 4;
+  const size_t dyn = (size_t)(HID + 3 * D) * 4;
   const int nw = mlp_fwd_waves();
   a.ntiles = (int)((M + 32 * nw - 1) / (32 * nw));
   const int per_cu = 1;

@@ -508,6 +508,33 @@ def mlp_fwd(x2d, w1_b, b1, w2t_b, b2, res1=None, res2=None):
     return out
 
 
+def mlp_fwd_ln(x32, ln_w, ln_b, w1_b, b1, w2t_b, b2, res1=None, res2=None, save=True):
+    """res1 [+ res2] + c_proj(GELU(c_fc(LayerNorm(x32)))) in one kernel (lthm_mlp_fwd_ln) ->
+    (out f32 [M, D], h bf16 [M, D], mean, rstd) -- h / mean / rstd None unless ``save``."""
+    require_gpu(x32, w1_b, w2t_b)
+    M, D = x32.shape
+    HID = w1_b.shape[0]
+    _check(x32.dtype == torch.float32 and w1_b.dtype == torch.bfloat16 and w2t_b.dtype == torch.bfloat16,
+           "mlp_fwd_ln takes f32 x and bf16 weights")
+    _check(mlp_supported(D, HID), f"fused MLP does not take D={D} HID={HID}")
+    _check(tuple(w1_b.shape) == (HID, D) and tuple(w2t_b.shape) == (HID, D), "mlp_fwd_ln: weight shapes")
+    for t in (x32, w1_b, w2t_b, b1, b2, res1, res2, ln_w, ln_b):
+        _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_fwd_ln: contiguous aligned operands")
+    for t, n in ((b1, HID), (b2, D), (ln_w, D), (ln_b, D)):
+        _check(t is None or (t.dtype == torch.float32 and t.numel() == n), "mlp_fwd_ln: f32 vectors")
+    for t in (res1, res2):
+        _check(t is None or (t.dtype == torch.float32 and t.numel() == M * D), "mlp_fwd_ln: f32 [M, D] residuals")
+    dev = x32.device
+    out = torch.empty((M, D), dtype=torch.float32, device=dev)
+    h = torch.empty((M, D), dtype=torch.bfloat16, device=dev) if save else None
+    mean = torch.empty(M, dtype=torch.float32, device=dev) if save else None
+    rstd = torch.empty(M, dtype=torch.float32, device=dev) if save else None
+    call("lthm_mlp_fwd_ln", ptr(x32), ptr(ln_w), ptr(ln_b), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(b2),
+         ptr(res1), ptr(res2), ptr(out), ptr(h), ptr(mean), ptr(rstd), stream(),
+         _key=(_GEMM_TAG[-1] + ":mlp_fwd") if _GEMM_TAG else "mlp_fwd", _work=4.0 * M * D * HID, _unit="flop")
+    return out, h, mean, rstd
+
+
 def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
     """Backward of the fused MLP with the hidden recomputed (lthm_mlp_bwd): -> (dx [M, D],
     g [M, HID] = GELU(pre) bf16, dpre [M, HID] bf16).  x2d / dy2d [M, D] bf16."""

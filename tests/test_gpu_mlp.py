@@ -126,3 +126,26 @@ def test_mlp_bwd_recompute_vs_fp64(dev, M, D, HID, bias, dxf32):
     check(f"mlp bwd dX ({M},{D},{HID})", relerr(dx.cpu().double(), xd.grad), 1e-2)
     check(f"mlp bwd dW1 ({M},{D},{HID})", relerr(dw1.cpu().double(), w1d.grad), 1e-2)
     check(f"mlp bwd dW2 ({M},{D},{HID})", relerr(dw2.cpu().double(), w2d.grad), 1e-2)
+
+
+@pytest.mark.parametrize("M,D,HID,lnb", [(4096, 256, 1024, False), (1000, 128, 512, True), (77, 256, 96, True)])
+def test_mlp_fwd_ln_fused(dev, M, D, HID, lnb):
+    """lthm_mlp_fwd_ln (ln_2 in the MLP kernel's prologue) against the separate LayerNorm kernel
+    + lthm_mlp_fwd: the saved LN output, mean and rstd (1e-5 / one bf16 rounding apart: the row
+    sums add in another order) and the block output (2e-3 relative Frobenius, as the MLP)."""
+    from recommendations_amd import kernels as K
+    _, w1, w2, b1, b2, r1, r2 = _operands(M, D, HID, 11 * M + D, True)
+    g = torch.Generator().manual_seed(M + 1)
+    x = torch.randn(M, D, generator=g) * 3 + 0.5
+    lw = 1.0 + 0.2 * torch.randn(D, generator=g)
+    lb = 0.1 * torch.randn(D, generator=g) if lnb else None
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    out, h, mu, rs = K.mlp_fwd_ln(d(x), d(lw), d(lb), d(w1), d(b1), d(w2.T.contiguous()), d(b2), res1=d(x), res2=d(r2))
+    h_ref, mu_ref, rs_ref = K.layernorm_fwd(d(x), d(lw), d(lb))
+    out_ref = K.mlp_fwd(h_ref, d(w1), d(b1), d(w2.T.contiguous()), d(b2), res1=d(x), res2=d(r2))
+    torch.cuda.synchronize()
+    check(f"ln-fused mean ({M},{D})", relerr(mu.cpu(), mu_ref.cpu()), 1e-5)
+    check(f"ln-fused rstd ({M},{D})", relerr(rs.cpu(), rs_ref.cpu()), 1e-5)
+    check(f"ln-fused h ({M},{D})", relerr(h.float().cpu(), h_ref.float().cpu()), 2e-3)
+    base = (x + r2).double()
+    check(f"ln-fused out ({M},{D},{HID})", relerr(out.cpu().double() - base, out_ref.cpu().double() - base), 2e-3)
