@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 31 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 32 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -209,6 +209,10 @@ int lthm_mlp_fwd_ln(const float* x, const float* ln_w, const float* ln_b, int64_
  * commons/transformers/layers.py:279-284's backward. */
 int lthm_mlp_bwd(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1, const float* b1,
                  const void* W2T, void* dX, int32_t dx_dtype, void* G, void* dP, void* stream);
+/* The same recompute without dX (G and dP only; two waves per SIMD): dX = dP W1 then runs on the
+ * GEMM.  HID <= 4096. */
+int lthm_mlp_bwd_hidden(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                        const float* b1, const void* W2T, void* G, void* dP, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm (commons/transformers/layers.py:142-149, eps 1e-5)               */

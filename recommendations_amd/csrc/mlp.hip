@@ -473,6 +473,89 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
   }
 }
 
+// The split backward: the same recompute without the dX accumulator (dX = dP W1 then runs on
+// the GEMM), so the x / dy fragments (128 registers) leave room for two waves per SIMD.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
+  constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, TR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) bf16_t stb_all[NW][2 * 32 * 32];  // per-wave g / dp strips
+  __shared__ float b1s[4096];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  bf16_t* stb = stb_all[wave];
+  retire_loads();
+  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
+  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  __syncthreads();  // b1s
+  int g = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform
+    bf16x8m xf[KS], df[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
+    const bool more_tiles = t0 + TR < re;
+    for (int j = 0; j < NC; ++j, ++g) {
+      wait_vm<0>();
+      __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
+      asm volatile("" ::: "memory");
+      if (j + 1 < NC || more_tiles) {
+        const int jn = j + 1 < NC ? j + 1 : 0;
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      }
+      if (!active) continue;
+      const unsigned char* w1 = img[g & 1][0];
+      const unsigned char* w2 = img[g & 1][1];
+      f32x16 S = f32x16{}, dH = f32x16{};
+      bf16x8m fa = mlp_row_frag<D>(w1, lane, 0), fb = mlp_row_frag<D>(w2, lane, 0);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int kn = k + 1 < KS ? k + 1 : k;
+        const bf16x8m na = mlp_row_frag<D>(w1, lane, kn), nb = mlp_row_frag<D>(w2, lane, kn);
+        S = mfma32(fa, xf[k], S);
+        dH = mfma32(fb, df[k], dH);
+        fa = na;
+        fb = nb;
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+        float gv[4], dv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float gd;
+          gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
+          dv[e] = dH[4 * m + e] * gd;
+        }
+        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * m + 4 * h) = uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
+        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * m + 4 * h) =
+            uint2{pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3])};
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
+        const int64_t row = rb + rl;
+        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + pc);
+        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + pc);
+        if (row < lim) {
+          *reinterpret_cast<u32x4*>(a.G + row * a.HID + 32 * j + pc) = vg;
+          *reinterpret_cast<u32x4*>(a.dP + row * a.HID + 32 * j + pc) = vd;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -575,6 +658,28 @@ extern "C" int lthm_mlp_bwd(const void* X, const void* dY, int64_t M, int32_t D,
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());
   if (D == 256) hipLaunchKernelGGL((mlp_bwd_k<256, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
   else hipLaunchKernelGGL((mlp_bwd_k<128, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_mlp_bwd_hidden(const void* X, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                                   const float* b1, const void* W2T, void* G, void* dP, void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && HID <= 4096 && M >= 0);
+  LTHM_REQUIRE(X && dY && W1 && W2T && G && dP);
+  LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)dY % 16) == 0 && ((uintptr_t)W1 % 16) == 0 &&
+               ((uintptr_t)W2T % 16) == 0 && ((uintptr_t)b1 % 16) == 0 && ((uintptr_t)G % 16) == 0 &&
+               ((uintptr_t)dP % 16) == 0);
+  if (M == 0) return 0;
+  MlpBwdArgs a{};
+  a.X = (const bf16_t*)X; a.dY = (const bf16_t*)dY; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1; a.G = (bf16_t*)G; a.dP = (bf16_t*)dP;
+  a.M = M; a.HID = HID;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int NW = 8;
+  const int64_t ntiles = (M + 32 * NW - 1) / (32 * NW);
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());
+  if (D == 256) hipLaunchKernelGGL((mlp_bwdp_k<256, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((mlp_bwdp_k<128, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

@@ -535,6 +535,10 @@ def mlp_fwd_ln(x32, ln_w, ln_b, w1_b, b1, w2t_b, b2, res1=None, res2=None, save=
     return out, h, mean, rstd
 
 
+# LTHM_MLP_BWD=fused: one kernel also accumulates dX (one wave per SIMD); default: the split form
+_MLP_BWD_SPLIT = os.environ.get("LTHM_MLP_BWD", "split") != "fused"
+
+
 def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
     """Backward of the fused MLP with the hidden recomputed (lthm_mlp_bwd): -> (dx [M, D],
     g [M, HID] = GELU(pre) bf16, dpre [M, HID] bf16).  x2d / dy2d [M, D] bf16."""
@@ -550,9 +554,15 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
         _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_bwd: contiguous 16-B aligned operands")
     _check(b1 is None or (b1.dtype == torch.float32 and b1.numel() == HID), "mlp_bwd: f32 b1")
     dev = x2d.device
-    dx = torch.empty((M, D), dtype=dx_dtype, device=dev)
     g = torch.empty((M, HID), dtype=torch.bfloat16, device=dev)
     dpre = torch.empty((M, HID), dtype=torch.bfloat16, device=dev)
+    if _MLP_BWD_SPLIT and HID <= 4096:
+        # recompute kernel for G / dP at two waves per SIMD, then dX = dP W1 on the GEMM
+        call("lthm_mlp_bwd_hidden", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(g), ptr(dpre),
+             stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd", _work=4.0 * M * D * HID,
+             _unit="flop")
+        return linear_dgrad(dpre, w1_b, out_dtype=dx_dtype), g, dpre
+    dx = torch.empty((M, D), dtype=dx_dtype, device=dev)
     call("lthm_mlp_bwd", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dx), dcode(dx),
          ptr(g), ptr(dpre), stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd",
          _work=6.0 * M * D * HID, _unit="flop")

@@ -149,3 +149,21 @@ def test_mlp_fwd_ln_fused(dev, M, D, HID, lnb):
     check(f"ln-fused h ({M},{D})", relerr(h.float().cpu(), h_ref.float().cpu()), 2e-3)
     base = (x + r2).double()
     check(f"ln-fused out ({M},{D},{HID})", relerr(out.cpu().double() - base, out_ref.cpu().double() - base), 2e-3)
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_mlp_bwd_forms_agree(dev, split, monkeypatch):
+    """The split backward (lthm_mlp_bwd_hidden + the dX GEMM) and the one-kernel form give the same
+    G / dP bit for bit and dX within one bf16 rounding (the dX sums run in another order)."""
+    from recommendations_amd import kernels as K
+    M, D, HID = 4100, 256, 1024
+    x, w1, w2, b1, _, _, _ = _operands(M, D, HID, 99, True)
+    dy = torch.randn(M, D, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16)
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    monkeypatch.setattr(K, "_MLP_BWD_SPLIT", True)
+    dx1, g1, p1 = K.mlp_bwd(d(x), d(dy), d(w1), d(b1), d(w2.T.contiguous()), dx_dtype=torch.float32)
+    monkeypatch.setattr(K, "_MLP_BWD_SPLIT", False)
+    dx2, g2, p2 = K.mlp_bwd(d(x), d(dy), d(w1), d(b1), d(w2.T.contiguous()), dx_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2) and torch.equal(p1, p2)
+    check("mlp bwd split vs fused dX", relerr(dx1.cpu(), dx2.cpu()), 1e-5)
