@@ -1569,16 +1569,47 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
   stage(0);
   if (ntile > 1) stage(1);
   if (ntile > 2) stage(2);
+#if defined(CL_EXP) && CL_EXP >= 6
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+#endif
   for (int tI = 0; tI < ntile; ++tI) {
+#if defined(CL_EXP) && CL_EXP >= 6
+    // skeleton experiment: no staging / waits / barriers (the first tiles are reused)
+    const int cb = tI % 3, y0 = tI * 64;
+#else
     const int cb = tI % CL_NB32, y0 = tI * 64;
     if (tI + 2 < ntile) wait_vm<2 * PT>();
     else if (tI + 1 < ntile) wait_vm<PT>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (tI + 3 < ntile) stage(tI + 3);
+#endif
     const unsigned char* img = sh.r.img[cb];
     const float* colb = sh.r.m0[cb][w];
     f32x16 acc[2];
+#if defined(CL_PF)
+    // the two image blocks' S chains interleaved (no back-to-back dependent MFMA), each
+    // k-step's A fragments read one step ahead behind a compiler fence
+    {
+      acc[0] = f32x16{};
+      acc[1] = f32x16{};
+      auto rd = [&](int ib, int s2) {
+        return __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ib * 8192 + roff[s2]));
+      };
+      bf16x8v a0 = rd(0, 0), a1 = rd(1, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) {
+        const int sn = s2 + 1 < 8 ? s2 + 1 : s2;
+        const bf16x8v n0 = rd(0, sn), n1 = rd(1, sn);
+        acc[0] = mfma32(a0, qf[s2], acc[0]);
+        acc[1] = mfma32(a1, qf[s2], acc[1]);
+        a0 = n0;
+        a1 = n1;
+        asm volatile("" ::: "memory");
+      }
+    }
+#else
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
 #pragma unroll
@@ -1589,6 +1620,7 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
         acc[ib] = mfma32(af, qf[s], acc[ib]);
       }
     }
+#endif
 #if defined(CL_EXP) && CL_EXP >= 2
     const bool special = false;
 #else
@@ -1661,6 +1693,28 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
         }
       }
       // dacc[32 x 128] += p[32 x 32] . img[32 x 128] (as cl_bwd32_head)
+#if defined(CL_PF)
+      {
+        const f32x16& pvv = acc[ib];
+        const bf16x8v af0 = __builtin_bit_cast(bf16x8v, u32x4{pk_bf16(pvv[0], pvv[1]), pk_bf16(pvv[2], pvv[3]),
+                                                              pk_bf16(pvv[4], pvv[5]), pk_bf16(pvv[6], pvv[7])});
+        const bf16x8v af1 = __builtin_bit_cast(bf16x8v, u32x4{pk_bf16(pvv[8], pvv[9]), pk_bf16(pvv[10], pvv[11]),
+                                                              pk_bf16(pvv[12], pvv[13]), pk_bf16(pvv[14], pvv[15])});
+        const int k0 = 2 * ib * 4096, k1 = (2 * ib + 1) * 4096;
+        bf16x8v b0 = tr_frag32(img, toff[0][0] + k0, toff[0][1] + k0), b1 = tr_frag32(img, toff[0][0] + k1, toff[0][1] + k1);
+#pragma unroll
+        for (int nd = 0; nd < 4; ++nd) {
+          const int nn = nd + 1 < 4 ? nd + 1 : nd;
+          const bf16x8v q0 = tr_frag32(img, toff[nn][0] + k0, toff[nn][1] + k0);
+          const bf16x8v q1 = tr_frag32(img, toff[nn][0] + k1, toff[nn][1] + k1);
+          dacc[nd] = mfma32(af0, b0, dacc[nd]);
+          dacc[nd] = mfma32(af1, b1, dacc[nd]);
+          b0 = q0;
+          b1 = q1;
+          asm volatile("" ::: "memory");
+        }
+      }
+#else
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         const int ks = 2 * ib + hf, o = 8 * hf;
@@ -1674,6 +1728,7 @@ __device__ __forceinline__ void cl_fr32_head(ClTile32<4>& sh, f32x16 (&dacc)[4],
           dacc[nd] = mfma32(af, bfr, dacc[nd]);
         }
       }
+#endif
     }
   }
 }

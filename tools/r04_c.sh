@@ -22,3 +22,6 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/r04c_prof -o run -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-gather --no-kernel-timing > gpurun_out/r04c_prof.log 2>&1 || exit 1
 python3 tools/rocpd_stats.py $(find gpurun_out/r04c_prof -name "*.db" | head -1) 40 > gpurun_out/r04c_kernel_stats.txt
 head -25 gpurun_out/r04c_kernel_stats.txt
+VARIANTS="base pf sp2 pfsp2 exp5 pfexp5 exp6 pfexp6" bash tools/r04_loss_exp.sh > gpurun_out/r04c_lossexp.log 2>&1; echo "lossexp rc=$?"
+grep -E "^==|cl_fr32|cl_bwd32" gpurun_out/r04c_lossexp.log
+LTHM_LIB_PATH=$GRAFT_REPO_ROOT/recommendations_amd/liblthm_hip_pfsp2.so timeout -k 10 300 python -u -m pytest tests/test_gpu_loss_golden.py tests/test_gpu_loss.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r04c_pfsp2_golden.log 2>&1; echo "pfsp2 goldens rc=$?"; tail -1 gpurun_out/r04c_pfsp2_golden.log
