@@ -1016,6 +1016,12 @@ struct BtSmem {
 
 __device__ __forceinline__ int bt_off(int r, int c) { return r * 64 + ((c ^ ((3 * (r >> 2)) & 3)) << 4); }
 
+// F8: A and B are e4m3 bytes with K and the leading dims in 2-byte units (the geometry of the
+// bf16 kernel: a stage is 64 k of fp8); one v_mfma_scale_f32_16x16x128_f8f6f4 (unit block
+// scales) consumes TWO stages: lane group kg takes 16 B of stage s and 16 B of stage s + 1
+// (the same k permutation for A and B, so the dot products are unchanged); the per-tensor
+// scales fold into alpha.
+template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) BtSmem sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1048,8 +1054,43 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   retire_loads();
-  for (int st = 0; st < BT_NST - 1 && st < S; ++st) issue(st);
   const int r16 = lane & 15, c4 = lane >> 4;
+  if constexpr (F8) {
+    // stage pairs (p = 2 stages) double-buffered in the 4-stage ring
+    for (int st = 0; st < 2 && st < S; ++st) issue(st);
+    for (int s = 0; s < S; s += 2) {
+      // this pair landed: stages s, s + 1 (issued: 0 .. min(S - 1, s + 1)); 4 DMAs per wave and stage
+      wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < S) issue(s + 2);
+      if (s + 3 < S) issue(s + 3);
+      const unsigned char* sa0 = sh.ring[s % BT_NST][0];
+      const unsigned char* sb0 = sh.ring[s % BT_NST][1];
+      const unsigned char* sa1 = sh.ring[(s + 1) % BT_NST][0];
+      const unsigned char* sb1 = sh.ring[(s + 1) % BT_NST][1];
+      i32x8v af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + r16;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(sa0 + bt_off(r, c4));
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(sa1 + bt_off(r, c4));
+        af[i] = i32x8v{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = wn * 128 + j * 16 + r16;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(sb0 + bt_off(r, c4));
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(sb1 + bt_off(r, c4));
+        const i32x8v bfr = {(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr, acc[i][j], 0, 0, 0, 127, 0, 127);
+      }
+    }
+  } else {
+  for (int st = 0; st < BT_NST - 1 && st < S; ++st) issue(st);
   for (int s = 0; s < S; ++s) {
     // issued: 0 .. min(S-1, s+NST-2); step s must have landed (4 DMAs per wave and stage)
     const int behind = min(S - 1, s + BT_NST - 2) - s;
@@ -1074,6 +1115,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
       for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
     }
   }
+  }
+  const float alpha = F8 ? g.alpha * *g.sa * *g.sb : g.alpha;
   // epilogue: every wave's ring reads are done before the ring becomes the staging area
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1097,7 +1140,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
       const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + lr * LDP + cq + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
+      for (int e = 0; e < 8; ++e) v[e] *= alpha;
       if (row < g.M && col0 < g.N) epilogue8(g, v, row, col0, 0, 0);
     }
     __builtin_amdgcn_wave_barrier();
@@ -1241,6 +1284,15 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     GemmArgs g8 = g;
     g8.K = d->K / 2; g8.lda = d->lda / 2; g8.ldb = d->ldb / 2;
     g8.sa = d->a_scale; g8.sb = d->b_scale;
+    if (lthm_gemm_bt_mode() && d->K > 256 && d->K % 128 == 0 && d->M >= 4096 && d->N >= 256 && !d->amax_out) {
+      // 256 x 256 tiles (the persistent kernel's 128 x 128 tile re-reads the LDS per flop at K >= 512)
+      const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
+      g8.ws = nullptr;
+      g8.amax = nullptr;
+      hipLaunchKernelGGL(gemm_bt_k<true>, dim3(tm * tn), dim3(512), 0, s, g8, tm, tn);
+      LTHM_CHECK_LAUNCH();
+      return 0;
+    }
     const int R = per_xcd / tiles_n;
     dim3 grid(8 * R * tiles_n);
     const bool bres = g8.K <= 4 * BK;
@@ -1267,7 +1319,7 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     GemmArgs gb = g;
     gb.ws = nullptr;
-    hipLaunchKernelGGL(gemm_bt_k, dim3(tm * tn), dim3(512), 0, s, gb, tm, tn);
+    hipLaunchKernelGGL(gemm_bt_k<false>, dim3(tm * tn), dim3(512), 0, s, gb, tm, tn);
     LTHM_CHECK_LAUNCH();
     return amax_after();
   }

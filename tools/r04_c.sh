@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PARITY_LOG=gpurun_out/r04c_parity.json
-timeout -k 10 300 python -u -m pytest tests/test_gpu_lthm.py tests/test_gpu_wrapper_api.py tests/test_gpu_mlp.py -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/r04c_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_lthm.py tests/test_gpu_wrapper_api.py tests/test_gpu_mlp.py tests/test_gpu_fp8.py tests/test_gpu_gemm_bigk.py -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/r04c_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r04c_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-hbm-gather > gpurun_out/r04c_bench.log 2>&1 || { tail -20 gpurun_out/r04c_bench.log; exit 1; }
