@@ -468,7 +468,11 @@ def main():
                                 + (", fp8 e4m3 forward encoder GEMMs" if cfgd.get("fp8") else "")
                                 + (f", {cfgd['mbs']}-sequence loss mini-batches" if cfgd.get("mbs") else "")),
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": cfgd.get("T"),
-                   "activation_checkpointing": cfgd["ckpt"], "distinct_batches": nb,
+                   "activation_checkpointing": cfgd["ckpt"],
+                   "activation_checkpointing_note": ("the reference yaml (model/lthm.yaml:53) recomputes every block in "
+                                                     "the backward; this line runs without it unless --checkpointing "
+                                                     "(a memory knob the 288 GB part does not need)"),
+                   "distinct_batches": nb,
                    "item_lookup": ("one step ahead on a side stream (Encoder.prefetch after the backward is "
                                    "enqueued), "
                                    "inside the timed loop"
