@@ -69,6 +69,8 @@ def _grad_bf16(g32: torch.Tensor) -> torch.Tensor:
 # training through the fused MLP (forward hidden on chip, backward recomputes it); LTHM_MLP_TRAIN=0
 # restores the stored-hidden chain (c_fc GEMM with the GELU' aux, c_proj GEMM, two dgrad GEMMs)
 _MLP_TRAIN = os.environ.get("LTHM_MLP_TRAIN", "1") == "1"
+# ln_2 inside the fused MLP kernel (LTHM_MLP_LN=0: the LayerNorm kernel, then the MLP kernel)
+_MLP_LN = os.environ.get("LTHM_MLP_LN", "1") == "1"
 
 
 class TransformerBlockFn(torch.autograd.Function):
@@ -132,8 +134,12 @@ class TransformerBlockFn(torch.autograd.Function):
             # ln_2 and the MLP in one kernel: the [M, 4d] hidden stays on chip; in training the
             # backward recomputes it (K.mlp_bwd), so neither the hidden nor GELU' is stored
             w2t_b = w2_b.t().contiguous()
-            out, h2, mu2, rs2 = K.mlp_fwd_ln(x1, ln2w.detach(), _f(ln2b), w1_b, _f(b1), w2t_b, _f(b2), res1=x1,
-                                             res2=x2 if double_residual else None, save=not infer)
+            if _MLP_LN:
+                out, h2, mu2, rs2 = K.mlp_fwd_ln(x1, ln2w.detach(), _f(ln2b), w1_b, _f(b1), w2t_b, _f(b2), res1=x1,
+                                                 res2=x2 if double_residual else None, save=not infer)
+            else:
+                h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+                out = K.mlp_fwd(h2, w1_b, _f(b1), w2t_b, _f(b2), res1=x1, res2=x2 if double_residual else None)
             if infer:
                 return out.view(B, T, d)
             ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, _f(b1), w2t_b,

@@ -1284,7 +1284,7 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     GemmArgs g8 = g;
     g8.K = d->K / 2; g8.lda = d->lda / 2; g8.ldb = d->ldb / 2;
     g8.sa = d->a_scale; g8.sb = d->b_scale;
-    if (lthm_gemm_bt_mode() && d->K > 256 && d->K % 128 == 0 && d->M >= 4096 && d->N >= 256 && !d->amax_out) {
+    if (lthm_gemm_bt_mode() && d->K > 256 && d->K % 128 == 0 && d->M >= 4096 && d->N >= 512 && !d->amax_out) {
       // 256 x 256 tiles (the persistent kernel's 128 x 128 tile re-reads the LDS per flop at K >= 512)
       const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
       g8.ws = nullptr;
@@ -1315,7 +1315,9 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   }
   if (lthm_gemm_bt_mode() && d->ab_dtype != LTHM_FP8_E4M3 && ka && kb && splits == 1 && d->batch == 1 &&
       g.fast_ok && d->K > 4 * BK &&
-      d->K % BT_BK == 0 && d->M >= 4096 && d->N >= 256) {
+      d->K % BT_BK == 0 && d->M >= 4096 && d->N >= 512) {
+    // (N = 256 stays on the persistent kernel: C2 dX / qkv-dgrad forms ran 0.45 ms here against
+    // its ~0.4, HBM-bound either way)
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     GemmArgs gb = g;
     gb.ws = nullptr;
