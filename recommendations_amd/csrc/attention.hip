@@ -35,6 +35,7 @@ struct AttnArgs {
   int B;
   const float* mask;         // additive [., ., T, T] or null (VALU kernels only)
   int64_t m_bs, m_hs, m_rs;
+  int tail;                  // attn_bwd32_k: the last query as a vector pass (bwd32_tail_mode)
 };
 
 __device__ __forceinline__ const float* mask_head(const AttnArgs& a, int b, int h) {
@@ -856,7 +857,7 @@ __device__ __forceinline__ void store_accT32(const f32x16& x, float scale, bf16_
 // the wave's units over the NW waves, longest first: unit u < nt is the rows unit of query
 // tile u, unit nt + j the columns unit of key tile j (cost: tiles visited + 1)
 template <int NW>
-__device__ __forceinline__ uint32_t lpt_units(int nt, bool causal, int wave) {
+__device__ __forceinline__ uint32_t lpt_units(int nt, bool causal, int wave, bool tail = false) {
   int load[NW] = {};
   uint32_t mine = 0;
   for (int c = nt; c >= 1; --c)  // descending cost; causal: rows tile c - 1 and columns tile nt - c
@@ -870,6 +871,13 @@ __device__ __forceinline__ uint32_t lpt_units(int nt, bool causal, int wave) {
       load[w] += cost;
       if (w == wave) mine |= 1u << u;
     }
+  if (tail) {  // the tail unit (bit 2 nt), about two tile visits, on the least loaded wave
+    int w = 0;
+#pragma unroll
+    for (int j = 1; j < NW; ++j)
+      if (load[j] < load[w]) w = j;
+    if (w == wave) mine |= 1u << (2 * nt);
+  }
   return mine;
 }
 
@@ -883,7 +891,16 @@ struct Bwd32Smem {
   const float *bfw, *brv, *lse, *dlt;
   float* dbias;
   int ne;
+  const float *tp, *tds;  // tail query's P and dS per key (bwd32_tail_mode), else null
 };
+
+// Causal T' = 32 n + 1 (C2: T' = 129, the history plus one token): the last query row would
+// take a tile of its own, a third of the tile visits for one row.  Instead the units cover
+// rows / keys [0, T' - 1) and the last query q* = T' - 1 runs as a vector pass: its P / dS
+// per key into LDS (and its bias-gradient diagonal), dQ[q*] and dK / dV of key q* (only q*
+// sees it) in a small extra unit, and the rank-1 terms dS[q*][k] Q[q*], P[q*][k] dO[q*]
+// added to the columns units' accumulators before they store.
+__host__ __device__ __forceinline__ bool bwd32_tail_mode(int T, int causal) { return causal && T > 32 && (T & 31) == 1; }
 
 // rows unit: dQ of query tile i (and the bias gradient of its tiles)
 template <bool EDGE>
@@ -906,13 +923,14 @@ __device__ __forceinline__ void rows_math(f32x16& st, const f32x16& pt, const fl
 
 // G: Q / dO fragments from global memory, once per query tile (the rows kernel of long T'
 // holds only the K / V images); else re-read per tile from the images
+// Tu: rows / keys the units cover (T', or T' - 1 in the tail mode)
 template <bool G = false>
 __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
-                                           int i, int lane) {
+                                           int i, int lane, int Tu) {
   constexpr float L2E = 1.4426950408889634f;
-  const int T = a.T, nt = (T + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
+  const int T = a.T, nt = (Tu + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
   const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
-  const bool ragged = (T & 31) != 0;
+  const bool ragged = (Tu & 31) != 0;
   const int q0 = 32 * i, q = q0 + r32;
   bf16x8v gq[4], gd[4];
   if constexpr (G) {
@@ -921,7 +939,7 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       u32x4 u = {0u, 0u, 0u, 0u}, v = u;
-      if (q < T) {
+      if (q < Tu) {
         u = *reinterpret_cast<const u32x4*>(qg + (int64_t)q * a.q_ts + 16 * s + 8 * hh);
         v = *reinterpret_cast<const u32x4*>(dg + (int64_t)q * a.o_ts + 16 * s + 8 * hh);
       }
@@ -930,7 +948,7 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
     }
   }
   const float lq = m.lse[q], dl = m.dlt[q];
-  const int kmax = q < T ? (a.causal ? q + 1 : T) : 0;  // keys k < kmax are live for this query
+  const int kmax = q < Tu ? (a.causal ? q + 1 : Tu) : 0;  // keys k < kmax are live for this query
   f32x16 dq[2];
 #pragma unroll
   for (int nd = 0; nd < 2; ++nd)
@@ -1033,11 +1051,11 @@ __device__ __forceinline__ void cols_math(f32x16& sx, f32x16& px, const float* b
 // holds only the Q / dO images)
 template <bool G = false>
 __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
-                                           int j, int lane) {
+                                           int j, int lane, int Tu) {
   constexpr float L2E = 1.4426950408889634f;
-  const int T = a.T, nt = (T + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
+  const int T = a.T, nt = (Tu + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
   const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
-  const bool ragged = (T & 31) != 0;
+  const bool ragged = (Tu & 31) != 0;
   const int k0 = 32 * j, k = k0 + r32;
   bf16x8v gk[4], gv[4];
   if constexpr (G) {
@@ -1046,7 +1064,7 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       u32x4 u = {0u, 0u, 0u, 0u}, v = u;
-      if (k < T) {
+      if (k < Tu) {
         u = *reinterpret_cast<const u32x4*>(kg + (int64_t)k * a.k_ts + 16 * s + 8 * hh);
         v = *reinterpret_cast<const u32x4*>(vg + (int64_t)k * a.v_ts + 16 * s + 8 * hh);
       }
@@ -1055,7 +1073,7 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
     }
   }
   // live queries of this key: [qlo, T)
-  const int qlo = k < T ? (a.causal ? k : 0) : T, span = T - qlo;
+  const int qlo = k < Tu ? (a.causal ? k : 0) : Tu, span = Tu - qlo;
   f32x16 dk[2], dv[2];
 #pragma unroll
   for (int nd = 0; nd < 2; ++nd)
@@ -1101,6 +1119,27 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
       }
     }
   }
+  if (m.tds) {  // tail mode: the last query's rank-1 terms (k < Tu: every lane's key is live)
+    const int qs = T - 1, sw = a32_swz(qs);
+    const float dsk = m.tds[k], pk = m.tp[k];
+#pragma unroll
+    for (int nd = 0; nd < 2; ++nd)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = 32 * nd + 8 * g + 4 * hh, off = qs * 128 + (((e >> 3) ^ sw) << 4) + 8 * hh;
+        const uint2 qv = *reinterpret_cast<const uint2*>(m.IQ + off);
+        const uint2 ov = *reinterpret_cast<const uint2*>(m.IO + off);
+        const float qf[4] = {__uint_as_float(qv.x << 16), __uint_as_float(qv.x & 0xffff0000u),
+                             __uint_as_float(qv.y << 16), __uint_as_float(qv.y & 0xffff0000u)};
+        const float of[4] = {__uint_as_float(ov.x << 16), __uint_as_float(ov.x & 0xffff0000u),
+                             __uint_as_float(ov.y << 16), __uint_as_float(ov.y & 0xffff0000u)};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          dk[nd][4 * g + jj] = fmaf(dsk, qf[jj], dk[nd][4 * g + jj]);
+          dv[nd][4 * g + jj] = fmaf(pk, of[jj], dv[nd][4 * g + jj]);
+        }
+      }
+  }
   bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
   bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
 #pragma unroll
@@ -1110,15 +1149,74 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
   }
 }
 
-__host__ __device__ __forceinline__ int bwd32_timg(int T) { return (T + 7) & ~7; }
-__host__ __device__ __forceinline__ int bwd32_fbytes(int T) {  // float region, 16-byte multiple
-  return (4 * bias_ne(T) + 2 * ((T + 31) & ~31) + ((2 * T + 1 + 3) & ~3)) * 4;
+// the tail query's vector pass (bwd32_tail_mode): P and dS of (q*, k) for every key k <= q*
+// (a thread per key; dot products over the swizzled image rows), stored to tp / tds and as
+// the bias gradient's diagonal q* - k (written once each, before any unit adds to it)
+__device__ __forceinline__ void bwd32_tail_pass(const Bwd32Smem& m, float* tp, float* tds, float* dbias, int T, int tid,
+                                                int nth) {
+  const float c2 = rsqrtf((float)E_BWD32) * 1.4426950408889634f;
+  const int qs = T - 1, sq = a32_swz(qs);
+  const float lq = m.lse[qs], dl = m.dlt[qs];
+  for (int k = tid; k <= qs; k += nth) {
+    const int sk = a32_swz(k);
+    float sc = 0.f, dp = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+      const bf16x8v kf = frag_at(m.IK + k * 128 + ((ch ^ sk) << 4)), vf = frag_at(m.IV + k * 128 + ((ch ^ sk) << 4));
+      const bf16x8v qf = frag_at(m.IQ + qs * 128 + ((ch ^ sq) << 4)), of = frag_at(m.IO + qs * 128 + ((ch ^ sq) << 4));
+      sc += bf8_dot(kf, qf);
+      dp += bf8_dot(vf, of);
+    }
+    const float p = __builtin_amdgcn_exp2f(fmaf(sc, c2, m.bfw[qs - k + T + BPAD] - lq));
+    const float ds = p * (dp - dl);
+    tp[k] = p;
+    tds[k] = ds;
+    dbias[qs - k + T] = ds;
+  }
 }
 
-__host__ __device__ __forceinline__ int bwd32_slack(int T) {  // rows past V for the last tile
-  const int d = ((T + 31) & ~31) - bwd32_timg(T);
+// the tail unit: dQ[q*] = rs sum_k dS[q*][k] K[k] (lane = a column pair, the lane halves split
+// the keys), dK[q*] = rs dS[q*][q*] Q[q*] and dV[q*] = P[q*][q*] dO[q*]
+__device__ __forceinline__ void bwd32_tail_unit(const AttnArgs& a, const Bwd32Smem& m, int b, int h, int lane) {
+  const float rs = rsqrtf((float)E_BWD32);
+  const int T = a.T, qs = T - 1, hh = lane >> 5, c = 2 * (lane & 31);
+  float a0 = 0.f, a1 = 0.f;
+  for (int k = hh; k <= qs; k += 2) {
+    const float d = m.tds[k];
+    const uint32_t kv = *reinterpret_cast<const uint32_t*>(m.IK + k * 128 + (((c >> 3) ^ a32_swz(k)) << 4) + 2 * (c & 7));
+    a0 = fmaf(d, __uint_as_float(kv << 16), a0);
+    a1 = fmaf(d, __uint_as_float(kv & 0xffff0000u), a1);
+  }
+  a0 += __shfl_xor(a0, 32, 64);
+  a1 += __shfl_xor(a1, 32, 64);
+  const int off = qs * 128 + (((c >> 3) ^ a32_swz(qs)) << 4) + 2 * (c & 7);
+  if (hh == 0) {
+    *reinterpret_cast<uint32_t*>(a.dq + b * a.q_bs + h * a.q_hs + (int64_t)qs * a.q_ts + c) = pk_bf16_rne(rs * a0, rs * a1);
+    const uint32_t qv = *reinterpret_cast<const uint32_t*>(m.IQ + off);
+    const float f = rs * m.tds[qs];
+    *reinterpret_cast<uint32_t*>(a.dk + b * a.k_bs + h * a.k_hs + (int64_t)qs * a.k_ts + c) =
+        pk_bf16_rne(f * __uint_as_float(qv << 16), f * __uint_as_float(qv & 0xffff0000u));
+  } else {
+    const uint32_t ov = *reinterpret_cast<const uint32_t*>(m.IO + off);
+    const float f = m.tp[qs];
+    *reinterpret_cast<uint32_t*>(a.dv + b * a.v_bs + h * a.v_hs + (int64_t)qs * a.v_ts + c) =
+        pk_bf16_rne(f * __uint_as_float(ov << 16), f * __uint_as_float(ov & 0xffff0000u));
+  }
+}
+
+__host__ __device__ __forceinline__ int bwd32_timg(int T) { return (T + 7) & ~7; }
+// float region, 16-byte multiple: bias copies, lse, delta, bias gradient, and in the tail mode
+// the tail query's P / dS per key
+__host__ __device__ __forceinline__ int bwd32_fbytes(int T, bool tail = false) {
+  return (4 * bias_ne(T) + 2 * ((T + 31) & ~31) + ((2 * T + 1 + 3) & ~3) + (tail ? 2 * ((T + 3) & ~3) : 0)) * 4;
+}
+
+// rows past V for the last tile (Tu: the rows the units cover)
+__host__ __device__ __forceinline__ int bwd32_slack(int T, int Tu) {
+  const int d = ((Tu + 31) & ~31) - bwd32_timg(T);
   return d > 0 ? d : 0;
 }
+__host__ __device__ __forceinline__ int bwd32_slack(int T) { return bwd32_slack(T, T); }
 
 constexpr int BWD32_NW = 4, BWD32_WPE = 2;  // waves per (b, h); waves per SIMD the registers allow
 
@@ -1126,13 +1224,17 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_WPE, BWD32_WPE))) void attn_bwd32_k(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr float L2E = 1.4426950408889634f;
-  const int T = a.T, Tk = (T + 31) & ~31, nt = Tk / 32, ne = bias_ne(T), Ti = bwd32_timg(T);
+  const int T = a.T, Tk = (T + 31) & ~31, ne = bias_ne(T), Ti = bwd32_timg(T);
+  const bool tail = a.tail != 0;
+  const int Tu = tail ? T - 1 : T, nt = (Tu + 31) >> 5;  // rows / keys of the units
   float* bfw = reinterpret_cast<float*>(smem);  // [2][ne] ascending copies
   float* brv = bfw + 2 * ne;                     // [2][ne] descending copies
   float* lse_s = brv + 2 * ne;                   // [Tk] lse * log2 e (0 past T)
   float* dlt_s = lse_s + Tk;                     // [Tk] delta = dO . O (0 past T)
   float* dbias = dlt_s + Tk;                     // [2T + 1]
-  unsigned char* IK = smem + bwd32_fbytes(T);
+  float* tp = dbias + ((2 * T + 1 + 3) & ~3);    // tail mode: [T] P, [T] dS of the last query
+  float* tds = tp + ((T + 3) & ~3);
+  unsigned char* IK = smem + bwd32_fbytes(T, tail);
   unsigned char* IQ = IK + Ti * 128;
   unsigned char* IO = IQ + Ti * 128;
   unsigned char* IV = IO + Ti * 128;
@@ -1184,25 +1286,30 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_W
       brv[c * ne + y] = (a.table && xr >= 0 && xr <= 2 * T) ? a.table[(int64_t)xr * a.H + h] * L2E : 0.f;
     }
   for (int i = tid; i <= 2 * T; i += 64 * NW) dbias[i] = 0.f;
-  for (int i = tid; i < bwd32_slack(T) * 32; i += 64 * NW) reinterpret_cast<float*>(IV + Ti * 128)[i] = 0.f;
+  for (int i = tid; i < bwd32_slack(T, Tu) * 32; i += 64 * NW) reinterpret_cast<float*>(IV + Ti * 128)[i] = 0.f;
   wait_vm<0>();
   __syncthreads();
-  const Bwd32Smem m{IK, IQ, IO, IV, bfw, brv, lse_s, dlt_s, dbias, ne};
+  const Bwd32Smem m{IK, IQ, IO, IV, bfw, brv, lse_s, dlt_s, dbias, ne, tail ? tp : nullptr, tail ? tds : nullptr};
+  if (tail) {
+    bwd32_tail_pass(m, tp, tds, dbias, T, tid, 64 * NW);
+    __syncthreads();
+  }
   const Frag32Off fo = frag32_off(lane);
-  const uint32_t mine = lpt_units<NW>(nt, a.causal, wave);
+  const uint32_t mine = lpt_units<NW>(nt, a.causal, wave, tail);
   // longest first: the rows unit of tile c - 1 and the columns unit of tile nt - c cost alike
   for (int c = nt; c >= 1; --c) {
-    if (mine & (1u << (c - 1))) bwd32_rows(a, m, fo, b, h, c - 1, lane);
-    if (mine & (1u << (2 * nt - c))) bwd32_cols(a, m, fo, b, h, nt - c, lane);
+    if (mine & (1u << (c - 1))) bwd32_rows(a, m, fo, b, h, c - 1, lane, Tu);
+    if (mine & (1u << (2 * nt - c))) bwd32_cols(a, m, fo, b, h, nt - c, lane, Tu);
   }
+  if (mine & (1u << (2 * nt))) bwd32_tail_unit(a, m, b, h, lane);
   if (a.dtable_part) {
     __syncthreads();
     for (int i = tid; i <= 2 * T; i += 64 * NW) a.dtable_part[((int64_t)b * (2 * T + 1) + i) * a.H + h] = dbias[i];
   }
 }
 
-static size_t bwd32_lds(int T) {
-  return (size_t)bwd32_fbytes(T) + (size_t)(4 * bwd32_timg(T) + bwd32_slack(T)) * 128;
+static size_t bwd32_lds(int T, bool tail) {
+  return (size_t)bwd32_fbytes(T, tail) + (size_t)(4 * bwd32_timg(T) + bwd32_slack(T, tail ? T - 1 : T)) * 128;
 }
 
 // ===========================================================================
@@ -1616,8 +1723,12 @@ static size_t bwd_mfma_lds(int T, int E) {
 template <int E>
 static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   static const bool old_bwd = getenv("LTHM_ATTN_BWD_OLD") && atoi(getenv("LTHM_ATTN_BWD_OLD"));  // A/B switch
+  // LTHM_ATTN_TAIL=0: the last query of T' = 32 n + 1 in tiles like the others (A/B switch)
+  static const bool no_tail = getenv("LTHM_ATTN_TAIL") && getenv("LTHM_ATTN_TAIL")[0] == '0';
   if (E == 64 && bwd && !old_bwd) {
-    hipLaunchKernelGGL(attn_bwd32_k<BWD32_NW>, dim3(B * a.H), dim3(64 * BWD32_NW), bwd32_lds(a.T), s, a);
+    AttnArgs t = a;
+    t.tail = !no_tail && bwd32_tail_mode(a.T, a.causal);
+    hipLaunchKernelGGL(attn_bwd32_k<BWD32_NW>, dim3(B * a.H), dim3(64 * BWD32_NW), bwd32_lds(a.T, t.tail), s, t);
     LTHM_CHECK_LAUNCH();
     return 0;
   }
@@ -1705,8 +1816,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
   for (int i = tid; i < bwd32_slack(T) * 32; i += 64 * NW) reinterpret_cast<float*>(I1 + Ti * 128)[i] = 0.f;
   wait_vm<0>();
   __syncthreads();
-  const Bwd32Smem m = ROWS ? Bwd32Smem{I0, nullptr, nullptr, I1, nullptr, bias, lse_s, dlt_s, dbias, ne}
-                           : Bwd32Smem{nullptr, I0, I1, nullptr, bias, nullptr, lse_s, dlt_s, dbias, ne};
+  const Bwd32Smem m = ROWS ? Bwd32Smem{I0, nullptr, nullptr, I1, nullptr, bias, lse_s, dlt_s, dbias, ne, nullptr, nullptr}
+                           : Bwd32Smem{nullptr, I0, I1, nullptr, bias, nullptr, lse_s, dlt_s, dbias, ne, nullptr, nullptr};
   const Frag32Off fo = frag32_off(lane);
   // tiles over the waves, longest first (rows: query tile t visits t + 1 key tiles; columns:
   // key tile t visits nt - t query tiles)
@@ -1727,8 +1838,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
   for (int c = nt; c >= 1; --c) {
     const int t = ROWS ? c - 1 : nt - c;
     if (!((mk[t >> 5] >> (t & 31)) & 1u)) continue;
-    if (ROWS) bwd32_rows<true>(a, m, fo, b, h, t, lane);
-    else bwd32_cols<true>(a, m, fo, b, h, t, lane);
+    if (ROWS) bwd32_rows<true>(a, m, fo, b, h, t, lane, T);
+    else bwd32_cols<true>(a, m, fo, b, h, t, lane, T);
   }
   if (ROWS && a.dtable_part) {
     __syncthreads();
@@ -1991,7 +2102,7 @@ extern "C" int64_t lthm_attn_bwd_parts(int32_t B, int32_t T) { return attn_parts
 extern "C" int lthm_attn_fwd(const lthm_attn_desc* d, void* stream) {
   LTHM_REQUIRE(check_desc(d) == 0 && d->lse != nullptr && d->out != nullptr);
   if (d->B == 0) return 0;
-  AttnArgs a;
+  AttnArgs a{};
   fill_common(a, d);
   return attn_dispatch(a, d->B, d->E, false, (hipStream_t)stream);
 }
@@ -2000,7 +2111,7 @@ extern "C" int lthm_attn_bwd(const lthm_attn_desc* d, void* stream) {
   LTHM_REQUIRE(check_desc(d) == 0 && d->dout && d->dq && d->dk && d->dv);
   LTHM_REQUIRE(d->k_head_stride != 0 || d->H == 1);  // shared-KV heads: caller expands (see kernels.py)
   if (d->B == 0) return 0;
-  AttnArgs a;
+  AttnArgs a{};
   fill_common(a, d);
   return attn_dispatch(a, d->B, d->E, true, (hipStream_t)stream);
 }

@@ -1173,12 +1173,14 @@ static int lthm_gemm_ps_mode() {
   return mode;
 }
 
-// 256 x 256 big-K kernel: 1 when eligible (default), 0 never (LTHM_GEMM_BT=0, A/B)
+// 256 x 256 big-K kernel: off by default (LTHM_GEMM_BT=1 selects it where eligible).  Measured
+// against the default kernels (profiles/r04d_*): C4 12.66 -> 12.18 M samples/s, C5 5,424 -> 4,664
+// samples/s (C5 forward GEMMs 1.28 -> 2.04 ms bf16, 0.98 -> 1.51 ms fp8 per call)
 static int lthm_gemm_bt_mode() {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("LTHM_GEMM_BT");
-    mode = (e && e[0] == '0') ? 0 : 1;
+    mode = (e && e[0] == '1') ? 1 : 0;
   }
   return mode;
 }

@@ -250,10 +250,12 @@ __device__ __forceinline__ void mlp_load_ln(const MlpArgs& a, const float* lw, c
   }
 }
 
-template <int D, int NW>
+// NS: weight-chunk ring slots (3: two chunks of DMA in flight behind the MFMAs; 2: one)
+template <int D, int NW, int NS>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
-  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
+  constexpr int DPC = 2 * (32 * D / 8) / NTH;  // DMAs per thread and chunk (both images)
+  __shared__ __attribute__((aligned(16))) unsigned char img[NS][2][IMG];  // [stage][W1_j, W2T_j]
   __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave epilogue strips
   extern __shared__ float b1s[];                                         // [HID] b1, [D] b2, [D] ln w, [D] ln b
   float* b2s = b1s + a.HID;
@@ -274,9 +276,16 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   retire_loads();
   mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
   mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  const int64_t ntile_wg = (re - rs + TR - 1) / TR;
+  if (NS == 3 && (NC > 1 || ntile_wg > 1)) {  // chunk 1 (of this tile or the next) into slot 1
+    const int j1 = NC > 1 ? 1 : 0;
+    mlp_dma32<D, NTH>(img[1 % NS][0], a.W1 + (int64_t)j1 * 32 * D, tid);
+    mlp_dma32<D, NTH>(img[1 % NS][1], a.W2T + (int64_t)j1 * 32 * D, tid);
+  }
   __syncthreads();  // b1s / b2s / ln
   int g = 0;
-  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+  int64_t tix = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR, ++tix) {
     const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
     const bool active = rb < lim;  // wave-uniform: a wave past the tile's rows only streams weights
     bf16x8m xf[KS];
@@ -285,19 +294,27 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-    const bool more_tiles = t0 + TR < re;
     for (int j = 0; j < NC; ++j, ++g) {
-      wait_vm<0>();
-      __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
+      // retire chunk g; with 3 slots chunk g + 1 stays in flight (a tile's first step drains:
+      // the x / residual / output accesses were issued behind the DMAs)
+      if (NS == 2 || j == 0) wait_vm<0>();
+      else wait_vm<DPC>();
+      __syncthreads();  // chunk g landed everywhere; every wave is done with chunk g - 1's slot
       asm volatile("" ::: "memory");
-      if (j + 1 < NC || more_tiles) {
-        const int jn = j + 1 < NC ? j + 1 : 0;
-        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
-        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      {
+        // chunk g + NS - 1: of this tile, or the next tile's (same weights, chunk index wraps)
+        const int64_t cg = (int64_t)j + NS - 1;
+        const int64_t tnext = tix + cg / NC;
+        if (tnext < ntile_wg) {
+          const int jn = (int)(cg % NC);
+          unsigned char* dst = img[(g + NS - 1) % NS][0];
+          mlp_dma32<D, NTH>(dst, a.W1 + (int64_t)jn * 32 * D, tid);
+          mlp_dma32<D, NTH>(dst + IMG, a.W2T + (int64_t)jn * 32 * D, tid);
+        }
       }
       if (!active) continue;
-      const unsigned char* w1 = img[g & 1][0];
-      const unsigned char* w2 = img[g & 1][1];
+      const unsigned char* w1 = img[g % NS][0];
+      const unsigned char* w2 = img[g % NS][1];
       // LDS reads one step ahead of their MFMA; the compiler fences keep the unrolled loops
       // from hoisting every read (register pressure: 2 waves per SIMD)
       f32x16 S = f32x16{};
@@ -629,7 +646,12 @@ static int mlp_fwd_launch(MlpArgs a, int D, void* stream) {
   a.ntiles = (int)((M + 32 * nw - 1) / (32 * nw));
   const int per_cu = 1;
   int grid = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count() * per_cu);
-#define LTHM_MLPF(D_, NW_) hipLaunchKernelGGL((mlp_fwd_k<D_, NW_>), dim3(grid), dim3(64 * NW_), dyn, s, a)
+  static const int ns = (getenv("LTHM_MLP_NS") && getenv("LTHM_MLP_NS")[0] == '2') ? 2 : 3;
+#define LTHM_MLPF(D_, NW_)                                                                                 \
+  do {                                                                                                     \
+    if (ns == 3) hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, 3>), dim3(grid), dim3(64 * NW_), dyn, s, a);      \
+    else hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, 2>), dim3(grid), dim3(64 * NW_), dyn, s, a);              \
+  } while (0)
   if (D == 256) { if (nw == 8) LTHM_MLPF(256, 8); else LTHM_MLPF(256, 4); }
   else { if (nw == 8) LTHM_MLPF(128, 8); else LTHM_MLPF(128, 4); }
 #undef LTHM_MLPF

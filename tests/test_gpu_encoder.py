@@ -168,7 +168,7 @@ def test_layernorm_golden(dev):
 @pytest.mark.parametrize("B,T,H,E,causal", [(3, 129, 4, 64, True), (2, 33, 1, 64, True), (4, 17, 2, 32, False),
                                             (2, 200, 2, 64, True), (1, 256, 1, 16, True), (2, 128, 2, 64, True),
                                             (1, 256, 2, 64, False), (2, 64, 2, 128, True), (3, 1, 2, 64, True),
-                                            (2, 47, 3, 32, True),
+                                            (2, 47, 3, 32, True), (2, 225, 2, 64, True), (3, 97, 1, 64, False),
                                             # windowed long-sequence path (T' > 256; C5 has T' = 513)
                                             (2, 513, 2, 64, True), (3, 300, 1, 64, False), (17, 257, 1, 32, True),
                                             (1, 400, 2, 128, True), (20, 520, 1, 64, True)])

@@ -43,7 +43,8 @@ def _ref_fwd(x, w1, w2, b1, b2, res):
 
 @pytest.mark.parametrize("M,D,HID,bias,nres", [(4096, 256, 1024, True, 1), (1000, 256, 1024, True, 2),
                                                (257, 128, 512, False, 1), (33, 256, 96, True, 0),
-                                               (5000, 128, 4096, True, 1)])
+                                               (5000, 128, 4096, True, 1),
+                                               (70000, 128, 32, True, 1)])
 def test_mlp_fwd_vs_fp32(dev, M, D, HID, bias, nres):
     from recommendations_amd import kernels as K
     x, w1, w2, b1, b2, r1, r2 = _operands(M, D, HID, M + D + HID, bias)
