@@ -250,18 +250,27 @@ __device__ __forceinline__ void mlp_load_ln(const MlpArgs& a, const float* lw, c
   }
 }
 
-// NS: weight-chunk ring slots (3: two chunks of DMA in flight behind the MFMAs; 2: one)
-template <int D, int NW, int NS>
+// Weight chunks ride a 3-slot LDS-DMA ring.  STAG (two waves per SIMD): waves NW/2 .. NW - 1
+// share their SIMDs with waves 0 .. NW/2 - 1 and would run in lockstep with them (one barrier per
+// chunk), so both would issue the S chain, then both the GELU, then both the output products.
+// The upper half instead lags half a chunk: at step j it finishes chunk j - 1 (GELU, then
+// Y += H W2T_{j-1}) and then forms S of chunk j, carried across the barrier; its VALU runs
+// beside the partner's S MFMAs and its output MFMAs beside the partner's GELU
+// (MI355X_MICROARCH.md, two waves per SIMD, item 9).  The ring then prefetches one chunk ahead
+// (chunk j - 1 stays readable during step j); without STAG it prefetches two.
+template <int D, int NW, bool STAG>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
+  constexpr int NS = 3, DIST = STAG ? 1 : 2;
   constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
   constexpr int DPC = 2 * (32 * D / 8) / NTH;  // DMAs per thread and chunk (both images)
-  __shared__ __attribute__((aligned(16))) unsigned char img[NS][2][IMG];  // [stage][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) unsigned char img[NS][2][IMG];  // [slot][W1_j, W2T_j]
   __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave epilogue strips
   extern __shared__ float b1s[];                                         // [HID] b1, [D] b2, [D] ln w, [D] ln b
   float* b2s = b1s + a.HID;
   float* lws = b2s + D;
   float* lbs = lws + D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const bool lag = STAG && wave >= NW / 2;  // wave-uniform
   const int NC = a.HID / 32;
   const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
   if (rs >= re) return;  // uniform
@@ -274,15 +283,52 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     }
   float* stg = stg_all[wave];
   retire_loads();
-  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
-  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
   const int64_t ntile_wg = (re - rs + TR - 1) / TR;
-  if (NS == 3 && (NC > 1 || ntile_wg > 1)) {  // chunk 1 (of this tile or the next) into slot 1
-    const int j1 = NC > 1 ? 1 : 0;
-    mlp_dma32<D, NTH>(img[1 % NS][0], a.W1 + (int64_t)j1 * 32 * D, tid);
-    mlp_dma32<D, NTH>(img[1 % NS][1], a.W2T + (int64_t)j1 * 32 * D, tid);
-  }
+  // chunks 0 .. DIST - 1 of the stream (chunk c: index c % NC of tile c / NC)
+#pragma unroll
+  for (int c = 0; c < DIST; ++c)
+    if (c / NC < ntile_wg) {
+      mlp_dma32<D, NTH>(img[c][0], a.W1 + (int64_t)(c % NC) * 32 * D, tid);
+      mlp_dma32<D, NTH>(img[c][1], a.W2T + (int64_t)(c % NC) * 32 * D, tid);
+    }
   __syncthreads();  // b1s / b2s / ln
+  // S^T = W1_j . x^T (hidden units of chunk j on the registers, the token on the lane)
+  auto s_phase = [&](const unsigned char* w1, const bf16x8m(&xf)[KS]) {
+    // LDS reads one step ahead of their MFMA; the compiler fences keep the unrolled loops
+    // from hoisting every read (register pressure: 2 waves per SIMD)
+    f32x16 S = f32x16{};
+    bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const bf16x8m fn = mlp_row_frag<D>(w1, lane, k + 1 < KS ? k + 1 : k);
+      S = mfma32(fa, xf[k], S);
+      fa = fn;
+      asm volatile("" ::: "memory");
+    }
+    return S;
+  };
+  // H = bf16(GELU(S + b1_j)), Y += H . W2T_j
+  auto gelu_out = [&](const f32x16& S, int j, const unsigned char* w2, f32x16(&acc)[NT]) {
+    float hv[16];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hv[4 * m + e] = gelu_tanh(S[4 * m + e] + bb[e]);
+    }
+    const bf16x8m hf0 = mlp_pack(hv), hf1 = mlp_pack(hv + 8);
+    bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int tn = t + 1 < NT ? t + 1 : t;
+      const bf16x8m n0 = mlp_tr_frag<D>(w2, lane, 0, tn), n1 = mlp_tr_frag<D>(w2, lane, 1, tn);
+      acc[t] = mfma32(hf0, b0, acc[t]);
+      acc[t] = mfma32(hf1, b1, acc[t]);
+      b0 = n0;
+      b1 = n1;
+      asm volatile("" ::: "memory");
+    }
+  };
   int g = 0;
   int64_t tix = 0;
   for (int64_t t0 = rs; t0 < re; t0 += TR, ++tix) {
@@ -294,62 +340,170 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    f32x16 S = f32x16{};  // lagging waves: chunk j - 1's S across the barrier
     for (int j = 0; j < NC; ++j, ++g) {
-      // retire chunk g; with 3 slots chunk g + 1 stays in flight (a tile's first step drains:
-      // the x / residual / output accesses were issued behind the DMAs)
-      if (NS == 2 || j == 0) wait_vm<0>();
+      // retire chunk g; at prefetch distance 2 chunk g + 1 stays in flight (a tile's first step
+      // drains: the x / residual / output accesses were issued behind the DMAs)
+      if (DIST == 1 || j == 0) wait_vm<0>();
       else wait_vm<DPC>();
-      __syncthreads();  // chunk g landed everywhere; every wave is done with chunk g - 1's slot
+      __syncthreads();  // chunk g landed everywhere; every wave is done with chunk g + DIST - NS
       asm volatile("" ::: "memory");
       {
-        // chunk g + NS - 1: of this tile, or the next tile's (same weights, chunk index wraps)
-        const int64_t cg = (int64_t)j + NS - 1;
-        const int64_t tnext = tix + cg / NC;
-        if (tnext < ntile_wg) {
+        // chunk g + DIST: of this tile, or the next tile's (same weights, chunk index wraps)
+        const int64_t cg = (int64_t)j + DIST;
+        if (tix + cg / NC < ntile_wg) {
           const int jn = (int)(cg % NC);
-          unsigned char* dst = img[(g + NS - 1) % NS][0];
+          unsigned char* dst = img[(g + DIST) % NS][0];
           mlp_dma32<D, NTH>(dst, a.W1 + (int64_t)jn * 32 * D, tid);
           mlp_dma32<D, NTH>(dst + IMG, a.W2T + (int64_t)jn * 32 * D, tid);
         }
       }
       if (!active) continue;
-      const unsigned char* w1 = img[g % NS][0];
-      const unsigned char* w2 = img[g % NS][1];
-      // LDS reads one step ahead of their MFMA; the compiler fences keep the unrolled loops
-      // from hoisting every read (register pressure: 2 waves per SIMD)
-      f32x16 S = f32x16{};
-      bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const bf16x8m fn = mlp_row_frag<D>(w1, lane, k + 1 < KS ? k + 1 : k);
-        S = mfma32(fa, xf[k], S);
-        fa = fn;
-        asm volatile("" ::: "memory");
-      }
-      float hv[16];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) hv[4 * m + e] = gelu_tanh(S[4 * m + e] + bb[e]);
-      }
-      const bf16x8m hf0 = mlp_pack(hv), hf1 = mlp_pack(hv + 8);
-      bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int tn = t + 1 < NT ? t + 1 : t;
-        const bf16x8m n0 = mlp_tr_frag<D>(w2, lane, 0, tn), n1 = mlp_tr_frag<D>(w2, lane, 1, tn);
-        acc[t] = mfma32(hf0, b0, acc[t]);
-        acc[t] = mfma32(hf1, b1, acc[t]);
-        b0 = n0;
-        b1 = n1;
-        asm volatile("" ::: "memory");
+      if (lag) {
+        if (j > 0) gelu_out(S, j - 1, img[(g + NS - 1) % NS][1], acc);
+        S = s_phase(img[g % NS][0], xf);
+      } else {
+        const f32x16 Sj = s_phase(img[g % NS][0], xf);
+        gelu_out(Sj, j, img[g % NS][1], acc);
+        S = f32x16{};  // nothing carried: keeps the loop-carried S out of this path's live range
       }
     }
     if (active) {
+      if (lag) gelu_out(S, NC - 1, img[(g + NS - 1) % NS][1], acc);  // chunk g - 1: slot kept until step g + 1
       if (a.res1 && a.res2) mlp_fwd_epi<D, NT, 2>(a, acc, b2s, stg, rb, lim, lane);
       else if (a.res1) mlp_fwd_epi<D, NT, 1>(a, acc, b2s, stg, rb, lim, lane);
       else mlp_fwd_epi<D, NT, 0>(a, acc, b2s, stg, rb, lim, lane);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward, software-pipelined
+// One wave per SIMD (4 waves, 512 registers each), the chunk stream software-pipelined inside
+// the wave so that the MFMAs and the GELU VALU of different chunks issue side by side: phase k
+// of a tile runs
+//   S_k   = W1_k . x^T                        (16 MFMAs, one accumulation chain)
+//   H_k-1 = bf16(GELU(S_k-1 + b1))            (VALU, between those MFMAs)
+//   Y    += H_k-2 . W2T_k-2                   (16 MFMAs on the 8 output tiles)
+// for k = 0 .. NC + 1 (the terms whose chunk exists).  Per steady phase 32 MFMAs (1,024 cycles
+// of the matrix pipe) carry ~620 cycles of GELU in their issue gaps.  W1 and W2T chunks ride
+// separate 2-slot LDS-DMA rings, one barrier per phase.  The accumulator starts as the residual
+// (+ b2), loaded straight into the C layout (each half-wave reads a 128-B row piece), and is
+// stored from the C layout the same way: no LDS restaging.
+// one phase of mlp_fwd_pipe_k: DS: S_k = W1_k . x^T into Sp (after its GELU is taken); DG: H =
+// GELU(Sp + b1) into ho (after its products are issued); DO: Y += ho . W2T.  Step i pairs S
+// MFMA i with output MFMA i (tile i / 2, k-step i % 2) and GELU element i; the LDS fragments
+// are read one step ahead (compiler fences keep the unrolled steps from hoisting every read).
+template <int D, bool DS, bool DG, bool DO>
+__device__ __forceinline__ void mlp_pipe_phase(const unsigned char* w1, const unsigned char* w2, const float* bj,
+                                               const bf16x8m (&xf)[D / 16], f32x16 (&acc)[D / 32], f32x16& Sp,
+                                               bf16x8m& ho0, bf16x8m& ho1, int lane) {
+  constexpr int KS = D / 16;
+  f32x16 Sn = f32x16{};
+  float hv[16];
+  bf16x8m fa = {}, fb = {};
+  if (DS) fa = mlp_row_frag<D>(w1, lane, 0);
+  if (DO) fb = mlp_tr_frag<D>(w2, lane, 0, 0);
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    bf16x8m na = fa, nb = fb;
+    if (i + 1 < KS) {
+      if (DS) na = mlp_row_frag<D>(w1, lane, i + 1);
+      if (DO) nb = mlp_tr_frag<D>(w2, lane, (i + 1) & 1, (i + 1) >> 1);
+    }
+    if (DS) Sn = mfma32(fa, xf[i], Sn);
+    if (DO) acc[i >> 1] = mfma32((i & 1) ? ho1 : ho0, fb, acc[i >> 1]);
+    if (DG && i < 16) hv[i] = gelu_tanh(Sp[i] + bj[8 * (i >> 2) + (i & 3)]);
+    fa = na;
+    fb = nb;
+    asm volatile("" ::: "memory");
+  }
+  if (DG) {
+    ho0 = mlp_pack(hv);
+    ho1 = mlp_pack(hv + 8);
+  }
+  if (DS) Sp = Sn;
+}
+
+template <int D, int NRES>
+__global__ __launch_bounds__(256, 1) void mlp_fwd_pipe_k(MlpArgs a) {
+  constexpr int NW = 4, NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
+  static_assert(KS == 2 * NT, "one S MFMA and one output MFMA per step");
+  __shared__ __attribute__((aligned(16))) unsigned char im1[2][IMG];  // W1 chunk ring
+  __shared__ __attribute__((aligned(16))) unsigned char im2[2][IMG];  // W2T chunk ring
+  extern __shared__ float b1s[];                                      // [HID] b1, [D] b2
+  float* b2s = b1s + a.HID;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  for (int i = tid; i < D; i += NTH) b2s[i] = a.b2 ? a.b2[i] : 0.f;
+  retire_loads();
+  const int64_t ntile_wg = (re - rs + TR - 1) / TR;
+  mlp_dma32<D, NTH>(im1[0], a.W1, tid);
+  mlp_dma32<D, NTH>(im2[0], a.W2T, tid);
+  __syncthreads();  // b1s / b2s
+  // W1 / W2T chunk reads so far (ring slot: count & 1), and the chunk / tile of the next read
+  int w1c = 0, w2c = 0, n1c = NC > 1 ? 1 : 0, n1t = NC > 1 ? 0 : 1, n2c = n1c, n2t = n1t;
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform
+    bf16x8m xf[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    f32x16 acc[NT];
+    // acc = b2 + res1 (+ res2) in the C layout: register i of tile t is row rb + 4 h + (i & 3) +
+    // 8 (i >> 2), column 32 t + r32.  One 32-bit offset per register row (rows past the range
+    // clamped to its last row: their values are never stored), the tile in the immediate.
+    const int nrow = (int)min((int64_t)32, lim - rb) - 4 * h;  // live register rows: (i & 3) + 8 (i >> 2) < nrow
+    uint32_t ro[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ro[i] = (uint32_t)(min(rb + 4 * h + (i & 3) + 8 * (i >> 2), lim - 1) * D + r32);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float bb = b2s[32 * t + r32];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float v = bb;
+        if constexpr (NRES >= 1) v += a.res1[ro[i] + 32 * t];
+        if constexpr (NRES >= 2) v += a.res2[ro[i] + 32 * t];
+        acc[t][i] = v;
+      }
+    }
+    f32x16 Sp = f32x16{};       // S of the previous phase's chunk
+    bf16x8m ho0 = {}, ho1 = {};  // H of the chunk two phases back
+    for (int k = 0; k < NC + 2; ++k) {
+      const bool rd1 = k < NC, rd2 = k >= 2;
+      wait_vm<0>();
+      __syncthreads();  // this phase's chunks landed; the slots the DMAs below refill are free
+      asm volatile("" ::: "memory");
+      if (rd1 && n1t < ntile_wg) mlp_dma32<D, NTH>(im1[(w1c + 1) & 1], a.W1 + n1c * 32 * D, tid);
+      if (rd2 && n2t < ntile_wg) mlp_dma32<D, NTH>(im2[(w2c + 1) & 1], a.W2T + n2c * 32 * D, tid);
+      if (active) {
+        // every phase runs all three streams (one code path keeps the register allocation within
+        // the 512 of one wave per SIMD); the edge phases' extra terms are inert: H starts as zero
+        // (the products of phases 0 and 1 add exact zeros, their W2T slot holds finite weights),
+        // the S chains of phases NC and NC + 1 read finite stale or next-tile W1 data and feed
+        // only a GELU whose H is discarded when the tile ends
+        const int jg = min(max(k - 1, 0), NC - 1);  // chunk of the GELU
+        mlp_pipe_phase<D, true, true, true>(im1[w1c & 1], im2[w2c & 1], b1s + 32 * jg + 4 * h, xf, acc, Sp, ho0, ho1,
+                                            lane);
+        if (k == 0) ho0 = ho1 = bf16x8m{};
+      }
+      if (rd1) {
+        ++w1c;
+        if (++n1c == NC) n1c = 0, ++n1t;
+      }
+      if (rd2) {
+        ++w2c;
+        if (++n2c == NC) n2c = 0, ++n2t;
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((i & 3) + 8 * (i >> 2) < nrow) a.out[ro[i] + 32 * t] = acc[t][i];
     }
   }
 }
@@ -509,15 +663,21 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
   mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
   __syncthreads();  // b1s
   int g = 0;
+  // the previous step issued its 4 G / dP stores AFTER the DMA of this step's chunk: a full-tile
+  // wave retires the DMA with vmcnt 4, leaving its stores in flight (vmcnt retires in order)
+  bool st4 = false;
   for (int64_t t0 = rs; t0 < re; t0 += TR) {
     const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
     const bool active = rb < lim;  // wave-uniform
+    const bool full = rb + 32 <= lim;
     bf16x8m xf[KS], df[KS];
     mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
     mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
     const bool more_tiles = t0 + TR < re;
     for (int j = 0; j < NC; ++j, ++g) {
-      wait_vm<0>();
+      if (st4) wait_vm<4>();
+      else wait_vm<0>();
+      st4 = false;
       __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
       asm volatile("" ::: "memory");
       if (j + 1 < NC || more_tiles) {
@@ -567,6 +727,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
           *reinterpret_cast<u32x4*>(a.dP + row * a.HID + 32 * j + pc) = vd;
         }
       }
+      st4 = full;  // every lane stored: exactly 4 store instructions issued
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
     }
@@ -646,11 +807,29 @@ static int mlp_fwd_launch(MlpArgs a, int D, void* stream) {
   a.ntiles = (int)((M + 32 * nw - 1) / (32 * nw));
   const int per_cu = 1;
   int grid = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count() * per_cu);
-  static const int ns = (getenv("LTHM_MLP_NS") && getenv("LTHM_MLP_NS")[0] == '2') ? 2 : 3;
+  // LTHM_MLP_PIPE=1: the software-pipelined one-wave-per-SIMD form (no ln_2 prologue)
+  static const bool pipe = getenv("LTHM_MLP_PIPE") && getenv("LTHM_MLP_PIPE")[0] == '1';
+  if (pipe && !a.ln_w && M * D < ((int64_t)1 << 29)) {
+    a.ntiles = (int)((M + 127) / 128);
+    const int gp = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count());
+    const size_t dynp = (size_t)(HID + D) * 4;
+    if (!a.res1 && a.res2) std::swap(a.res1, a.res2);
+    const int nres = a.res2 ? 2 : a.res1 ? 1 : 0;
+#define LTHM_MLPP(D_)                                                                                      \
+    if (nres == 2) hipLaunchKernelGGL((mlp_fwd_pipe_k<D_, 2>), dim3(gp), dim3(256), dynp, s, a);           \
+    else if (nres == 1) hipLaunchKernelGGL((mlp_fwd_pipe_k<D_, 1>), dim3(gp), dim3(256), dynp, s, a);      \
+    else hipLaunchKernelGGL((mlp_fwd_pipe_k<D_, 0>), dim3(gp), dim3(256), dynp, s, a);
+    if (D == 256) { LTHM_MLPP(256) } else { LTHM_MLPP(128) }
+#undef LTHM_MLPP
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
+  // LTHM_MLP_STAG=1: the 8-wave form with the half-chunk lag of waves 4-7 (A/B)
+  static const bool stag = getenv("LTHM_MLP_STAG") && getenv("LTHM_MLP_STAG")[0] == '1';
 #define LTHM_MLPF(D_, NW_)                                                                                 \
   do {                                                                                                     \
-    if (ns == 3) hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, 3>), dim3(grid), dim3(64 * NW_), dyn, s, a);      \
-    else hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, 2>), dim3(grid), dim3(64 * NW_), dyn, s, a);              \
+    if (stag && NW_ == 8) hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, true>), dim3(grid), dim3(64 * NW_), dyn, s, a); \
+    else hipLaunchKernelGGL((mlp_fwd_k<D_, NW_, false>), dim3(grid), dim3(64 * NW_), dyn, s, a);          \
   } while (0)
   if (D == 256) { if (nw == 8) LTHM_MLPF(256, 8); else LTHM_MLPF(256, 4); }
   else { if (nw == 8) LTHM_MLPF(128, 8); else LTHM_MLPF(128, 4); }

@@ -380,13 +380,15 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   constexpr int SLAB = 32 * D * 2;           // one 32-row bf16 slab
   constexpr int PD = (32 * D / 8 + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // wN / xs rows padded to Din + 4 floats: the 16 rows a ds_read_b128 lane group reads start
+  // on 16 distinct 16-B slots (Din = 32: the 128-B pitch put them on 2, an 8-way conflict)
+  const int Din = d.Din, DinP = Din + 4;
   unsigned char* slab = smem;                                            // [2][SLAB]
-  float* wN = reinterpret_cast<float*>(smem + 2 * SLAB);                // [D][Din] (nn.Linear layout)
-  float* xs = wN + d.Din * D;                                           // [PE_TOK][Din]
-  u32x4* lut = reinterpret_cast<u32x4*>(xs + PE_TOK * d.Din);           // [256] bf16 0/1 octets
-  uint32_t* bits = reinterpret_cast<uint32_t*>(lut + 256);              // [PE_TOK][RBW]
+  float* wN = reinterpret_cast<float*>(smem + 2 * SLAB);                // [D][DinP] (nn.Linear layout)
+  float* xs = wN + DinP * D;                                            // [PE_TOK][DinP]
+  uint2* lut = reinterpret_cast<uint2*>(xs + PE_TOK * DinP);            // [16][32]: nibble -> four bf16 0/1
+  uint32_t* bits = reinterpret_cast<uint32_t*>(lut + 512);              // [PE_TOK][RBW]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int Din = d.Din;
   const int R32 = (R + 31) & ~31;
   const int RBW = pe_rbw(R32);
   const int64_t t0 = (int64_t)blockIdx.x * PE_TOK;
@@ -394,13 +396,14 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
   const int ldt = D * (int)gridDim.y, col0 = D * (int)blockIdx.y;
   const bf16_t* tab = reinterpret_cast<const bf16_t*>(d.tables) + col0;
   // ---- per-block staging: mapper weights, 0/1 octet table, row bitmask, normalised x
-  for (int i = tid; i < Din * D; i += 512) wN[i] = d.w_map[(int64_t)col0 * Din + i];
-  if (tid < 256) {
-    u32x4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      v[q] = (((tid >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((tid >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
-    lut[tid] = v;
+  for (int i = tid; i < Din * D; i += 512) wN[(i / Din) * DinP + i % Din] = d.w_map[(int64_t)col0 * Din + i];
+  {
+    // A fragment = two nibble lookups; 32 copies of the 16-entry table, copy = lane & 31, entry
+    // n at n * 256 B + 8 copy: a 32-lane ds_read_b64 group covers all 64 banks whatever the
+    // nibbles (the 256-entry octet table read with ds_read_b128 hit random banks)
+    const int n = tid >> 5;
+    lut[tid] = uint2{((n & 1) ? 0x3F80u : 0u) | ((n & 2) ? 0x3F800000u : 0u),
+                     ((n & 4) ? 0x3F80u : 0u) | ((n & 8) ? 0x3F800000u : 0u)};
   }
   for (int i = tid; i < PE_TOK * RBW; i += 512) bits[i] = 0u;
   __syncthreads();
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int c = (lane & 7) + 8 * i;
-        if (c < Din) xs[tb * Din + c] = v[i] / den;
+        if (c < Din) xs[tb * DinP + c] = v[i] / den;
       }
     }
   }
@@ -535,11 +538,11 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
     const int valid = max(0, min(8, Din - kb));
     bf16x8v xh[MT], xl[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) split8(xs + (tg * 16 * MT + mt * 16 + (lane & 15)) * Din + kb, valid, xh[mt], xl[mt]);
+    for (int mt = 0; mt < MT; ++mt) split8(xs + (tg * 16 * MT + mt * 16 + (lane & 15)) * DinP + kb, valid, xh[mt], xl[mt]);
 #pragma unroll
     for (int f = 0; f < NFW; ++f) {
       bf16x8v wh, wl;
-      split8(wN + (nb0 + f * 16 + (lane & 15)) * Din + kb, valid, wh, wl);
+      split8(wN + (nb0 + f * 16 + (lane & 15)) * DinP + kb, valid, wh, wl);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         acc[mt][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[mt], wh, acc[mt][f], 0, 0, 0);
@@ -578,7 +581,11 @@ __global__ __launch_bounds__(512) void ptower_emb_mfma_k(lthm_ptower_desc d, int
     }
     bf16x8v af[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) af[mt] = __builtin_bit_cast(bf16x8v, lut[mb[mt][k0 >> 3]]);
+    for (int mt = 0; mt < MT; ++mt) {
+      const unsigned v = mb[mt][k0 >> 3];
+      const uint2 lo = lut[(v & 15) * 32 + (lane & 31)], hi = lut[(v >> 4) * 32 + (lane & 31)];
+      af[mt] = __builtin_bit_cast(bf16x8v, u32x4{lo.x, lo.y, hi.x, hi.y});
+    }
 #pragma unroll
     for (int f = 0; f < NFW; ++f) {
       const bf16x8v bf = ct_tr_frag<D>(img, nb0 + f * 16, lane);
@@ -1065,8 +1072,8 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
   const int Dm = d->Dout;
   const int nsl = (Dm > 256 && Dm % 256 == 0) ? Dm / 256 : 1;  // 256-wide column slices (grid.y)
   const int Ds = Dm / nsl;
-  const size_t sh_mfma = (size_t)2 * 32 * Ds * 2 + (size_t)d->Din * Ds * 4 + (size_t)PE_TOK * d->Din * 4 +
-                         (size_t)256 * 16 + (size_t)PE_TOK * pe_rbw(R32) * 4;
+  const size_t sh_mfma = (size_t)2 * 32 * Ds * 2 + (size_t)(d->Din + 4) * Ds * 4 + (size_t)PE_TOK * (d->Din + 4) * 4 +
+                         (size_t)512 * 8 + (size_t)PE_TOK * pe_rbw(R32) * 4;
   int maxnb = 0, nproj = 0;
   for (int j = 0; j < d->n_mod; ++j) {
     maxnb = std::max(maxnb, d->mod_nbins[j]);
@@ -1089,7 +1096,7 @@ extern "C" int lthm_product_tower_fwd(const lthm_ptower_desc* d, void* stream) {
     const dim3 g2((unsigned)((d->n + PE_TOK - 1) / PE_TOK), (unsigned)nsl);
     // the 4-deep DMA ring needs the mapper staging (wN + xs) to hold two 32-row slabs
     const bool dma = (Ds == 128 || Ds == 256) &&
-                     (size_t)d->Din * Ds * 4 + (size_t)PE_TOK * d->Din * 4 >= (size_t)2 * 32 * Ds * 2;
+                     (size_t)(d->Din + 4) * Ds * 4 + (size_t)PE_TOK * (d->Din + 4) * 4 >= (size_t)2 * 32 * Ds * 2;
 #define LTHM_PT_EMB(TX)                                                                                     \
   switch (Ds) {                                                                                             \
     case 16: hipLaunchKernelGGL((ptower_emb_mfma_k<TX, 1>), g2, dim3(512), sh_mfma, s, *d, total, R); break;  \

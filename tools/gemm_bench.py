@@ -30,6 +30,9 @@ def main():
     if os.environ.get("GEMM_BENCH_CFG") == "c5":  # C5: B 1024 x T' 513, d 512, MQA (q 512 + kv 128)
         M = 1024 * 513
         shapes = [("qkv", M, 640, 512), ("proj", M, 512, 512), ("fc", M, 2048, 512), ("fc2", M, 512, 2048)]
+    if os.environ.get("GEMM_BENCH_CFG") == "c4":  # C4 ranker MLP: 2,176 -> 1,024 -> 512 at batch 65,536
+        M = 65536
+        shapes = [("fc1", M, 1024, 2176), ("fc2", M, 512, 1024), ("fc1dg", M, 2176, 1024)]
     if os.environ.get("GEMM_BENCH_SQUARE"):
         shapes.append(("sq4096", 4096, 4096, 4096))
     for name, m, n, k in shapes:
