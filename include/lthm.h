@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 32 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 33 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -560,8 +560,18 @@ typedef struct lthm_contrastive_desc {
                              (forward: cl_fr32_k / cl_fwd_k; backward: the cl_bwd32_k columns / rows passes),
                              for live per-kernel timing (bench.py); NULL: not recorded */
   void* main_ev1;
+  void* vc_ws;            /* optional, training at the fixed shift (the fused forward + ROWS pass and its rows_done
+                             backward): device workspace of lthm_contrastive_vc_ws_bytes bytes, the SAME buffer for the
+                             forward and its backward.  The S passes then run over the valid (non-pad) indices of each
+                             (mini-batch, head) only -- every logit of a pad row or column is excluded anyway
+                             (wrapper.py:175-190).  Requires head 0, heads_run = n_heads, head_stride = n_mb * n_max,
+                             mb_size <= 4096.  NULL: the full n x n passes */
+  int64_t vc_ws_bytes;
 } lthm_contrastive_desc;
 
+/* bytes of lthm_contrastive_desc.vc_ws (-1: invalid sizes) */
+int64_t lthm_contrastive_vc_ws_bytes(int64_t B, int32_t T, int32_t n_heads, int32_t mb_size, int32_t n_mb,
+                                     int32_t n_max);
 /* bytes of lthm_contrastive_desc.stats_ws for one forward launch (-1: invalid sizes) */
 int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads);
 

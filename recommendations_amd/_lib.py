@@ -211,6 +211,18 @@ def sub_events(key: str, work: float = None, unit: str = None, nbytes: float = N
     return e0, e1
 
 
+def TIMER_RECORDS() -> list:
+    """The live timer's records (key, ev0, ev1, work, unit, bytes) as mutable lists, or [] when the
+    timer is off: a wrapper replaces a record's work by a callable once the device knows it."""
+    t = TIMER
+    if t is None:
+        return []
+    for i, r in enumerate(t.records):
+        if not isinstance(r, list):
+            t.records[i] = list(r)
+    return t.records
+
+
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 

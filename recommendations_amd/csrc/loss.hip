@@ -254,6 +254,18 @@ struct ClArgs {
   const float* t_norm;  // [B, T]
   void* dt;             // [B, T, DE], dtype t_dtype, every row written
   int xcd_order;        // fused forward: XCD-remapped block order (A/B switch LTHM_CL_FR_XCD)
+  // valid-row compaction (training at the fixed shift, lthm_contrastive_desc.vc_ws): the valid
+  // indices of each (mini-batch, head) in order; per head, advanced by head_args
+  int* vm;        // [NH][n_mb] valid count m
+  int* vcs;       // [NH][n_mb][mbs + 1] compact start of each sequence (vcs[Bm] = m)
+  int* vridx;     // [NH][n_mb][n_max] index r of compact row i
+  float* vsh;     // [NH][n_mb][n_max] backward: exp2 shift of compact row i
+  float* vw;      // [NH][n_mb][n_max] backward: row weight of compact row i
+  int* vcmap;     // [NH][n_mb][mbs T] physical `in` row b T + t of the mini-batch -> compact column, or -1
+  bf16_t* vR;     // [NH][n_mb][n_max][DE] compact `out` rows
+  bf16_t* vC;     // [NH][n_mb][n_max][DE] compact `in` rows (column images)
+  int* vpidx;     // [n_mb][mbs T] the mini-batch's valid physical `in` rows b T + t, in order
+  int* vnp;       // [n_mb] their count
 };
 
 // the per-head view of a multi-head forward launch: head head0 + z, buffers advanced by z strides
@@ -266,6 +278,14 @@ __device__ __forceinline__ ClArgs head_args(const ClArgs& a0, int z) {
     a.w += o;
     if (a.colb) a.colb += o;
     if (a.lqcol) a.lqcol += o;
+    if (a.vm) {
+      const int64_t hv = (int64_t)z * a0.n_mb * a0.n_max;
+      a.vm += (int64_t)z * a0.n_mb;
+      a.vcs += (int64_t)z * a0.n_mb * (a0.mbs + 1);
+      a.vridx += hv; a.vsh += hv; a.vw += hv;
+      a.vcmap += (int64_t)z * a0.n_mb * a0.mbs * a0.T;
+      a.vR += hv * DE; a.vC += hv * DE;
+    }
   }
   return a;
 }
@@ -1827,6 +1847,610 @@ __global__ __launch_bounds__(256, 2) void cl_fr32_k(ClArgs a0) {
   }
 }
 
+
+// ---------------------------------------------------------------- valid-row compaction (VC)
+// Every logit of a pad row or a pad column is excluded (wrapper.py:175-190): a pad row has no
+// loss term and no gradient, a pad column enters no row's softmax.  Training at the fixed
+// shift therefore runs the S passes over the valid indices of each (mini-batch, head) only:
+// m x m instead of n x n (C2 with history lengths ~ U[1, T]: m / n ~ 0.56, a third of the
+// tiles).  cl_vpack_k lists the valid indices r in order (rows and columns share the index
+// space: the pad flag of r is the mask of `in` token (b, t + off)), cl_vgather_k copies their
+// normalised `out` / `in` rows into contiguous compact images, and the fused pass streams the
+// compact `in` rows as its column tiles.  Sequences stay contiguous in compact order, so the
+// same-sequence exclusion is a compact range [vcs[b], vcs[b + 1]); no column is a pad, so a
+// clean tile needs no per-column bias at all.
+struct VcLayout {
+  int64_t m, np, cs, ridx, sh, w, cmap, pidx, R, C, total;
+};
+static inline VcLayout vc_layout(int64_t NH, int64_t n_mb, int64_t mbs, int64_t T, int64_t n_max) {
+  auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+  VcLayout L;
+  int64_t o = 0;
+  L.m = o; o += al(NH * n_mb * 4);
+  L.np = o; o += al(n_mb * 4);
+  L.cs = o; o += al(NH * n_mb * (mbs + 1) * 4);
+  L.ridx = o; o += al(NH * n_mb * n_max * 4);
+  L.sh = o; o += al(NH * n_mb * n_max * 4);
+  L.w = o; o += al(NH * n_mb * n_max * 4);
+  L.cmap = o; o += al(NH * n_mb * mbs * T * 4);
+  L.pidx = o; o += al(n_mb * mbs * T * 4);
+  L.R = o; o += al(NH * n_mb * n_max * DE * 2);
+  L.C = o; o += al(NH * n_mb * n_max * DE * 2);
+  L.total = o;
+  return L;
+}
+
+// wave-level stream compaction of one sequence's positions tp in [0, T): valid(tp) in order
+// -> out[k0 + rank]; returns the count.  f(tp) -> bool, emit(k, tp), miss(tp) for the rest.
+template <typename F, typename E, typename M>
+__device__ __forceinline__ int wave_compact(int T, int k0, int lane, F valid, E emit, M miss) {
+  int k = k0;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int c = 0; c < T; c += 64) {
+    const int tp = c + lane;
+    const bool v = tp < T && valid(tp);
+    const uint64_t bal = __ballot(v);
+    if (v) emit(k + __popcll(bal & lt), tp);
+    else if (tp < T) miss(tp);
+    k += __popcll(bal);
+  }
+  return k - k0;
+}
+
+// One block per (mini-batch, head): the compact index lists, the row weights (as cl_used_k)
+// and the zero dy rows the fused pass never writes (t >= L and pad rows).  The head-0 block
+// also lists the mini-batch's valid physical `in` rows (the columns pass's register rows).
+__global__ __launch_bounds__(256) void cl_vpack_k(ClArgs a0, float* __restrict__ w0, float loss_scale) {
+  const ClArgs a = head_args(a0, blockIdx.y);
+  float* wout = w0 + (int64_t)blockIdx.y * a0.head_stride;
+  const int mb = blockIdx.x;
+  const Geo g = geo(a, mb);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t base = (int64_t)mb * a.n_max;
+  const int T = a.T, off = g.off, Bm = g.Bm;
+  __shared__ int V[CL_UMAXB + 1];   // valid rows per sequence, then compact starts
+  __shared__ int V2[CL_UMAXB + 1];  // head 0: valid physical `in` rows per sequence, then starts
+  __shared__ int scan[256];
+  __shared__ double red[256];
+  const bool phys = blockIdx.y == 0;
+  auto mrow = [&](int b) { return a.mask + (g.b0 + b) * a.mask_stride; };
+  // pass 1: counts (one wave per sequence)
+  for (int b = wv; b < Bm; b += 4) {
+    const uint8_t* mr = mrow(b);
+    int v = 0, v2 = 0;
+    for (int c = 0; c < T; c += 64) {
+      const int tp = c + lane;
+      const bool ok = tp < T && mr[tp] == 0;
+      v += __popcll(__ballot(ok && tp >= off));
+      v2 += __popcll(__ballot(ok));
+    }
+    if (lane == 0) { V[b] = v; V2[b] = v2; }
+  }
+  __syncthreads();
+  // exclusive scans over the sequences: each thread a contiguous run
+  const int per = (Bm + 255) / 256;
+  const int r0 = min(tid * per, Bm), r1 = min(r0 + per, Bm);
+  for (int pass = 0; pass < (phys ? 2 : 1); ++pass) {
+    int* A = pass ? V2 : V;
+    int run = 0;
+    for (int b = r0; b < r1; ++b) run += A[b];
+    scan[tid] = run;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const int t = tid >= o ? scan[tid - o] : 0;
+      __syncthreads();
+      scan[tid] += t;
+      __syncthreads();
+    }
+    const int total = scan[255];
+    int k = scan[tid] - run;
+    __syncthreads();
+    for (int b = r0; b < r1; ++b) {
+      const int c = A[b];
+      A[b] = k;
+      k += c;
+    }
+    if (tid == 0) A[Bm] = total;
+    __syncthreads();
+  }
+  const int N = V[Bm];
+  int* cs = a.vcs + (int64_t)mb * (a.mbs + 1);
+  for (int b = tid; b <= Bm; b += 256) cs[b] = V[b];
+  if (tid == 0) {
+    a.vm[mb] = N;
+    if (phys) a.vnp[mb] = V2[Bm];
+  }
+  // pass 2: the lists (one wave per sequence)
+  int* cmap = a.vcmap + (int64_t)mb * a.mbs * T;
+  int* pidx = a.vpidx + (int64_t)mb * a.mbs * T;
+  const int L = g.L;
+  for (int b = wv; b < Bm; b += 4) {
+    const uint8_t* mr = mrow(b);
+    int* cm = cmap + (int64_t)b * T;
+    wave_compact(T, V[b], lane, [&](int tp) { return tp >= off && mr[tp] == 0; },
+                 [&](int k, int tp) { a.vridx[base + k] = b * L + tp - off; cm[tp] = k; },
+                 [&](int tp) { cm[tp] = -1; });
+    if (phys)
+      wave_compact(T, V2[b], lane, [&](int tp) { return mr[tp] == 0; },
+                   [&](int k, int tp) { pidx[k] = b * T + tp; }, [&](int) {});
+  }
+  // row weights (cl_used_k): used = valid with a valid column outside its own sequence
+  int u = 0;
+  for (int b = tid; b < Bm; b += 256) {
+    const int vb = V[b + 1] - V[b];
+    u += (N - vb > 0) ? vb : 0;
+  }
+  const int U = (int)block_dsum((double)u, red);
+  const float wr = U > 0 ? loss_scale / (float)U : 0.f;
+  for (int r = tid; r < a.n_max; r += 256) {
+    float wvv = 0.f;
+    if (r < g.n) {
+      const int b = seq_of(g, r);
+      wvv = (!pad_of(a, g, r) && N - (V[b + 1] - V[b]) > 0) ? wr : 0.f;
+    }
+    wout[base + r] = wvv;
+  }
+  // zero dy rows (b, t, head) with t >= L or a pad index (the fused pass writes the valid ones)
+  const int per_row = DE / 4;
+  const int64_t cnt = (int64_t)Bm * (T + 1) * per_row;
+  for (int64_t i = tid; i < cnt; i += 256) {
+    const int row = (int)(i / per_row), c4 = (int)(i - (int64_t)row * per_row);
+    const int b = row / (T + 1), t = row - b * (T + 1);
+    if (t < L && mrow(b)[t + off] == 0) continue;
+    const int64_t o = (((g.b0 + b) * (T + 1) + t) * a.NH + a.head) * DE + c4 * 4;
+    if (a.y_dtype == LTHM_BF16) *reinterpret_cast<uint2*>(a.dy + o) = uint2{0u, 0u};
+    else *reinterpret_cast<float4*>((float*)a.dy + o) = float4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// compact images: vR[i] = normalised `out` row of r_i, vC[i] = normalised `in` row of r_i
+__global__ __launch_bounds__(256) void cl_vgather_k(ClArgs a0) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  const int mb = blockIdx.y;
+  const Geo g = geo(a, mb);
+  const int m = a.vm[mb];
+  const int64_t base = (int64_t)mb * a.n_max;
+  const int sub = threadIdx.x & 15;
+  for (int i = blockIdx.x * 16 + (threadIdx.x >> 4); i < m; i += gridDim.x * 16) {
+    const int r = a.vridx[base + i];
+    const u32x4 ov = *reinterpret_cast<const u32x4*>(out_row(a, g, r) + sub * 8);
+    const u32x4 iv = *reinterpret_cast<const u32x4*>(in_row(a, g, r) + sub * 8);
+    *reinterpret_cast<u32x4*>(a.vR + (base + i) * DE + sub * 8) = ov;
+    *reinterpret_cast<u32x4*>(a.vC + (base + i) * DE + sub * 8) = iv;
+  }
+}
+
+// backward prologue of the compact columns pass: the exp2 shift and weight of every compact
+// row (cl_shift_k's values, in compact order) and, on the head-0 blocks, zero dt rows of the
+// pad physical `in` rows (the columns pass writes the valid ones)
+__global__ __launch_bounds__(256) void cl_vshift_k(ClArgs a0) {
+  const ClArgs a = head_args(a0, blockIdx.z);
+  const int mb = blockIdx.y;
+  const int m = a.vm[mb];
+  const int64_t base = (int64_t)mb * a.n_max;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) {
+    const int r = a.vridx[base + i];
+    const float wv = a.w[base + r];
+    a.vsh[base + i] = wv != 0.f ? __log2f(wv) - a.lse[base + r] * LOG2E : -INFINITY;
+    a.vw[base + i] = wv;
+  }
+  if (blockIdx.z != 0) return;
+  const Geo g = geo(a, mb);
+  const int T = a.T;
+  const int per_row = DE / 4;
+  const int64_t cnt = (int64_t)g.Bm * T * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+    const int row = (int)(i / per_row), c4 = (int)(i - (int64_t)row * per_row);
+    const int b = row / T, t = row - b * T;
+    if (a.mask[(g.b0 + b) * a.mask_stride + t] == 0) continue;
+    const int64_t o = ((g.b0 + b) * T + t) * DE + c4 * 4;
+    if (a.t_dtype == LTHM_BF16) *reinterpret_cast<uint2*>((bf16_t*)a.dt + o) = uint2{0u, 0u};
+    else *reinterpret_cast<float4*>((float*)a.dt + o) = float4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// LDS of the compact fused pass: the 4-deep image ring (no per-column vector: no column is a
+// pad) in a union with the epilogue restage
+struct VTile {
+  union {
+    unsigned char img[CL_NB32][64 * 256];
+    float ep[4][32][CL_EPS];
+  };
+};
+
+// contiguous-row image cursor: wave w stages rows 16 w .. 16 w + 15 of tile t with four DMAs
+// of 4 rows x 256 B (lane l: row 64 t + 16 w + 4 k + l / 16, slot l % 16, source chunk
+// slot ^ swz32(row)); rows at or past `lim` come from the zero row.  Tiles are staged in any
+// order (the compact passes visit the clean tiles first).
+struct VCursor {
+  const unsigned char* base;
+  int row0, lim, ch0;
+  __device__ __forceinline__ void init(const bf16_t* base_, int lim_, int w, int lane) {
+    base = reinterpret_cast<const unsigned char*>(base_);
+    row0 = 16 * w + (lane >> 4);
+    lim = lim_;
+    ch0 = (lane & 15) ^ (((lane >> 4) & 3) << 2);  // swz32(row) = ((row & 3) << 2) | ((row >> 2) & 3)
+  }
+  __device__ __forceinline__ void stage(unsigned char* img, int t, int w, int lane) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = 64 * t + row0 + 4 * k;
+      const void* src = row < lim ? (const void*)(base + (int64_t)row * 256 + ((ch0 ^ k) << 4))
+                                  : (const void*)(cl_zero_row + 16 * (lane & 15));
+      glds16(src, img + (16 * w + 4 * k) * 256);
+    }
+  }
+};
+
+// the compact passes' tile order: the clean tiles first, then the special ones (the tiles of
+// the register rows' own sequences [ts_lo, ts_hi], then the partial last tile tl if it lies
+// past them), so that each loop runs one branch-free body
+struct TileOrder {
+  int ts_lo, nspan, nclean, tl;
+  __device__ __forceinline__ void init(int spec_lo, int spec_hi, int m, int ntile, bool last_special) {
+    ts_lo = spec_lo / 64;
+    const int ts_hi = (spec_hi - 1) / 64;
+    nspan = ts_hi - ts_lo + 1;
+    tl = (last_special && (m & 63) && ntile - 1 > ts_hi) ? ntile - 1 : -1;
+    nclean = ntile - nspan - (tl >= 0 ? 1 : 0);
+  }
+  __device__ __forceinline__ int at(int i) const {
+    if (i < ts_lo) return i;
+    if (i < nclean) return i + nspan;
+    const int j = i - nclean;
+    return j < nspan ? ts_lo + j : tl;
+  }
+};
+
+// S^T tile of the 32x32x16 engine: acc[ib] = img rows 32 ib .. 32 ib + 31 against the register
+// rows (the two chains interleaved, each k-step's A fragments read one step ahead)
+__device__ __forceinline__ void s_tile32(f32x16 (&acc)[2], const unsigned char* img, const int (&roff)[8],
+                                         const bf16x8v (&qf)[8]) {
+  acc[0] = f32x16{};
+  acc[1] = f32x16{};
+  auto rd = [&](int ib, int s) {
+    return __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(img + ib * 8192 + roff[s]));
+  };
+  bf16x8v f0 = rd(0, 0), f1 = rd(1, 0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int sn = s + 1 < 8 ? s + 1 : s;
+    const bf16x8v n0 = rd(0, sn), n1 = rd(1, sn);
+    acc[0] = mfma32(f0, qf[s], acc[0]);
+    acc[1] = mfma32(f1, qf[s], acc[1]);
+    f0 = n0;
+    f1 = n1;
+  }
+}
+
+// dacc[32 x 128] += P[32 x 32] . img[32 x 128] for image block ib (k-steps 2 ib, 2 ib + 1)
+__device__ __forceinline__ void pv_tile32(f32x16 (&dacc)[4], const f32x16& p, int ib, const unsigned char* img,
+                                          const int (&toff)[4][2]) {
+  const bf16x8v af0 = __builtin_bit_cast(bf16x8v, u32x4{pk_bf16(p[0], p[1]), pk_bf16(p[2], p[3]),
+                                                        pk_bf16(p[4], p[5]), pk_bf16(p[6], p[7])});
+  const bf16x8v af1 = __builtin_bit_cast(bf16x8v, u32x4{pk_bf16(p[8], p[9]), pk_bf16(p[10], p[11]),
+                                                        pk_bf16(p[12], p[13]), pk_bf16(p[14], p[15])});
+  const int k0 = 2 * ib * 4096, k1 = (2 * ib + 1) * 4096;
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd) {
+    dacc[nd] = mfma32(af0, tr_frag32(img, toff[nd][0] + k0, toff[nd][1] + k0), dacc[nd]);
+    dacc[nd] = mfma32(af1, tr_frag32(img, toff[nd][0] + k1, toff[nd][1] + k1), dacc[nd]);
+  }
+}
+
+// Fused forward + ROWS pass over compact rows x (register rows) and compact columns y (image
+// tiles) of one (mini-batch, head): as cl_fr32_k, with the clean tiles visited first in a loop
+// of their own (one branch-free body), then the special ones (TileOrder).
+// grid ((n_max + 127) / 128, n_mb, heads): 4 waves x 32 register rows
+__global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
+  constexpr int NW = 4, XR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) VTile sh;
+  __shared__ float rs_sc[NW][32], rs_w[NW][32];  // per register row: w / Z and w
+  const int z = blockIdx.z, mb = blockIdx.y, xb = blockIdx.x;
+  const ClArgs a = head_args(a0, z);
+  const int m = a.vm[mb];
+  const int x0 = xb * XR;
+  if (x0 >= m) return;
+  const Geo g = geo(a, mb);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int64_t base = (int64_t)mb * a.n_max;
+  const int* cs = a.vcs + (int64_t)mb * (a.mbs + 1);
+  const int* ridx = a.vridx + base;
+  int roff[8], toff[4][2];
+  frag32_offsets(roff, toff, lane);
+  f32x16 dacc[4];
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd) dacc[nd] = f32x16{};
+  const int x = x0 + 32 * w + r32;
+  const bool live = x < m;
+  const int r = live ? ridx[x] : 0;
+  bf16x8v qf[8];
+  {
+    const bf16_t* rp = a.vR + (base + (live ? x : 0)) * DE;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (live) v = *reinterpret_cast<const u32x4*>(rp + 16 * s + 8 * hh);
+      qf[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
+  const float it = 1.f / a.tau, c1 = it * LOG2E, csh = -c1;  // p = e^(S / tau - 1 / tau)
+  const float dg = live ? a.diag[base + r] : 0.f;
+  const float thr = rank_threshold(dg, it, a.tau);
+  const int xsq = live ? seq_of(g, r) : 0;
+  const int xlo = live ? cs[xsq] : -(1 << 30);
+  const unsigned xlen = live ? (unsigned)(cs[xsq + 1] - cs[xsq]) : 0u;
+  // the block's own sequences (compact ranges), where the same-sequence exclusion applies
+  const int rlo = ridx[x0], rhi = ridx[min(x0 + XR, m) - 1];
+  const int spec_lo = cs[seq_of(g, rlo)], spec_hi = cs[seq_of(g, rhi) + 1];
+  float Z = 0.f, pv = -INFINITY;
+  int cn = 0, rk = 0;
+  const int ntile = (m + 63) / 64;
+  TileOrder ord;
+  ord.init(spec_lo, spec_hi, m, ntile, true);
+  VCursor cur;
+  cur.init(a.vC + base * DE, m, w, lane);
+  retire_loads();
+  cur.stage(sh.img[0], ord.at(0), w, lane);
+  if (ntile > 1) cur.stage(sh.img[1], ord.at(1), w, lane);
+  if (ntile > 2) cur.stage(sh.img[2], ord.at(2), w, lane);
+  // step i of the visiting order: tile i landed (i + 1, i + 2 may still be in flight), every
+  // wave is done with step i - 1, whose ring slot takes step i + 3
+  auto open_step = [&](int i) {
+    if (i + 2 < ntile) wait_vm<8>();
+    else if (i + 1 < ntile) wait_vm<4>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (i + 3 < ntile) cur.stage(sh.img[(i + 3) % CL_NB32], ord.at(i + 3), w, lane);
+  };
+  // clean tiles: no exclusion, no pad, every element kept
+  for (int i = 0; i < ord.nclean; ++i) {
+    open_step(i);
+    const unsigned char* img = sh.img[i % CL_NB32];
+    f32x16 sacc[2];
+    s_tile32(sacc, img, roff, qf);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float sv = sacc[ib][v];
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, csh));
+        Z += p;
+        rk += sv > thr ? 1 : 0;
+        sacc[ib][v] = p;
+      }
+    }
+    cn += 32;
+    pv_tile32(dacc, sacc[0], 0, img, toff);
+    pv_tile32(dacc, sacc[1], 1, img, toff);
+  }
+  // special tiles: the register rows' own sequences (exclusion, diagonal) and the partial tile
+  for (int i = ord.nclean; i < ntile; ++i) {
+    open_step(i);
+    const unsigned char* img = sh.img[i % CL_NB32];
+    f32x16 sacc[2];
+    s_tile32(sacc, img, roff, qf);
+    // per-tile lane bases (laundered, else the 32 per-element offsets are hoisted into 32
+    // VGPRs each); element v of block ib is column y = y0 + 4 hh + cv, cv a compile-time constant
+    const int y0 = 64 * ord.at(i);
+    int dl = y0 + 4 * hh - xlo, dx = y0 + 4 * hh - x, dm = y0 + 4 * hh - m;
+    asm volatile("" : "+v"(dl), "+v"(dx), "+v"(dm));
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int cv = 32 * ib + 8 * (v >> 2) + (v & 3);
+        const float sv = sacc[ib][v];
+        const bool dgl = dx + cv == 0;
+        if (dgl) pv = sv * it;
+        const bool same = (unsigned)(dl + cv) < xlen;
+        const bool keep = live && dm + cv < 0 && (!same || dgl);
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, csh));
+        const float p = keep ? e : 0.f;
+        Z += p;
+        cn += keep ? 1 : 0;
+        rk += (keep && !dgl && sv > thr) ? 1 : 0;
+        sacc[ib][v] = p;
+      }
+    }
+    pv_tile32(dacc, sacc[0], 0, img, toff);
+    pv_tile32(dacc, sacc[1], 1, img, toff);
+  }
+  // the two lane halves hold the row's alternate column groups
+  Z += __shfl_xor(Z, 32, 64);
+  cn += __shfl_xor(cn, 32, 64);
+  rk += __shfl_xor(rk, 32, 64);
+  pv = fmaxf(pv, __shfl_xor(pv, 32, 64));
+  const float wx = live ? a.w[base + r] : 0.f;
+  if (hh == 0) {
+    if (live) {
+      a.lse[base + r] = cn > 0 ? it + __logf(Z) : -INFINITY;
+      a.pos[base + r] = pv;
+      a.cnt[base + r] = cn;
+      a.rank[base + r] = rk;
+    }
+    rs_sc[w][r32] = (wx != 0.f && Z > 0.f) ? wx / Z : 0.f;
+    rs_w[w][r32] = wx;
+  }
+  // epilogue: restage, then 16 lanes per row through F.normalize into dy
+  __syncthreads();
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) sh.ep[w][8 * (v >> 2) + 4 * hh + (v & 3)][32 * nd + r32] = dacc[nd][v];
+  __syncthreads();
+  const float gs = 1.f / a.tau;  // unit upstream gradient
+  const int sub = lane & 15;
+#pragma unroll 1
+  for (int ps = 0; ps < 8; ++ps) {
+    const int rl = 4 * ps + (lane >> 4), xr = x0 + 32 * w + rl;
+    const int xc = min(xr, m - 1);  // every lane takes part in the row reduction
+    const int rr = ridx[xc];
+    const int b = rr / g.L, t = rr - b * g.L;
+    const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
+    const float sc = rs_sc[w][rl], wr = rs_w[w][rl];
+    float inv[8];
+    load_vec<bf16_t, 16>(a.vC + (base + xc) * DE + 8 * sub, inv);
+    const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
+    const float4 u1 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub + 4]);
+    const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    float gv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = gs * (uu[i] * sc - wr * inv[i]);
+    normalize_bwd_store(gv, a.y_raw, a.y_dtype, a.y_norm[ro], a.dy, ro * DE + 8 * sub, xr < m);
+  }
+}
+
+// Columns pass over compact images: register rows = the mini-batch's valid physical `in` rows
+// (the same operand for every head), image = the compact `out` rows of each head in turn, so
+// dIn is summed over the heads in registers and dt is written once (as cl_bwd32_k COLS).
+// grid ((mbs T + 127) / 128, n_mb)
+__global__ __launch_bounds__(256, 2) void cl_bwd32v_k(ClArgs a0) {
+  constexpr int NW = 4, XR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) ClTile32<NW> sh;
+  const int per = gridDim.x * gridDim.y;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, per);
+  const int mb = lin / gridDim.x, xb = lin - mb * gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int T = a0.T;
+  const int64_t b0 = (int64_t)mb * a0.mbs;
+  const int np = a0.vnp[mb];
+  const int j0 = xb * XR;
+  if (j0 >= np) return;
+  const int* pidx = a0.vpidx + (int64_t)mb * a0.mbs * T;
+  const int j = j0 + 32 * w + r32;
+  const bool pin = j < np;
+  const int p = pidx[pin ? j : np - 1];
+  const int pb = p / T, pt = p - pb * T;
+  int roff[8], toff[4][2];
+  frag32_offsets(roff, toff, lane);
+  f32x16 dacc[4];
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd) dacc[nd] = f32x16{};
+  bf16x8v qf[8];
+  {
+    const bf16_t* rp = a0.in_n + ((b0 + pb) * T + pt) * DE;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (pin) v = *reinterpret_cast<const u32x4*>(rp + 16 * s + 8 * hh);
+      qf[s] = __builtin_bit_cast(bf16x8v, v);
+    }
+  }
+  const int b_lo = pidx[j0] / T, b_hi = pidx[min(j0 + XR, np) - 1] / T;
+  const float c1 = LOG2E / a0.tau;
+  const int nrun = a0.heads_run;
+#pragma unroll 1
+  for (int hz = 0; hz < nrun; ++hz) {
+    const ClArgs a = head_args(a0, hz);
+    const int m = a.vm[mb];
+    if (m == 0) continue;
+    const int64_t base = (int64_t)mb * a.n_max;
+    const int* cs = a.vcs + (int64_t)mb * (a.mbs + 1);
+    const int xc = pin ? a.vcmap[(int64_t)mb * a.mbs * T + p] : -1;
+    const bool live = xc >= 0;
+    const int xlo = cs[pb];
+    const unsigned xlen = (unsigned)(cs[pb + 1] - xlo);
+    const int spec_lo = cs[b_lo], spec_hi = cs[b_hi + 1];
+    const bool wmask = __ballot(!live) != 0ull;
+    const float* shv = a.vsh + base;
+    const float* wvv = a.vw + base;
+    VCursor cur;
+    cur.init(a.vR + base * DE, m, w, lane);
+    const int ntile = (m + 63) / 64;
+    TileOrder ord;
+    ord.init(spec_lo, spec_hi, m, ntile, false);  // past m: shift -inf, so the partial tile is clean
+    auto stage = [&](int i) {
+      const int buf = i % CL_NB32, y0 = ord.at(i) * 64;
+      cur.stage(sh.r.img[buf], ord.at(i), w, lane);
+      const bool inr = y0 + lane < m;
+      glds4(inr ? shv + y0 + lane : &cl_ninf, sh.r.m0[buf][w]);
+      glds4(inr ? wvv + y0 + lane : &cl_zero_f, sh.r.m1[buf][w]);
+    };
+    constexpr int PT = 6;  // DMAs per wave and tile
+    __syncthreads();  // the previous head's last tiles are read before this head's prologue restages the ring
+    retire_loads();
+    stage(0);
+    if (ntile > 1) stage(1);
+    if (ntile > 2) stage(2);
+    auto open_step = [&](int i) {
+      if (i + 2 < ntile) wait_vm<2 * PT>();
+      else if (i + 1 < ntile) wait_vm<PT>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      if (i + 3 < ntile) stage(i + 3);
+    };
+    for (int i = 0; i < ord.nclean; ++i) {
+      open_step(i);
+      const int cb = i % CL_NB32;
+      const unsigned char* img = sh.r.img[cb];
+      f32x16 acc[2];
+      s_tile32(acc, img, roff, qf);
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const float4 ys = *reinterpret_cast<const float4*>(&sh.r.m0[cb][w][32 * ib + 8 * qd + 4 * hh]);
+          const float yv[4] = {ys.x, ys.y, ys.z, ys.w};
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            acc[ib][4 * qd + jj] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][4 * qd + jj], c1, yv[jj]));
+        }
+      if (wmask && !live) {
+        acc[0] = f32x16{};
+        acc[1] = f32x16{};
+      }
+      pv_tile32(dacc, acc[0], 0, img, toff);
+      pv_tile32(dacc, acc[1], 1, img, toff);
+    }
+    for (int i = ord.nclean; i < ntile; ++i) {
+      open_step(i);
+      const int cb = i % CL_NB32;
+      const unsigned char* img = sh.r.img[cb];
+      f32x16 acc[2];
+      s_tile32(acc, img, roff, qf);
+      const int y0 = 64 * ord.at(i);
+      int dl = y0 + 4 * hh - xlo, dx = y0 + 4 * hh - xc;
+      asm volatile("" : "+v"(dl), "+v"(dx));
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int cv = 32 * ib + 8 * (v >> 2) + (v & 3), yl = cv + 4 * hh;
+          const bool same = (unsigned)(dl + cv) < xlen;
+          const bool dgl = dx + cv == 0;
+          const bool keep = live && (!same || dgl);
+          const float ysh = sh.r.m0[cb][w][yl], yw = sh.r.m1[cb][w][yl];
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][v], c1, ysh)) - (dgl ? yw : 0.f);
+          acc[ib][v] = (keep && yw != 0.f) ? e : 0.f;
+        }
+      pv_tile32(dacc, acc[0], 0, img, toff);
+      pv_tile32(dacc, acc[1], 1, img, toff);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nd = 0; nd < 4; ++nd)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) sh.ep[w][8 * (v >> 2) + 4 * hh + (v & 3)][32 * nd + r32] = dacc[nd][v];
+  const float gs = (a0.gscale ? *a0.gscale : 1.f) / a0.tau;
+  const int sub = lane & 15;
+#pragma unroll 1
+  for (int ps = 0; ps < 8; ++ps) {
+    const int rl = 4 * ps + (lane >> 4), q = j0 + 32 * w + rl;
+    const int pq = pidx[min(q, np - 1)];
+    const int64_t ro = b0 * T + pq;
+    float gv[8];
+    const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
+    const float4 u1 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub + 4]);
+    gv[0] = gs * u0.x; gv[1] = gs * u0.y; gv[2] = gs * u0.z; gv[3] = gs * u0.w;
+    gv[4] = gs * u1.x; gv[5] = gs * u1.y; gv[6] = gs * u1.z; gv[7] = gs * u1.w;
+    normalize_bwd_store(gv, a0.t_raw, a0.t_dtype, a0.t_norm[ro], a0.dt, ro * DE + 8 * sub, q < np);
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -1847,6 +2471,15 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.heads_run = d->heads_run > 1 ? d->heads_run : 1;
   a.t_raw = d->t_raw; a.t_dtype = d->t_dtype; a.t_norm = d->t_norm; a.dt = d->dt;
   a.xcd_order = 0;
+  a.vm = nullptr; a.vcs = nullptr; a.vridx = nullptr; a.vsh = nullptr; a.vw = nullptr; a.vcmap = nullptr;
+  a.vR = nullptr; a.vC = nullptr; a.vpidx = nullptr; a.vnp = nullptr;
+  if (d->vc_ws) {
+    const VcLayout L = vc_layout(d->n_heads, d->n_mb, d->mb_size, d->T, d->n_max);
+    char* b = (char*)d->vc_ws;
+    a.vm = (int*)(b + L.m); a.vnp = (int*)(b + L.np); a.vcs = (int*)(b + L.cs); a.vridx = (int*)(b + L.ridx);
+    a.vsh = (float*)(b + L.sh); a.vw = (float*)(b + L.w); a.vcmap = (int*)(b + L.cmap); a.vpidx = (int*)(b + L.pidx);
+    a.vR = (bf16_t*)(b + L.R); a.vC = (bf16_t*)(b + L.C);
+  }
   return a;
 }
 
@@ -1860,6 +2493,20 @@ static int cl_check(const lthm_contrastive_desc* d) {
 }
 
 static int64_t cl_stats_blocks(int32_t n_max) { return (n_max + CL_SROWS - 1) / CL_SROWS; }
+
+extern "C" int64_t lthm_contrastive_vc_ws_bytes(int64_t B, int32_t T, int32_t n_heads, int32_t mb_size, int32_t n_mb,
+                                                int32_t n_max) {
+  if (B <= 0 || T <= 0 || n_heads <= 0 || mb_size <= 0 || n_mb <= 0 || n_max <= 0) return -1;
+  return vc_layout(n_heads, n_mb, mb_size, T, n_max).total;
+}
+
+// the compact path's preconditions (beyond cl_check and the fused-rows ones)
+static bool vc_ok(const lthm_contrastive_desc* d) {
+  if (!d->vc_ws) return false;
+  if (d->vc_ws_bytes < vc_layout(d->n_heads, d->n_mb, d->mb_size, d->T, d->n_max).total) return false;
+  return d->head == 0 && d->heads_run == d->n_heads && d->head_stride == (int64_t)d->n_mb * d->n_max &&
+         d->mb_size <= CL_UMAXB && (int64_t)d->mb_size * d->T <= (1ll << 30);
+}
 
 extern "C" int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads) {
   if (n_mb <= 0 || n_max <= 0 || heads <= 0) return -1;
@@ -1951,12 +2598,24 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
   if (rows) {
     // forward + the row side of the backward in one pass (row weights from the pad mask first)
-    hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
-    LTHM_CHECK_LAUNCH();
+    const bool vc = vc_ok(d);
+    if (d->vc_ws && !vc) return 1;
+    if (vc) {
+      // valid-row compaction: index lists + weights + zero dy rows, then the compact images
+      hipLaunchKernelGGL(cl_vpack_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
+      LTHM_CHECK_LAUNCH();
+      hipLaunchKernelGGL(cl_vgather_k, dim3(std::max(1, std::min(16, d->n_max / 256)), d->n_mb, nrun), dim3(256), 0,
+                         s, a);
+      LTHM_CHECK_LAUNCH();
+    } else {
+      hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
+      LTHM_CHECK_LAUNCH();
+    }
     static const int xcd = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : 0;
     a.xcd_order = xcd;
     if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
-    hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
+    if (vc) hipLaunchKernelGGL(cl_fr32v_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     if (d->main_ev1 && hipEventRecord((hipEvent_t)d->main_ev1, s) != hipSuccess) return (int)hipGetLastError();
     if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
@@ -1999,14 +2658,23 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
     LTHM_REQUIRE(fixed && d->head == 0 && nrun == d->n_heads);
     LTHM_REQUIRE((d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32) &&
                  (d->t_dtype == LTHM_BF16 || d->t_dtype == LTHM_F32));
-    ClArgs ash = a;
-    ash.dy = nullptr;
-    ash.d_out = nullptr;  // the dy tails were zeroed by the forward
-    hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, ash);
-    LTHM_CHECK_LAUNCH();
+    const bool vc = vc_ok(d);
+    if (d->vc_ws && !vc) return 1;
     const dim3 gcols((int)(((int64_t)d->mb_size * d->T + 127) / 128), d->n_mb, 1);
+    if (vc) {
+      hipLaunchKernelGGL(cl_vshift_k, dim3(std::max(1, std::min(16, d->n_max / 256)), d->n_mb, nrun), dim3(256), 0, s,
+                         a);
+      LTHM_CHECK_LAUNCH();
+    } else {
+      ClArgs ash = a;
+      ash.dy = nullptr;
+      ash.d_out = nullptr;  // the dy tails were zeroed by the forward
+      hipLaunchKernelGGL(cl_shift_k, dim3((d->n_max + 255) / 256, d->n_mb, nrun), dim3(256), 0, s, ash);
+      LTHM_CHECK_LAUNCH();
+    }
     if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
-    hipLaunchKernelGGL((cl_bwd32_k<false, true, 4>), gcols, dim3(256), 0, s, a);
+    if (vc) hipLaunchKernelGGL(cl_bwd32v_k, gcols, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((cl_bwd32_k<false, true, 4>), gcols, dim3(256), 0, s, a);
     LTHM_CHECK_LAUNCH();
     if (d->main_ev1 && hipEventRecord((hipEvent_t)d->main_ev1, s) != hipSuccess) return (int)hipGetLastError();
     if (d->gscale) {

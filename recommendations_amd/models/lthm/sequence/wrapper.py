@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
-from ...._lib import STRUCTS, call, dcode, load, ptr, stream, sub_events
+from ...._lib import STRUCTS, TIMER_RECORDS, call, dcode, load, ptr, stream, sub_events
 from ....commons.base_model_wrapper import BaseModelWrapper
 from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
@@ -85,22 +85,43 @@ class ContrastiveLossFn(torch.autograd.Function):
         rows = (ctx.needs_input_grad[0] and not _OLD_BWD and not _NO_FUSED_ROWS and logq is None
                 and 2.0 / tau <= 80.0 and mbs <= 4096 and yc.dtype in (torch.bfloat16, torch.float32))
         dy = None
+        vc = None
         if rows:
             dy = torch.empty_like(yc)
             d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
-        # algorithmic work: 2 n^2 De per head (S); with the row side also dS . in (2 n^2 De)
-        ev = sub_events("cl_fr32_k" if rows else "cl_fwd_main", (2.0 if rows else 1.0) * float(sum(cfg["flops"])),
-                        "flop")
+            if not _NO_VC:
+                # valid-row compaction: the S passes run over the non-pad indices only (the
+                # workspace is shared with this forward's backward)
+                vc = torch.empty(load().lthm_contrastive_vc_ws_bytes(B, T, NH, mbs, n_mb, n_max),
+                                 dtype=torch.uint8, device=dev)
+                d.vc_ws, d.vc_ws_bytes = ptr(vc), vc.numel()
+        # algorithmic work: 2 n^2 De per head (S); with the row side also dS . in (2 n^2 De); with
+        # the compaction n is the valid count m of each (mini-batch, head), read after the step
+        work = (2.0 if rows else 1.0) * float(sum(cfg["flops"]))
+        ev = sub_events("cl_fr32_k" if rows else "cl_fwd_main", work, "flop")
         if ev is not None:  # the fused pass alone, timed inside the call (bench.py's roofline kernel)
             d.main_ev0, d.main_ev1 = ev[0].cuda_event, ev[1].cuda_event
         call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
-             1.0 / n_mb, stream(), _key="cl_fwd_k", _work=(2.0 if rows else 1.0) * float(sum(cfg["flops"])),
-             _unit="flop")
+             1.0 / n_mb, stream(), _key="cl_fwd_k", _work=work, _unit="flop")
+        if vc is not None and ev is not None:
+            # the timer's work of both compact passes: 2 x 2 m^2 De per (mini-batch, head)
+            mv = vc[:NH * n_mb * 4].view(torch.int32).clone()
+            vwork = lambda: 4.0 * De * float((mv.double() ** 2).sum())  # noqa: E731
+            want = {"cl_fr32_k", "cl_fwd_k"}  # this call's two records, the latest of their keys
+            for rec in reversed(TIMER_RECORDS()):
+                if rec[0] in want:
+                    rec[3] = vwork
+                    want.discard(rec[0])
+                    if not want:
+                        break
+            cfg["vc_work"] = vwork
         # loss = sum_mb sum_heads mean-CE / n_mb  (wrapper.py:109-111)
         loss = torch.empty(1, **f32)
         call("lthm_colsum", ptr(stats), 0, NH * n_mb, 1, nstat, ptr(loss), 0, stream())
         loss = loss / n_mb
         ctx.save_for_backward(yc, tc, yn, tn, ynorm, tnorm, lse, w, diag, mask, offsets_dev, logq, lqc, dy)
+        ctx.vc = vc
+        ctx.vc_work = cfg.get("vc_work")
         ctx.meta = (B, T, NH, De, mbs, n_mb, n_max, tau)
         ctx.stats = stats
         cfg.get("stats_out", []).append(stats)
@@ -146,14 +167,18 @@ class ContrastiveLossFn(torch.autograd.Function):
         d.y_raw, d.y_norm, d.dy, d.y_dtype = ptr(yc), ptr(ynorm), ptr(dy), dcode(yc)
         d.t_raw, d.t_norm, d.dt, d.t_dtype = ptr(tc), ptr(tnorm), ptr(dt), dcode(tc)
         d.rows_done = 1 if dy_f is not None else 0
+        vw = None
+        if dy_f is not None and ctx.vc is not None:  # the forward's compact index lists and images
+            d.vc_ws, d.vc_ws_bytes = ptr(ctx.vc), ctx.vc.numel()
+            vw = ctx.vc_work
         if dy_f is not None:  # the columns pass alone: S recompute + dS^T . out, 4 n^2 De per head
-            ev = sub_events("cl_bwd32_k", 2.0 * float(sum(ctx.flops)), "flop")
+            ev = sub_events("cl_bwd32_k", vw or 2.0 * float(sum(ctx.flops)), "flop")
             if ev is not None:
                 d.main_ev0, d.main_ev1 = ev[0].cuda_event, ev[1].cuda_event
         # algorithmic work per head: one S recompute + dS^T . out (2 x 2 n^2 De) with the row side
         # done in the forward; else also dS . in (3 x; the ROWS and COLS kernels each recompute S)
         call("lthm_contrastive_bwd", ctypes.addressof(d), stream(), _key="cl_bwd_k",
-             _work=(2.0 if dy_f is not None else 3.0) * float(sum(ctx.flops)), _unit="flop")
+             _work=vw or (2.0 if dy_f is not None else 3.0) * float(sum(ctx.flops)), _unit="flop")
         return dy, dt, None, None, None, None
 
     @staticmethod
@@ -183,6 +208,7 @@ class ContrastiveLossFn(torch.autograd.Function):
 
 _OLD_BWD = os.environ.get("LTHM_CL_BWD_OLD") == "1"
 _NO_FUSED_ROWS = os.environ.get("LTHM_CL_NO_FUSED_ROWS") == "1"  # A/B: separate forward and ROWS passes
+_NO_VC = os.environ.get("LTHM_CL_VC") == "0"  # A/B: the full n x n passes (no valid-row compaction)
 
 
 def contrastive_step(y, tgt, mask, offs: np.ndarray, mbs: int, tau: float, ks: List[int], logq=None):

@@ -64,7 +64,7 @@ def main():
     if args.bwd and hasattr(K, "mlp_bwd"):
         dy = torch.randn(M, D, device=dev, generator=g).to(bf)
         fl_b = 7.0 * 2 * M * D * HID  # executed (recompute 1 + dH 1 + dX 1 + dW 2 + recompute 2)
-        ms = timed(lambda: K.mlp_bwd(x, w1, b1, w2t, dy), args.iters)
+        ms = timed(lambda: K.mlp_bwd(x, dy, w1, b1, w2t), args.iters)
         out["fused_bwd"] = {"ms": round(ms, 4), "alg_TFLOP/s": round(8.0 * M * D * HID / ms / 1e9, 1),
                             "exec_TFLOP/s": round(fl_b / ms / 1e9, 1)}
     print(json.dumps(out))
