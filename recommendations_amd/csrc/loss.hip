@@ -2003,7 +2003,9 @@ __global__ __launch_bounds__(256) void cl_vpack_k(ClArgs a0, float* __restrict__
   }
 }
 
-// compact images: vR[i] = normalised `out` row of r_i, vC[i] = normalised `in` row of r_i
+// compact images: vR[i] = normalised `out` row of r_i, vC[i] = normalised `in` row of r_i, and
+// the positive logit diag[r_i] = out . in / tau with cl_diag_k's arithmetic (the compact forward
+// reads no other diag entry).  16 lanes per row, two rows per lane group in flight.
 __global__ __launch_bounds__(256) void cl_vgather_k(ClArgs a0) {
   const ClArgs a = head_args(a0, blockIdx.z);
   const int mb = blockIdx.y;
@@ -2011,12 +2013,34 @@ __global__ __launch_bounds__(256) void cl_vgather_k(ClArgs a0) {
   const int m = a.vm[mb];
   const int64_t base = (int64_t)mb * a.n_max;
   const int sub = threadIdx.x & 15;
-  for (int i = blockIdx.x * 16 + (threadIdx.x >> 4); i < m; i += gridDim.x * 16) {
-    const int r = a.vridx[base + i];
-    const u32x4 ov = *reinterpret_cast<const u32x4*>(out_row(a, g, r) + sub * 8);
-    const u32x4 iv = *reinterpret_cast<const u32x4*>(in_row(a, g, r) + sub * 8);
-    *reinterpret_cast<u32x4*>(a.vR + (base + i) * DE + sub * 8) = ov;
-    *reinterpret_cast<u32x4*>(a.vC + (base + i) * DE + sub * 8) = iv;
+  const int step = gridDim.x * 32;
+  for (int i0 = blockIdx.x * 32 + (threadIdx.x >> 4); i0 < m; i0 += step) {
+    int rr[2];
+    u32x4 ov[2], iv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) rr[u] = a.vridx[base + min(i0 + 16 * u, m - 1)];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ov[u] = *reinterpret_cast<const u32x4*>(out_row(a, g, rr[u]) + sub * 8);
+      iv[u] = *reinterpret_cast<const u32x4*>(in_row(a, g, rr[u]) + sub * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + 16 * u;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = fmaf(__uint_as_float(ov[u][k] << 16), __uint_as_float(iv[u][k] << 16), acc);
+        acc = fmaf(__uint_as_float(ov[u][k] & 0xffff0000u), __uint_as_float(iv[u][k] & 0xffff0000u), acc);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      if (i < m) {
+        *reinterpret_cast<u32x4*>(a.vR + (base + i) * DE + sub * 8) = ov[u];
+        *reinterpret_cast<u32x4*>(a.vC + (base + i) * DE + sub * 8) = iv[u];
+        if (sub == 0) a.diag[base + rr[u]] = acc / a.tau;
+      }
+    }
   }
 }
 
@@ -2086,15 +2110,22 @@ struct VCursor {
 // the register rows' own sequences [ts_lo, ts_hi], then the partial last tile tl if it lies
 // past them), so that each loop runs one branch-free body
 struct TileOrder {
-  int ts_lo, nspan, nclean, tl;
+  int ts_lo, nspan, nclean, tl, rot;
   __device__ __forceinline__ void init(int spec_lo, int spec_hi, int m, int ntile, bool last_special) {
     ts_lo = spec_lo / 64;
     const int ts_hi = (spec_hi - 1) / 64;
     nspan = ts_hi - ts_lo + 1;
     tl = (last_special && (m & 63) && ntile - 1 > ts_hi) ? ntile - 1 : -1;
     nclean = ntile - nspan - (tl >= 0 ? 1 : 0);
+    rot = 0;
   }
+  // step i -> tile; the clean steps optionally rotated by `rot` (spreads the blocks that share an
+  // image over its tiles)
   __device__ __forceinline__ int at(int i) const {
+    if (i < nclean && rot) {
+      i += rot % nclean;
+      if (i >= nclean) i -= nclean;
+    }
     if (i < ts_lo) return i;
     if (i < nclean) return i + nspan;
     const int j = i - nclean;
@@ -2145,8 +2176,17 @@ __device__ __forceinline__ void pv_tile32(f32x16 (&dacc)[4], const f32x16& p, in
 __global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
   constexpr int NW = 4, XR = 32 * NW;
   __shared__ __attribute__((aligned(16))) VTile sh;
-  __shared__ float rs_sc[NW][32], rs_w[NW][32];  // per register row: w / Z and w
-  const int z = blockIdx.z, mb = blockIdx.y, xb = blockIdx.x;
+  __shared__ float rs_sc[NW][32], rs_w[NW][32], rs_pd[NW][32];  // per register row: w / Z, w, p of the diagonal
+  int z = blockIdx.z, mb = blockIdx.y, xb = blockIdx.x;
+  if (a0.xcd_order & 1) {
+    // XCD-contiguous order: the row blocks of one (mini-batch, head) share an XCD's L2
+    const int per = gridDim.x * gridDim.y;
+    const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), per * gridDim.z);
+    z = lin / per;
+    const int bid = lin - z * per;
+    mb = bid / gridDim.x;
+    xb = bid - mb * gridDim.x;
+  }
   const ClArgs a = head_args(a0, z);
   const int m = a.vm[mb];
   const int x0 = xb * XR;
@@ -2184,94 +2224,144 @@ __global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
   // the block's own sequences (compact ranges), where the same-sequence exclusion applies
   const int rlo = ridx[x0], rhi = ridx[min(x0 + XR, m) - 1];
   const int spec_lo = cs[seq_of(g, rlo)], spec_hi = cs[seq_of(g, rhi) + 1];
-  float Z = 0.f, pv = -INFINITY;
+  float Z = 0.f;
   int cn = 0, rk = 0;
   const int ntile = (m + 63) / 64;
   TileOrder ord;
   ord.init(spec_lo, spec_hi, m, ntile, true);
+  if (a0.xcd_order & 2) ord.rot = xb;  // the row blocks start their clean tiles at different columns
   VCursor cur;
   cur.init(a.vC + base * DE, m, w, lane);
   retire_loads();
   cur.stage(sh.img[0], ord.at(0), w, lane);
   if (ntile > 1) cur.stage(sh.img[1], ord.at(1), w, lane);
   if (ntile > 2) cur.stage(sh.img[2], ord.at(2), w, lane);
-  // step i of the visiting order: tile i landed (i + 1, i + 2 may still be in flight), every
-  // wave is done with step i - 1, whose ring slot takes step i + 3
+  if (ntile > 2) wait_vm<8>();
+  else if (ntile > 1) wait_vm<4>();
+  else wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  // software pipeline: step i's exp / sums / P . img run in the same basic block as step i + 1's
+  // S MFMAs (past the last step they read a stale slot and are discarded).  At the top of step
+  // i: step i + 1 landed (i + 2 may still be in flight), every wave is done with step i - 1, whose
+  // ring slot takes step i + 3.
+  f32x16 sacc[2];
+  s_tile32(sacc, sh.img[0], roff, qf);
   auto open_step = [&](int i) {
-    if (i + 2 < ntile) wait_vm<8>();
-    else if (i + 1 < ntile) wait_vm<4>();
+    if (i + 2 < ntile) wait_vm<4>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (i + 3 < ntile) cur.stage(sh.img[(i + 3) % CL_NB32], ord.at(i + 3), w, lane);
   };
+#if defined(CL_VX) && (CL_VX & 1)
+  wait_vm<0>();  // experiment: the clean loop re-reads the staged slots (no staging / waits / barriers)
+  __builtin_amdgcn_s_barrier();
+#endif
   // clean tiles: no exclusion, no pad, every element kept
   for (int i = 0; i < ord.nclean; ++i) {
+#if !defined(CL_VX) || !(CL_VX & 1)
     open_step(i);
+#endif
     const unsigned char* img = sh.img[i % CL_NB32];
-    f32x16 sacc[2];
-    s_tile32(sacc, img, roff, qf);
+    const unsigned char* imgn = sh.img[(i + 1) % CL_NB32];
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
+#if defined(CL_VX) && (CL_VX & 2)
+        (void)thr;  // experiment: no element work (P = S)
+#else
         const float sv = sacc[ib][v];
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, csh));
+        Z += p;
+        rk += sv > thr ? 1 : 0;
+        sacc[ib][v] = p;
+#endif
+      }
+    }
+    cn += 32;
+    f32x16 snext[2];
+    s_tile32(snext, imgn, roff, qf);
+    pv_tile32(dacc, sacc[0], 0, img, toff);
+    pv_tile32(dacc, sacc[1], 1, img, toff);
+#if defined(CL_SGB)
+    // interleave (A/B): per MFMA, its LDS fragment reads and CL_SGB elements' worth of VALU
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4 * CL_SGB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, CL_SGB, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 1, 0);
+    }
+#endif
+    sacc[0] = snext[0];
+    sacc[1] = snext[1];
+  }
+  // special tiles: the register rows' own sequences and the partial tile.  Per lane, the kept
+  // columns of row x form a 64-bit mask over the tile (x's own sequence, diagonal included, and
+  // the columns >= m excluded); an excluded S becomes -inf (v_bfe_i32 + v_bfi_b32), after which
+  // the clean body's operations give p = 0 and no rank.  The diagonal (always kept) enters in
+  // the epilogue, from the positive logit dg.
+  auto below = [](int k) { return k >= 64 ? ~0ull : (1ull << k) - 1ull; };
+#if defined(CL_VX) && (CL_VX & 1)
+  for (int i = ntile; i < ntile; ++i) {  // experiment: special tiles skipped
+#else
+  for (int i = ord.nclean; i < ntile; ++i) {
+#endif
+    open_step(i);
+    const unsigned char* img = sh.img[i % CL_NB32];
+    const unsigned char* imgn = sh.img[(i + 1) % CL_NB32];
+    const int y0 = 64 * ord.at(i);
+    const int lo = min(max(xlo - y0, 0), 64), hi = min(max(xlo + (int)xlen - y0, 0), 64);
+    const int me = min(max(m - y0, 0), 64);
+    uint64_t keep = live ? (below(lo) | (below(me) & ~below(hi))) : 0ull;
+    keep >>= 4 * hh;  // bit cv of this lane's element v of block ib: cv = 32 ib + 8 (v >> 2) + (v & 3)
+    const uint32_t kw[2] = {(uint32_t)keep, (uint32_t)(keep >> 32)};
+    cn += __popc(kw[0] & 0x0F0F0F0Fu) + __popc(kw[1] & 0x0F0F0F0Fu);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int msk = __builtin_amdgcn_sbfe((int)kw[ib], 8 * (v >> 2) + (v & 3), 1);
+        const float sv = __uint_as_float((__float_as_uint(sacc[ib][v]) & msk) | (0xff800000u & ~msk));
         const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, csh));
         Z += p;
         rk += sv > thr ? 1 : 0;
         sacc[ib][v] = p;
       }
     }
-    cn += 32;
+    f32x16 snext[2];
+    s_tile32(snext, imgn, roff, qf);
     pv_tile32(dacc, sacc[0], 0, img, toff);
     pv_tile32(dacc, sacc[1], 1, img, toff);
-  }
-  // special tiles: the register rows' own sequences (exclusion, diagonal) and the partial tile
-  for (int i = ord.nclean; i < ntile; ++i) {
-    open_step(i);
-    const unsigned char* img = sh.img[i % CL_NB32];
-    f32x16 sacc[2];
-    s_tile32(sacc, img, roff, qf);
-    // per-tile lane bases (laundered, else the 32 per-element offsets are hoisted into 32
-    // VGPRs each); element v of block ib is column y = y0 + 4 hh + cv, cv a compile-time constant
-    const int y0 = 64 * ord.at(i);
-    int dl = y0 + 4 * hh - xlo, dx = y0 + 4 * hh - x, dm = y0 + 4 * hh - m;
-    asm volatile("" : "+v"(dl), "+v"(dx), "+v"(dm));
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int cv = 32 * ib + 8 * (v >> 2) + (v & 3);
-        const float sv = sacc[ib][v];
-        const bool dgl = dx + cv == 0;
-        if (dgl) pv = sv * it;
-        const bool same = (unsigned)(dl + cv) < xlen;
-        const bool keep = live && dm + cv < 0 && (!same || dgl);
-        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, csh));
-        const float p = keep ? e : 0.f;
-        Z += p;
-        cn += keep ? 1 : 0;
-        rk += (keep && !dgl && sv > thr) ? 1 : 0;
-        sacc[ib][v] = p;
-      }
-    }
-    pv_tile32(dacc, sacc[0], 0, img, toff);
-    pv_tile32(dacc, sacc[1], 1, img, toff);
+    sacc[0] = snext[0];
+    sacc[1] = snext[1];
   }
   // the two lane halves hold the row's alternate column groups
   Z += __shfl_xor(Z, 32, 64);
   cn += __shfl_xor(cn, 32, 64);
   rk += __shfl_xor(rk, 32, 64);
-  pv = fmaxf(pv, __shfl_xor(pv, 32, 64));
+  // the diagonal: p = e^(S_xx / tau - 1 / tau) with S_xx / tau = dg, the positive logit
+  const float pd = live ? __builtin_amdgcn_exp2f((dg - it) * LOG2E) : 0.f;
+  Z += pd;
+  cn += live ? 1 : 0;
   const float wx = live ? a.w[base + r] : 0.f;
   if (hh == 0) {
     if (live) {
-      a.lse[base + r] = cn > 0 ? it + __logf(Z) : -INFINITY;
-      a.pos[base + r] = pv;
+      a.lse[base + r] = it + __logf(Z);
+      a.pos[base + r] = dg;
       a.cnt[base + r] = cn;
       a.rank[base + r] = rk;
     }
     rs_sc[w][r32] = (wx != 0.f && Z > 0.f) ? wx / Z : 0.f;
     rs_w[w][r32] = wx;
+    rs_pd[w][r32] = pd;
   }
   // epilogue: restage, then 16 lanes per row through F.normalize into dy
   __syncthreads();
@@ -2289,7 +2379,7 @@ __global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
     const int rr = ridx[xc];
     const int b = rr / g.L, t = rr - b * g.L;
     const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
-    const float sc = rs_sc[w][rl], wr = rs_w[w][rl];
+    const float sc = rs_sc[w][rl], wr = rs_w[w][rl], pdr = rs_pd[w][rl];
     float inv[8];
     load_vec<bf16_t, 16>(a.vC + (base + xc) * DE + 8 * sub, inv);
     const float4 u0 = *reinterpret_cast<const float4*>(&sh.ep[w][rl][8 * sub]);
@@ -2297,7 +2387,7 @@ __global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
     const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
     float gv[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) gv[i] = gs * (uu[i] * sc - wr * inv[i]);
+    for (int i = 0; i < 8; ++i) gv[i] = gs * (__builtin_fmaf(pdr, inv[i], uu[i]) * sc - wr * inv[i]);
     normalize_bwd_store(gv, a.y_raw, a.y_dtype, a.y_norm[ro], a.dy, ro * DE + 8 * sub, xr < m);
   }
 }
@@ -2411,21 +2501,40 @@ __global__ __launch_bounds__(256, 2) void cl_bwd32v_k(ClArgs a0) {
       const unsigned char* img = sh.r.img[cb];
       f32x16 acc[2];
       s_tile32(acc, img, roff, qf);
+      // kept image rows of column c as a 64-bit mask over the tile: c's own sequence is excluded
+      // except the diagonal (an excluded S becomes -inf, so its dS is 0); the diagonal's dS also
+      // carries the -w of w (p - [r == c])
       const int y0 = 64 * ord.at(i);
-      int dl = y0 + 4 * hh - xlo, dx = y0 + 4 * hh - xc;
-      asm volatile("" : "+v"(dl), "+v"(dx));
+      const int lo = min(max(xlo - y0, 0), 64), hi = min(max(xlo + (int)xlen - y0, 0), 64);
+      auto below = [](int k) { return k >= 64 ? ~0ull : (1ull << k) - 1ull; };
+      const int dd = xc - y0;
+      uint64_t keep = below(lo) | ~below(hi);
+      if (live && dd >= 0 && dd < 64) keep |= 1ull << dd;
+      keep >>= 4 * hh;
+      const uint32_t kw[2] = {(uint32_t)keep, (uint32_t)(keep >> 32)};
+      int dx = dd - 4 * hh;
+      asm volatile("" : "+v"(dx));
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int cv = 32 * ib + 8 * (v >> 2) + (v & 3), yl = cv + 4 * hh;
-          const bool same = (unsigned)(dl + cv) < xlen;
-          const bool dgl = dx + cv == 0;
-          const bool keep = live && (!same || dgl);
-          const float ysh = sh.r.m0[cb][w][yl], yw = sh.r.m1[cb][w][yl];
-          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[ib][v], c1, ysh)) - (dgl ? yw : 0.f);
-          acc[ib][v] = (keep && yw != 0.f) ? e : 0.f;
+        for (int qd = 0; qd < 4; ++qd) {
+          const float4 ys = *reinterpret_cast<const float4*>(&sh.r.m0[cb][w][32 * ib + 8 * qd + 4 * hh]);
+          const float4 ws = *reinterpret_cast<const float4*>(&sh.r.m1[cb][w][32 * ib + 8 * qd + 4 * hh]);
+          const float yv[4] = {ys.x, ys.y, ys.z, ys.w}, wv4[4] = {ws.x, ws.y, ws.z, ws.w};
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int v = 4 * qd + jj, cv = 8 * qd + jj;
+            const int msk = __builtin_amdgcn_sbfe((int)kw[ib], cv, 1);
+            const float sv = __uint_as_float((__float_as_uint(acc[ib][v]) & msk) | (0xff800000u & ~msk));
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c1, yv[jj]));
+            const uint32_t dm = 0u - (uint32_t)(dx == 32 * ib + cv);  // the diagonal: all ones
+            acc[ib][v] = e - __uint_as_float(__float_as_uint(wv4[jj]) & dm);
+          }
         }
+      if (wmask && !live) {
+        acc[0] = f32x16{};
+        acc[1] = f32x16{};
+      }
       pv_tile32(dacc, acc[0], 0, img, toff);
       pv_tile32(dacc, acc[1], 1, img, toff);
     }
@@ -2593,8 +2702,10 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
                     d->mb_size <= CL_UMAXB && (d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32);
   if (rows) a.colb = (float*)hist;  // the per-column bias lives in the histogram until the fused pass is done
   if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
-  hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb, nrun), dim3(256), 0, s, a);
-  LTHM_CHECK_LAUNCH();
+  if (!(rows && vc_ok(d))) {  // the compact path computes the diagonal in its gather
+    hipLaunchKernelGGL(cl_diag_k, dim3(64, d->n_mb, nrun), dim3(256), 0, s, a);
+    LTHM_CHECK_LAUNCH();
+  }
   const dim3 grid((d->n_max + CL_ROWS - 1) / CL_ROWS, d->n_mb, nrun);
   if (rows) {
     // forward + the row side of the backward in one pass (row weights from the pad mask first)
@@ -2611,8 +2722,11 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
       hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
       LTHM_CHECK_LAUNCH();
     }
-    static const int xcd = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : 0;
-    a.xcd_order = xcd;
+    // block order: the compact pass runs XCD-contiguous (the row blocks of one (mini-batch, head)
+    // share an XCD's L2: 4.97 -> 4.32 ms on tools/loss_bench.py, profiles/r04m_*); the full pass
+    // keeps the plain order (3-5 % faster there, tools/ab_fr_xcd.sh)
+    static const int xcd_env = getenv("LTHM_CL_FR_XCD") ? atoi(getenv("LTHM_CL_FR_XCD")) : -1;
+    a.xcd_order = xcd_env >= 0 ? xcd_env : (vc ? 1 : 0);
     if (d->main_ev0 && hipEventRecord((hipEvent_t)d->main_ev0, s) != hipSuccess) return (int)hipGetLastError();
     if (vc) hipLaunchKernelGGL(cl_fr32v_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(cl_fr32_k, dim3((d->n_max + 127) / 128, d->n_mb, nrun), dim3(256), 0, s, a);
