@@ -32,10 +32,13 @@ FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md 
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
 PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
-    "cl_fr32_k": ["cl_fr32_k"],
-    "cl_bwd32_k": ["cl_bwd32_k<"],
-    "cl_bwd_k": ["cl_bwd_k<", "cl_bwd32_k<", "cl_shift_k", "cl_dyscale_k<"],
-    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_fr32_k", "cl_used_k", "cl_stats_k", "cl_rowstats_k", "cl_wscale_k"],
+    "cl_fr32_k": ["cl_fr32_k", "cl_fr32v_k"],
+    "cl_bwd32_k": ["cl_bwd32_k<", "cl_bwd32v_k"],
+    "cl_bwd_k": ["cl_bwd_k<", "cl_bwd32_k<", "cl_bwd32v_k", "cl_shift_k", "cl_vshift_k", "cl_dyscale_k<"],
+    "cl_fwd_k": ["cl_diag_k", "cl_fwd_k<", "cl_fr32_k", "cl_fr32v_k", "cl_used_k", "cl_vpack_k", "cl_vgather_k",
+                 "cl_stats_k", "cl_rowstats_k", "cl_wscale_k"],
+    "lthm_layernorm_bwd": ["ln_bwd_v4_k<", "ln_bwd_k<"],
+    "lthm_layernorm_fwd": ["ln_fwd_v4_k<", "ln_fwd_k<"],
     "attn_bwd_k": ["attn_bwd_mfma_k<", "attn_bwd32_k<", "attn_bwd_rows_win_k<", "attn_bwd_cols_win_k<",
                    "attn_delta_k<", "attn_bwd32l_k<"],
     "attn_fwd_k": ["attn_fwd_mfma_k<", "attn_fwd_win_k<", "attn_fwd32_k<"],

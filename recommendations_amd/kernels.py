@@ -580,12 +580,15 @@ def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
     y = torch.empty((M, D), dtype=y_dtype, device=x2d.device)
     mean = torch.empty(M, dtype=torch.float32, device=x2d.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x2d.device)
+    # algorithmic bytes: x read, y written, the row statistics written
+    nb = float(M * D * (x2d.element_size() + y.element_size()) + 8 * M)
     if amax is not None:
         _check(amax.dtype == torch.int32 and amax.is_cuda, "amax is an int32 device word")
         call("lthm_layernorm_fwd_amax", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd),
-             ptr(amax), stream())
+             ptr(amax), stream(), _work=nb, _unit="byte")
     else:
-        call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream())
+        call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream(),
+             _work=nb, _unit="byte")
     return y, mean, rstd
 
 
@@ -601,8 +604,12 @@ def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True
     part = torch.empty((2, nblk, D), dtype=torch.float32, device=x2d.device)
     dx = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
     dxb = torch.empty((M, D), dtype=torch.bfloat16, device=x2d.device) if want_bf16 else None
+    # algorithmic bytes: dy, x and the residuals read, dx (and its bf16 copy) written, the row
+    # statistics read, the per-block weight-gradient partials written
+    nb = float(M * D * (dy2d.element_size() + x2d.element_size() + 4 + (4 if res1 is not None else 0)
+                        + (4 if res2 is not None else 0) + (2 if want_bf16 else 0)) + 8 * M + part.numel() * 4)
     call("lthm_layernorm_bwd", ptr(dy2d), dcode(dy2d), ptr(x2d), M, D, ptr(w), ptr(mean), ptr(rstd), ptr(res1),
-         ptr(res2), ptr(dx), ptr(dxb), ptr(part), stream())
+         ptr(res2), ptr(dx), ptr(dxb), ptr(part), stream(), _work=nb, _unit="byte")
     dw = colsum(part[0])
     db = colsum(part[1]) if need_bias else None
     return dx, dxb, dw, db
