@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 33 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 34 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -332,6 +332,14 @@ typedef struct lthm_ptower_desc {
 } lthm_ptower_desc;
 
 int lthm_product_tower_fwd(const lthm_ptower_desc* desc, void* stream);
+
+/* Row gather (scatter = 0: dst row i = src row idx[i], a zero row where idx[i] < 0) or scatter
+ * (scatter = 1: dst row idx[i] = src row i, skipped where idx[i] < 0) of `count` rows of
+ * row_bytes (a multiple of 16; 16-B aligned pointers and leading dims).  The product tower's
+ * token compaction (models/lthm/sequence/product_tower.py:43-62: a pad token's embedding is
+ * masked to zero, so the tower runs on the non-pad tokens only). */
+int lthm_rows_move(const void* src, int64_t src_ld_bytes, const int32_t* idx, int64_t count, void* dst,
+                   int64_t dst_ld_bytes, int64_t row_bytes, int32_t scatter, void* stream);
 
 /* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i < nidx <= 64 (0xffff = skip).
  * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows.

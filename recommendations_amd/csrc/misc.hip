@@ -857,3 +857,42 @@ extern "C" int lthm_moe_hidden_bwd(const float* dGH, const void* H, const void* 
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- row gather / scatter
+// Token compaction (the product tower runs on the non-pad tokens only): dst row i = src row
+// idx[i] (gather) or dst row idx[i] = src row i (scatter), rows of row_bytes (a multiple of 16),
+// 16-B lanes, a block of 256 threads walking rows.  idx[i] < 0 gathers a zero row.
+namespace lthm {
+__global__ __launch_bounds__(256) void rows_move_k(const unsigned char* __restrict__ src, int64_t sld,
+                                                   const int32_t* __restrict__ idx, int64_t count,
+                                                   unsigned char* __restrict__ dst, int64_t dld, int chunks,
+                                                   int scatter) {
+  const int64_t total = count * chunks;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / chunks;
+    const int c = (int)(e - i * chunks);
+    const int32_t j = idx[i];
+    if (scatter) {
+      if (j >= 0)
+        *reinterpret_cast<u32x4*>(dst + j * dld + 16 * c) = *reinterpret_cast<const u32x4*>(src + i * sld + 16 * c);
+    } else {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (j >= 0) v = *reinterpret_cast<const u32x4*>(src + j * sld + 16 * c);
+      *reinterpret_cast<u32x4*>(dst + i * dld + 16 * c) = v;
+    }
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_rows_move(const void* src, int64_t src_ld_bytes, const int32_t* idx, int64_t count, void* dst,
+                              int64_t dst_ld_bytes, int64_t row_bytes, int32_t scatter, void* stream) {
+  LTHM_REQUIRE(count >= 0 && row_bytes > 0 && row_bytes % 16 == 0 && src_ld_bytes % 16 == 0 && dst_ld_bytes % 16 == 0);
+  LTHM_REQUIRE(((uintptr_t)src | (uintptr_t)dst) % 16 == 0);
+  if (count == 0) return 0;
+  const int chunks = (int)(row_bytes / 16);
+  hipLaunchKernelGGL(rows_move_k, dim3(grid_for(count * chunks, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                     (const unsigned char*)src, src_ld_bytes, idx, count, (unsigned char*)dst, dst_ld_bytes, chunks,
+                     scatter);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -569,6 +569,24 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
     return dx, g, dpre
 
 
+# ----------------------------------------------------------------- row gather
+def rows_gather(src2d, idx, out=None):
+    """dst[i] = src2d[idx[i]] (a zero row where idx[i] < 0), idx int32 on the device, rows of a
+    multiple of 16 bytes (lthm_rows_move)."""
+    require_gpu(src2d, idx)
+    _check(src2d.dim() == 2 and src2d.is_contiguous() and idx.dtype == torch.int32 and idx.is_contiguous(),
+           "rows_gather takes a contiguous [n, W] source and int32 indices")
+    rb = src2d.shape[1] * src2d.element_size()
+    _check(rb % 16 == 0 and src2d.data_ptr() % 16 == 0, "rows_gather: 16-B rows")
+    c = idx.numel()
+    dst = out if out is not None else torch.empty((c, src2d.shape[1]), dtype=src2d.dtype, device=src2d.device)
+    _check(dst.is_contiguous() and tuple(dst.shape) == (c, src2d.shape[1]) and dst.dtype == src2d.dtype,
+           "rows_gather: destination shape")
+    call("lthm_rows_move", ptr(src2d), rb, ptr(idx), c, ptr(dst), rb, rb, 0, stream(), _work=2.0 * c * rb,
+         _unit="byte")
+    return dst
+
+
 # ----------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
     """amax: optional int32 [1] device word (zeroed by the caller) that receives the

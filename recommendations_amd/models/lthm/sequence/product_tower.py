@@ -12,6 +12,7 @@ is build-defined (commons/layers.py here), #2 ``num_proj`` maps to ``n_proj``,
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -22,10 +23,30 @@ from ....commons.layers import HistogramEmbedding
 from ....commons.transformers.layers import CosineVectorEmbedding
 
 
+# token compaction: a pad token (id 0) has its embedding masked to zero (product_tower.py:49,
+# 58), so no output or gradient of the tower depends on it; the tower runs on the non-pad tokens
+# and its outputs are expanded with zero rows (LTHM_TOWER_COMPACT=0: every token)
+_COMPACT = os.environ.get("LTHM_TOWER_COMPACT", "1") != "0"
+
+
 class ProductTowerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, x, w_map, b_map, w_pm, hist_w, tower, *tables):
         require_gpu(ids, x)
+        n_full = ids.numel()
+        ctx.full = None
+        if _COMPACT and n_full > 0 and x.shape[-1] * x.element_size() % 16 == 0:
+            ids_f = ids.reshape(-1)
+            valid = ids_f != 0
+            pos = torch.cumsum(valid, 0, dtype=torch.int32)
+            c = int(pos[-1])  # one 4-byte device->host read: the compact shapes
+            if c < n_full:
+                inv = torch.where(valid, pos - 1, torch.full_like(pos, -1))  # full row -> compact row or -1
+                idx = torch.nonzero(valid).view(-1).to(torch.int32)          # compact row -> full row
+                shape = ids.shape
+                ids = ids_f.index_select(0, idx.long())
+                x = K.rows_gather(x.reshape(n_full, -1).contiguous(), idx)
+                ctx.full = (shape, n_full, idx, inv)
         n = ids.numel()
         Din, Dout = x.shape[-1], w_map.shape[0]
         dev = x.device
@@ -66,7 +87,11 @@ class ProductTowerFn(torch.autograd.Function):
         call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
         w_pm_b = K.cast(w_pm.detach().contiguous(), torch.bfloat16)
         prod = K.linear_fwd(emb, w_pm_b)
-        ctx.save_for_backward(rows, xn, emb, w_pm_b)
+        # masked_fill (product_tower.py:58): no gradient reaches a masked token's pre-mask embedding;
+        # the backward zeroes those rows of `de` by a gather through this map (-1: zero row)
+        keep = torch.where(mask.bool(), torch.full((n,), -1, dtype=torch.int32, device=dev),
+                           torch.arange(n, dtype=torch.int32, device=dev))
+        ctx.save_for_backward(rows, xn, emb, w_pm_b, keep)
         ctx.meta = (R_cve, nb, [t.shape for t in tables], b_map is not None)
         mods, so = [], 0  # backward layout: per CVE module (slot0, n_proj, row0, nb+1) + the histogram slot
         for j, m in enumerate(cve):
@@ -76,18 +101,31 @@ class ProductTowerFn(torch.autograd.Function):
             mods.append((so, 1, R_cve, nb))
         ctx.modules = mods
         ctx.mark_non_differentiable(mask)
+        if ctx.full is not None:
+            shape, n_full, idx, inv = ctx.full
+            emb_f = K.rows_gather(emb, inv)
+            prod_f = K.rows_gather(prod, inv)
+            mask_f = torch.ones(n_full, dtype=torch.uint8, device=dev)
+            mask_f.index_copy_(0, idx.long(), mask)
+            return emb_f.view(*shape, Dout), prod_f.view(*shape, -1), mask_f.view(shape)
         return emb.view(*ids.shape, Dout), prod.view(*ids.shape, -1), mask.view(ids.shape)
 
     @staticmethod
     def backward(ctx, d_emb, d_prod, _dmask):
-        rows, xn, emb, w_pm_b = ctx.saved_tensors
+        rows, xn, emb, w_pm_b, keep = ctx.saved_tensors
         R_cve, nb, shapes, has_b = ctx.meta
         Dout = emb.shape[1]
         dpb = d_prod.contiguous().view(-1, d_prod.shape[-1])
         dpb = dpb if dpb.dtype == torch.bfloat16 else K.cast(dpb, torch.bfloat16)
-        dw_pm = K.linear_wgrad(dpb, emb)
         res = None if d_emb is None else d_emb.contiguous().view(-1, Dout)
+        if ctx.full is not None:  # the compact tokens' rows of the upstream gradients
+            idx = ctx.full[2]
+            dpb = K.rows_gather(dpb, idx)
+            if res is not None:
+                res = K.rows_gather(res, idx)
+        dw_pm = K.linear_wgrad(dpb, emb)
         de = K.linear_dgrad(dpb, w_pm_b, res1=res)  # bf16 total gradient of `emb`
+        de = K.rows_gather(de, keep, out=de)  # masked tokens: zero (each row reads itself or nothing)
         dw_map = K.linear_wgrad(de, xn)
         db_map = K.colsum(de) if has_b else None
         R = R_cve + max(nb, 1)

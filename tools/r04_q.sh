@@ -1,0 +1,19 @@
+# Round-4 GPU pass q: product-tower token compaction: tower / table / full-step tests, C2 bench
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r04q
+export PARITY_LOG=gpurun_out/r04q/parity.json
+timeout -k 10 400 python -u -m pytest tests/test_gpu_tables.py tests/test_gpu_lthm.py tests/test_gpu_lthm_step_golden.py tests/test_gpu_wrapper_api.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04q/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r04q/tests.log
+[ $rc -eq 0 ] || { grep -E "^FAILED|^E " gpurun_out/r04q/tests.log | head -20; exit 1; }
+grep "compaction" gpurun_out/r04q/tests.log | head -8
+n=gpurun_out/r04q/bench_c2.log
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-hbm-gather > $n 2>&1 || { tail -20 $n; exit 1; }
+python3 - $n <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith('{"metric"'):
+        d = json.loads(l)
+        print(d["value"], d["ms_per_step"], json.dumps(d["roofline"])[:200])
+        for k, v in sorted(d["kernels"].items(), key=lambda kv: -kv[1]["share"])[:22]:
+            print("   ", k, v["avg_ms"], v["calls_per_step"], round(v["avg_ms"] * v["calls_per_step"], 3))
+PY
