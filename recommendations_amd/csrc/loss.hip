@@ -2283,23 +2283,6 @@ __global__ __launch_bounds__(256, 2) void cl_fr32v_k(ClArgs a0) {
     s_tile32(snext, imgn, roff, qf);
     pv_tile32(dacc, sacc[0], 0, img, toff);
     pv_tile32(dacc, sacc[1], 1, img, toff);
-#if defined(CL_SGB)
-    // interleave (A/B): per MFMA, its LDS fragment reads and CL_SGB elements' worth of VALU
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 4 * CL_SGB, 0);
-      __builtin_amdgcn_sched_group_barrier(0x400, CL_SGB, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x400, 1, 0);
-    }
-#endif
     sacc[0] = snext[0];
     sacc[1] = snext[1];
   }
