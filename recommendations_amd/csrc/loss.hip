@@ -266,6 +266,7 @@ struct ClArgs {
   bf16_t* vC;     // [NH][n_mb][n_max][DE] compact `in` rows (column images)
   int* vpidx;     // [n_mb][mbs T] the mini-batch's valid physical `in` rows b T + t, in order
   int* vnp;       // [n_mb] their count
+  float* vnorm_out;  // compact forward without a normalised `out` (out_n null): y_norm, written by the gather
 };
 
 // the per-head view of a multi-head forward launch: head head0 + z, buffers advanced by z strides
@@ -2005,7 +2006,10 @@ __global__ __launch_bounds__(256) void cl_vpack_k(ClArgs a0, float* __restrict__
 
 // compact images: vR[i] = normalised `out` row of r_i, vC[i] = normalised `in` row of r_i, and
 // the positive logit diag[r_i] = out . in / tau with cl_diag_k's arithmetic (the compact forward
-// reads no other diag entry).  16 lanes per row, two rows per lane group in flight.
+// reads no other diag entry).  16 lanes per row, two rows per lane group in flight.  With
+// a.vnorm_out set, the `out` rows are normalised here from the raw next_token_emb (rownorm_v8_k's
+// arithmetic; their norms into y_norm): the compact path never reads the other rows.
+template <typename TY>
 __global__ __launch_bounds__(256) void cl_vgather_k(ClArgs a0) {
   const ClArgs a = head_args(a0, blockIdx.z);
   const int mb = blockIdx.y;
@@ -2017,16 +2021,38 @@ __global__ __launch_bounds__(256) void cl_vgather_k(ClArgs a0) {
   for (int i0 = blockIdx.x * 32 + (threadIdx.x >> 4); i0 < m; i0 += step) {
     int rr[2];
     u32x4 ov[2], iv[2];
+    float yv[2][8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) rr[u] = a.vridx[base + min(i0 + 16 * u, m - 1)];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      ov[u] = *reinterpret_cast<const u32x4*>(out_row(a, g, rr[u]) + sub * 8);
+      if (a.vnorm_out) {
+        const int b = rr[u] / g.L, t = rr[u] - b * g.L;
+        const int64_t ro = ((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head;
+        ld8(reinterpret_cast<const TY*>(a.y_raw) + ro * DE + sub * 8, yv[u]);
+      } else {
+        ov[u] = *reinterpret_cast<const u32x4*>(out_row(a, g, rr[u]) + sub * 8);
+      }
       iv[u] = *reinterpret_cast<const u32x4*>(in_row(a, g, rr[u]) + sub * 8);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i = i0 + 16 * u;
+      if (a.vnorm_out) {  // rownorm_v8_k<TY, 1>
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ss += yv[u][k] * yv[u][k];
+        const float nrm = sqrtf(group16_sum(ss));
+        const float den = fmaxf(nrm, 1e-12f);
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = yv[u][k] / den;
+        ov[u] = u32x4{pk_bf16(o[0], o[1]), pk_bf16(o[2], o[3]), pk_bf16(o[4], o[5]), pk_bf16(o[6], o[7])};
+        if (i < m && sub == 0) {
+          const int b = rr[u] / g.L, t = rr[u] - b * g.L;
+          a.vnorm_out[((g.b0 + b) * (a.T + 1) + t) * a.NH + a.head] = nrm;
+        }
+      }
       float acc = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -2564,7 +2590,7 @@ static ClArgs cl_args(const lthm_contrastive_desc* d) {
   a.t_raw = d->t_raw; a.t_dtype = d->t_dtype; a.t_norm = d->t_norm; a.dt = d->dt;
   a.xcd_order = 0;
   a.vm = nullptr; a.vcs = nullptr; a.vridx = nullptr; a.vsh = nullptr; a.vw = nullptr; a.vcmap = nullptr;
-  a.vR = nullptr; a.vC = nullptr; a.vpidx = nullptr; a.vnp = nullptr;
+  a.vR = nullptr; a.vC = nullptr; a.vpidx = nullptr; a.vnp = nullptr; a.vnorm_out = nullptr;
   if (d->vc_ws) {
     const VcLayout L = vc_layout(d->n_heads, d->n_mb, d->mb_size, d->T, d->n_max);
     char* b = (char*)d->vc_ws;
@@ -2595,6 +2621,7 @@ extern "C" int64_t lthm_contrastive_vc_ws_bytes(int64_t B, int32_t T, int32_t n_
 // the compact path's preconditions (beyond cl_check and the fused-rows ones)
 static bool vc_ok(const lthm_contrastive_desc* d) {
   if (!d->vc_ws) return false;
+  if (!d->out_n && !(d->y_raw && d->y_norm)) return false;
   if (d->vc_ws_bytes < vc_layout(d->n_heads, d->n_mb, d->mb_size, d->T, d->n_max).total) return false;
   return d->head == 0 && d->heads_run == d->n_heads && d->head_stride == (int64_t)d->n_mb * d->n_max &&
          d->mb_size <= CL_UMAXB && (int64_t)d->mb_size * d->T <= (1ll << 30);
@@ -2683,6 +2710,8 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
   const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
   const bool rows = fixed && d->y_raw && d->y_norm && d->dy && d->head == 0 && nrun == d->n_heads &&
                     d->mb_size <= CL_UMAXB && (d->y_dtype == LTHM_BF16 || d->y_dtype == LTHM_F32);
+  // out_n may be null only on the compact path (its gather normalises the `out` rows it needs)
+  LTHM_REQUIRE(d->out_n || (rows && vc_ok(d)));
   if (rows) a.colb = (float*)hist;  // the per-column bias lives in the histogram until the fused pass is done
   if (hipMemsetAsync(hist, 0, hm * d->n_max * 4, s) != hipSuccess) return (int)hipGetLastError();
   if (!(rows && vc_ok(d))) {  // the compact path computes the diagonal in its gather
@@ -2698,8 +2727,12 @@ extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats
       // valid-row compaction: index lists + weights + zero dy rows, then the compact images
       hipLaunchKernelGGL(cl_vpack_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
       LTHM_CHECK_LAUNCH();
-      hipLaunchKernelGGL(cl_vgather_k, dim3(std::max(1, std::min(16, d->n_max / 256)), d->n_mb, nrun), dim3(256), 0,
-                         s, a);
+      // out_n null: the gather normalises the valid `out` rows itself and writes their norms
+      ClArgs ag = a;
+      if (!d->out_n) ag.vnorm_out = const_cast<float*>(d->y_norm);
+      const dim3 gg(std::max(1, std::min(16, d->n_max / 256)), d->n_mb, nrun);
+      if (d->y_dtype == LTHM_BF16) hipLaunchKernelGGL(cl_vgather_k<bf16_t>, gg, dim3(256), 0, s, ag);
+      else hipLaunchKernelGGL(cl_vgather_k<float>, gg, dim3(256), 0, s, ag);
       LTHM_CHECK_LAUNCH();
     } else {
       hipLaunchKernelGGL(cl_used_k, dim3(d->n_mb, nrun), dim3(256), 0, s, a, d->w, loss_scale);
@@ -2750,6 +2783,7 @@ extern "C" int lthm_contrastive_bwd(const lthm_contrastive_desc* d, void* stream
   a.colb = d->diag;  // the shift scratch (advanced per head by head_args)
   hipStream_t s = (hipStream_t)stream;
   const bool fixed = 2.f / d->tau <= 80.f && !d->logq;
+  LTHM_REQUIRE(d->out_n || (fused && d->rows_done && vc_ok(d)));  // only the compact COLS pass reads no out_n
   if (fused && d->rows_done) {
     // the forward ran the ROWS side (dy for a unit upstream gradient): COLS, then dy *= gscale
     LTHM_REQUIRE(fixed && d->head == 0 && nrun == d->n_heads);

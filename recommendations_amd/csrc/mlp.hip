@@ -584,7 +584,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
           gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
           dp[4 * m + e] = dH[4 * m + e] * gd;
         }
-        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * m + 4 * h) =
+        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
             uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
       }
       const bf16x8m d0 = mlp_pack(dp), d1 = mlp_pack(dp + 8);
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
       // 4 consecutive units), then 16-B row pieces: lane -> row l / 4 (+ 16), piece l % 4
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * m + 4 * h) =
+        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
             uint2{pack_bf16x2(dp[4 * m], dp[4 * m + 1]), pack_bf16x2(dp[4 * m + 2], dp[4 * m + 3])};
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
@@ -606,8 +606,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
       for (int q = 0; q < 2; ++q) {
         const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
         const int64_t row = rb + rl;
-        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + pc);
-        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + pc);
+        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + (pc ^ (8 * ((rl >> 2) & 3))));
+        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + (pc ^ (8 * ((rl >> 2) & 3))));
         if (row < lim) {
           *reinterpret_cast<u32x4*>(a.G + row * a.HID + 32 * j + pc) = vg;
           *reinterpret_cast<u32x4*>(a.dP + row * a.HID + 32 * j + pc) = vd;
@@ -650,7 +650,9 @@ template <int D, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
   constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, TR = 32 * NW;
   __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
-  __shared__ __attribute__((aligned(16))) bf16_t stb_all[NW][2 * 32 * 32];  // per-wave g / dp strips
+  // per-wave g / dp strips: 32 rows x four 16-B chunks, chunk c of row r at c ^ ((r >> 2) & 3) (the
+  // C-layout b64 writes 2-way instead of 8-way bank-conflicted, the 16-B row reads conflict-free)
+  __shared__ __attribute__((aligned(16))) bf16_t stb_all[NW][2 * 32 * 32];
   __shared__ float b1s[4096];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
   const int NC = a.HID / 32;
@@ -710,8 +712,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
           gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
           dv[e] = dH[4 * m + e] * gd;
         }
-        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * m + 4 * h) = uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
-        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * m + 4 * h) =
+        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) = uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
+        *reinterpret_cast<uint2*>(stb + 1024 + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
             uint2{pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3])};
       }
       __builtin_amdgcn_wave_barrier();
@@ -720,8 +722,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
       for (int q = 0; q < 2; ++q) {
         const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
         const int64_t row = rb + rl;
-        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + pc);
-        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + pc);
+        const u32x4 vg = *reinterpret_cast<const u32x4*>(stb + rl * 32 + (pc ^ (8 * ((rl >> 2) & 3))));
+        const u32x4 vd = *reinterpret_cast<const u32x4*>(stb + 1024 + rl * 32 + (pc ^ (8 * ((rl >> 2) & 3))));
         if (row < lim) {
           *reinterpret_cast<u32x4*>(a.G + row * a.HID + 32 * j + pc) = vg;
           *reinterpret_cast<u32x4*>(a.dP + row * a.HID + 32 * j + pc) = vd;

@@ -55,7 +55,13 @@ class ContrastiveLossFn(torch.autograd.Function):
         dev = y.device
         yc = y.contiguous()
         tc = target.contiguous()
-        yn, ynorm = K.rownorm(yc.view(-1, De))
+        rows = (ctx.needs_input_grad[0] and not _OLD_BWD and not _NO_FUSED_ROWS and logq is None
+                and 2.0 / tau <= 80.0 and mbs <= 4096 and yc.dtype in (torch.bfloat16, torch.float32))
+        if rows and not _NO_VC:
+            # the compact path's gather normalises the `out` rows it reads (their norms into ynorm)
+            yn, ynorm = None, torch.empty(B * Tp * NH, dtype=torch.float32, device=y.device)
+        else:
+            yn, ynorm = K.rownorm(yc.view(-1, De))
         # pad positions of `in` are zero rows: every logit against them is excluded
         # anyway, and the loss kernels then need no per-element pad test
         tn, tnorm = K.rownorm(tc.view(-1, De), row_mask=mask)
@@ -82,8 +88,6 @@ class ContrastiveLossFn(torch.autograd.Function):
         d.stats_ws, d.stats_ws_bytes = ptr(ws), ws.numel() * 8
         # training at the fixed shift: the forward also runs the row side of the backward and
         # writes dy (unit upstream gradient) -- one S pass instead of the forward's plus ROWS'
-        rows = (ctx.needs_input_grad[0] and not _OLD_BWD and not _NO_FUSED_ROWS and logq is None
-                and 2.0 / tau <= 80.0 and mbs <= 4096 and yc.dtype in (torch.bfloat16, torch.float32))
         dy = None
         vc = None
         if rows:
@@ -155,6 +159,8 @@ class ContrastiveLossFn(torch.autograd.Function):
             # a second backward through this graph (retain_graph): the first one scaled the
             # forward's dy in place and returned it, so run the ROWS side again into a fresh dy
             dy_f = None
+        if yn is None and dy_f is None:  # the full passes read every normalised `out` row
+            yn, ynorm = K.rownorm(yc.view(-1, De))
         if dy_f is not None:
             ctx.dy_consumed = True
         dy = dy_f if dy_f is not None else torch.empty_like(yc)
