@@ -195,6 +195,26 @@ def cast_multi_bf16(ts):
     return outs
 
 
+def cast_multi_bf16_into(ts, outs):
+    """outs[i][:] = bf16(ts[i]) for contiguous fp32 sources and bf16 destinations of the same
+    element counts (e.g. row slices of one image), one launch per 48 tensors."""
+    import ctypes
+    ts = [t.detach() for t in ts]
+    n = len(ts)
+    _check(n == len(outs), "cast_multi_bf16_into: one destination per source")
+    for t, o in zip(ts, outs):
+        require_gpu(t, o)
+        _check(t.dtype == torch.float32 and o.dtype == torch.bfloat16 and t.numel() == o.numel()
+               and t.is_contiguous() and o.is_contiguous(), "cast_multi_bf16_into: fp32 -> bf16, equal sizes")
+    if n == 0:
+        return outs
+    arr = lambda xs: ctypes.cast((ctypes.c_void_p * n)(*[x.data_ptr() for x in xs]), ctypes.c_void_p)  # noqa: E731
+    cnt = (ctypes.c_int64 * n)(*[t.numel() for t in ts])
+    call("lthm_cast_multi_bf16", n, arr(ts), arr(outs), ctypes.cast(cnt, ctypes.c_void_p), stream(),
+         _key="cast_multi_k", _work=6.0 * sum(t.numel() for t in ts), _unit="byte")
+    return outs
+
+
 class bf16_operands:
     """Context: the bf16 copies of ``params`` (fp32), cast in one launch on entry and
     served by ``bf16_operand`` until exit.  Scopes nest; the innermost match wins."""

@@ -53,16 +53,35 @@ class ProductTowerFn(torch.autograd.Function):
         cve = tower.direction_emb
         R_cve = sum(t.shape[0] for t in tables)
         nb = tower.norm_bins if tower.norm_bins > 1 else 0
-        # bf16 gather images of the small tables (cast kernel into one buffer)
+        # bf16 gather images of the small tables (one buffer) and the product_mapper operand:
+        # one multi-tensor cast launch (f32 masters; a per-table cast was 8 launches)
         tab = torch.empty((R_cve + max(nb, 1), Dout), dtype=torch.bfloat16, device=dev)
-        r = 0
+        w_pm_b = torch.empty(w_pm.shape, dtype=torch.bfloat16, device=dev)
+        srcs, dsts, r = [], [], 0
         for t in tables:
-            call("lthm_cast", ptr(t), dcode(t), ptr(tab[r]), dcode(tab), t.numel(), stream())
+            srcs.append(t.detach().contiguous())
+            dsts.append(tab[r:r + t.shape[0]])
             r += t.shape[0]
         if nb:
-            call("lthm_cast", ptr(hist_w), dcode(hist_w), ptr(tab[R_cve]), dcode(tab), hist_w.numel(), stream())
-        proj = torch.cat([m.projection_mat.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
-        grids = torch.cat([m.grid.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
+            srcs.append(hist_w.detach().contiguous())
+            dsts.append(tab[R_cve:R_cve + nb])
+        srcs.append(w_pm.detach().contiguous())
+        dsts.append(w_pm_b)
+        if all(t.dtype == torch.float32 for t in srcs):
+            K.cast_multi_bf16_into(srcs, dsts)
+        else:
+            for t, o in zip(srcs, dsts):
+                call("lthm_cast", ptr(t), dcode(t), ptr(o), dcode(o), t.numel(), stream())
+        # the CVE buffers' concatenation, kept while the buffers are unchanged
+        key = tuple((m.projection_mat.data_ptr(), m.projection_mat._version, m.grid.data_ptr(), m.grid._version)
+                    for m in cve)
+        hit = getattr(tower, "_cve_cat", None)
+        if hit is not None and hit[0] == key:
+            proj, grids = hit[1], hit[2]
+        else:
+            proj = torch.cat([m.projection_mat.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
+            grids = torch.cat([m.grid.reshape(-1) for m in cve]) if len(cve) else torch.zeros(1, device=dev)
+            tower._cve_cat = (key, proj, grids)
         total = sum(m.n_proj for m in cve) + (1 if nb else 0)
         emb = torch.empty((n, Dout), dtype=torch.bfloat16, device=dev)
         rows = torch.empty((n, total), dtype=torch.int16, device=dev)
@@ -85,7 +104,6 @@ class ProductTowerFn(torch.autograd.Function):
             go += m.grid.numel()
         d.emb_out, d.rows_out, d.xn_out, d.mask_out = ptr(emb), ptr(rows), ptr(xn), ptr(mask)
         call("lthm_product_tower_fwd", ctypes.addressof(d), stream())
-        w_pm_b = K.cast(w_pm.detach().contiguous(), torch.bfloat16)
         prod = K.linear_fwd(emb, w_pm_b)
         # masked_fill (product_tower.py:58): no gradient reaches a masked token's pre-mask embedding;
         # the backward zeroes those rows of `de` by a gather through this map (-1: zero row)

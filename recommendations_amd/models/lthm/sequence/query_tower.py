@@ -97,8 +97,11 @@ class OutcomeHeadsFn(torch.autograd.Function):
              oc.shape[0], d, ptr(xo), ptr(rows), stream())
         Pe = head_ws[0].shape[0]
         wcat = torch.empty((len(head_ws) * Pe, d), dtype=torch.bfloat16, device=x.device)
-        for i, w in enumerate(head_ws):
-            call("lthm_cast", ptr(w), dcode(w), ptr(wcat[i * Pe]), dcode(wcat), w.numel(), stream())
+        if all(w.dtype == torch.float32 and w.is_contiguous() for w in head_ws):
+            K.cast_multi_bf16_into(list(head_ws), [wcat[i * Pe:(i + 1) * Pe] for i in range(len(head_ws))])
+        else:
+            for i, w in enumerate(head_ws):
+                call("lthm_cast", ptr(w), dcode(w), ptr(wcat[i * Pe]), dcode(wcat), w.numel(), stream())
         y = K.linear_fwd(xo, wcat)
         ctx.save_for_backward(xo, rows, wcat)
         ctx.meta = (B, Tp, d, len(head_ws), Pe, oc.shape[0])
