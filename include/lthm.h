@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 34 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 35 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -340,6 +340,28 @@ int lthm_product_tower_fwd(const lthm_ptower_desc* desc, void* stream);
  * masked to zero, so the tower runs on the non-pad tokens only). */
 int lthm_rows_move(const void* src, int64_t src_ld_bytes, const int32_t* idx, int64_t count, void* dst,
                    int64_t dst_ld_bytes, int64_t row_bytes, int32_t scatter, void* stream);
+
+/* Shared pad prefix (query_tower.py:99-137 over left-padded histories, encoder.py:52): with causal
+ * attention, no dropout and the same position-0 token for every sequence, a pad position's state
+ * depends only on its position, so the encoder runs the pad chain (positions 0 .. P) once and
+ * each sequence's positions past its pads ("packed" rows: the chain first, then the sequences'
+ * valid positions in order).
+ *   stats:  npad[b] = leading set bytes of mask row b; stats = {1 if every row is a prefix mask,
+ *           sum of T - npad, P = max npad, the first b with npad = P (the chain's owner)}.
+ *   maps:   full row f = b Tp + p (Tp = T + 1) -> packed row pof[f] (the chain row p for p <= npad[b]);
+ *           pof_x[f] the same but -1 at the pad rows of every sequence except the owner;
+ *           fop[r] = the full row of packed row r (chain rows: the owner's).  voff[b] = exclusive
+ *           prefix sum of T - npad.
+ *   sum:    dst[p] (p <= P, packed chain rows) = sum over b with npad[b] >= p of src[b Tp + p]
+ *           (rows of W elements, bf16 or f32, W % 8 == 0; fixed order); ws of
+ *           lthm_pad_prefix_ws_bytes bytes. */
+int lthm_pad_prefix_stats(const uint8_t* mask, int64_t mask_stride, int32_t B, int32_t T, int32_t* npad,
+                          int32_t* stats, void* stream);
+int lthm_pad_prefix_maps(const int32_t* npad, const int64_t* voff, int32_t B, int32_t Tp, int32_t P, int32_t owner,
+                         int32_t* pof, int32_t* pof_x, int32_t* fop, void* stream);
+int64_t lthm_pad_prefix_ws_bytes(int32_t B, int32_t P, int32_t W);
+int lthm_pad_prefix_sum(const void* src, int32_t dtype, int32_t W, const int32_t* npad, int32_t B, int32_t Tp,
+                        int32_t P, void* dst, void* ws, int64_t ws_bytes, void* stream);
 
 /* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i < nidx <= 64 (0xffff = skip).
  * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows.

@@ -211,6 +211,10 @@ def sub_events(key: str, work: float = None, unit: str = None, nbytes: float = N
     return e0, e1
 
 
+def timer_on() -> bool:
+    return TIMER is not None
+
+
 def TIMER_RECORDS() -> list:
     """The live timer's records (key, ev0, ev1, work, unit, bytes) as mutable lists, or [] when the
     timer is off: a wrapper replaces a record's work by a callable once the device knows it."""

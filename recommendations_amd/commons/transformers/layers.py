@@ -95,11 +95,17 @@ class TransformerBlockFn(torch.autograd.Function):
 
     @staticmethod
     def _forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wp, bp, table, ln2w, ln2b, w1, b1, w2, b2, H, causal,
-                 double_residual, fp8=False, drop=None, mask=None, infer=False):
+                 double_residual, fp8=False, drop=None, mask=None, infer=False, pack=None):
         require_gpu(x)
-        B, T, d = x.shape
+        if pack is not None:
+            # packed rows (shared pad prefix, recommendations_amd/pad_prefix.py): row-wise work on
+            # the M packed rows, attention on the full-length sequences rebuilt from them
+            M, d = x.shape
+            B, T = pack.B, pack.Tp
+        else:
+            B, T, d = x.shape
+            M = B * T
         E = d // H
-        M = B * T
         x2 = x.contiguous().view(M, d)
         wqkv_b, wp_b, w1_b, w2_b = _bf(wqkv), _bf(wp), _bf(w1), _bf(w2)
         # am: the activations' max |x| words for the fp8 mode, reduced by their producers
@@ -123,7 +129,14 @@ class TransformerBlockFn(torch.autograd.Function):
             K.dropout_rows_(qkv, 3, pa, seed)  # the attention sees (and the backward saves) the scaled q / k / v
         tab = None if table is None else table.detach().contiguous()
         mop = K.attn_mask_operand(mask, B, H, T)
-        o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop)
+        if pack is not None:
+            qkv_f = pack.unpack(qkv)
+            o_f, lse = K.attn_fwd_qkv(qkv_f, B, T, H, E, tab, causal, mop)
+            o = pack.pack(o_f)
+        else:
+            qkv_f, o_f = qkv, None
+            o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop)
+        ctx.pack, ctx.o_full = pack, o_f
         if fp8:
             K.amax_(o, am[1:2])
         if pr > 0.0:
@@ -142,14 +155,14 @@ class TransformerBlockFn(torch.autograd.Function):
                 h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
                 out = K.mlp_fwd(h2, w1_b, _f(b1), w2t_b, _f(b2), res1=x1, res2=x2 if double_residual else None)
             if infer:
-                return out.view(B, T, d)
-            ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, _f(b1), w2t_b,
+                return out if pack is not None else out.view(B, T, d)
+            ctx.save_for_backward(x2, h1, mu1, rs1, qkv_f, o, lse, x1, h2, mu2, rs2, _f(b1), w2t_b,
                                   wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
             ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
                        b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
             ctx.mop = mop
             ctx.fused_mlp = True
-            return out.view(B, T, d)
+            return out if pack is not None else out.view(B, T, d)
         h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
@@ -164,20 +177,21 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             out = lin(g, w2_b, _f(b2), res1=x1, res2=x2 if double_residual else None, out_dtype=torch.float32,
                       amax_in=gam)
-        ctx.save_for_backward(x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g,
+        ctx.save_for_backward(x2, h1, mu1, rs1, qkv_f, o, lse, x1, h2, mu2, rs2, pre, g,
                               wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w, tab)
         ctx.cfg = (B, T, d, H, E, causal, double_residual, ln1b is not None, bqkv is not None, bp is not None,
                    b1 is not None, b2 is not None, None if table is None else table.shape, pa, pr, seed)
         ctx.mop = mop
         ctx.fused_mlp = False
-        return out.view(B, T, d)
+        return out if pack is not None else out.view(B, T, d)
 
     @staticmethod
     def _backward(ctx, dout):
         (x2, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g, wqkv_b, wp_b, w1_b, w2_b, ln1w, ln2w,
          tab) = ctx.saved_tensors
         B, T, d, H, E, causal, dbl, has_ln1b, has_bqkv, has_bp, has_b1, has_b2, tshape, pa, pr, seed = ctx.cfg
-        M = B * T
+        pack = ctx.pack
+        M = x2.shape[0]
         dy = dout.contiguous().view(M, d)
         if dy.dtype != torch.float32:
             dy = dy.float()
@@ -212,7 +226,14 @@ class TransformerBlockFn(torch.autograd.Function):
         dwp = K.linear_wgrad(dx1b, o)
         dbp = K.colsum(dx1r) if has_bp else None
         do = K.linear_dgrad(dx1b, wp_b)
-        dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal, ctx.mop)
+        if pack is not None:
+            # dO only at the rows the packed output read (the chain from its owner); K / V
+            # gradients at pad rows summed over the sequences into the chain rows
+            dqkv_f, dtab = K.attn_bwd_qkv(qkv, ctx.o_full, pack.unpack_owner(do), lse, B, T, H, E, tab, causal,
+                                          ctx.mop)
+            dqkv = pack.reduce(dqkv_f)
+        else:
+            dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal, ctx.mop)
         if pa > 0.0:
             K.dropout_rows_(dqkv, 3, pa, seed)
         dwqkv = K.linear_wgrad(dqkv, h1)
@@ -225,8 +246,9 @@ class TransformerBlockFn(torch.autograd.Function):
         if tshape is not None:
             dtable = torch.zeros(tshape, dtype=torch.float32, device=dy.device)
             dtable[: dtab.shape[0]] = dtab
-        return (dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp, dbp, dtable,
-                dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None, None, None)
+        return (dx if pack is not None else dx.view(B, T, d), dln1w, dln1b if has_ln1b else None, dwqkv, dbqkv, dwp,
+                dbp, dtable, dln2w, dln2b if has_ln1b else None, dw1, db1, dw2, db2, None, None, None, None, None, None,
+                None, None)
 
 
 # ------------------------------------------------------------------ modules
@@ -545,9 +567,9 @@ class TransformerBlock(nn.Module):
         a, m = self.attn, self.mlp
         return [a.c_attn.weight, a.c_proj.weight, m.c_fc.weight, m.c_proj.weight]
 
-    def _fused(self, x, double_residual: bool, attn_mask: Optional[torch.Tensor] = None):
-        if x.dim() != 3:
-            raise ValueError("TransformerBlock expects [B, T, d]")
+    def _fused(self, x, double_residual: bool, attn_mask: Optional[torch.Tensor] = None, pack=None):
+        if x.dim() != (2 if pack is not None else 3):
+            raise ValueError("TransformerBlock expects [B, T, d] (packed rows: [M, d])")
         if self.is_moe:
             T = x.shape[1]
             mask = attn_mask
@@ -559,7 +581,8 @@ class TransformerBlock(nn.Module):
             y = y + self.mlp(self.ln_2(y))
             return y + x if double_residual else y
         if self.attn.attn.table is not None:
-            self.attn.attn.pos_bias.check(x.shape[1], x.shape[1])
+            tl = pack.Tp if pack is not None else x.shape[1]
+            self.attn.attn.pos_bias.check(tl, tl)
         drop = _drop_args(self, self.attn.attn_dropout.p, self.attn.resid_dropout.p)
         if drop is not None and self.mlp.dropout.p != drop[1]:
             raise NotImplementedError("the fused block applies one dropout p to the attention output and the MLP")
@@ -570,7 +593,7 @@ class TransformerBlock(nn.Module):
         with K.bf16_operands(self.gemm_weights()):
             # a general attn_mask is added to the scores on top of the causal flag (:404-408)
             return TransformerBlockFn.apply(x.float(), *args, self.attn.n_head, self.is_causal,
-                                            double_residual, self.fp8_gemm, drop, attn_mask, infer)
+                                            double_residual, self.fp8_gemm, drop, attn_mask, infer, pack)
 
     def _checkpointing(self) -> bool:
         return bool(self.enable_gradient_checkpointing and self.training and torch.is_grad_enabled())
@@ -614,13 +637,21 @@ class TransformerBlock(nn.Module):
             x_final[:, not_idx] = rest + self._null(rest)
         return x_final
 
-    def forward_double_residual(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_double_residual(self, x: torch.Tensor, pack=None) -> torch.Tensor:
         """x + block(x) in one op (models/lthm/sequence/query_tower.py:132-137); checkpointed
-        like forward (the reference checkpoints block(x) and adds x outside)."""
+        like forward (the reference checkpoints block(x) and adds x outside).  ``pack``: x is
+        the packed rows of a shared pad prefix (recommendations_amd/pad_prefix.py)."""
         if self._checkpointing():
-            return torch.utils.checkpoint.checkpoint(self._fused, x, True, use_reentrant=False,
+            return torch.utils.checkpoint.checkpoint(self._fused, x, True, None, pack, use_reentrant=False,
                                                      preserve_rng_state=True)
-        return self._fused(x, True)
+        return self._fused(x, True, None, pack)
+
+    def pad_prefix_ok(self) -> bool:
+        """The block keeps a pad position's state a function of its position: causal, dense,
+        no dropout in effect."""
+        return (self.is_causal and not self.is_moe and not self.is_sparse
+                and _drop_args(self, self.attn.attn_dropout.p, self.attn.resid_dropout.p) is None
+                and (not self.training or self.mlp.dropout.p == 0.0))
 
 
 # ------------------------------------------------------------------ vector-feature layers

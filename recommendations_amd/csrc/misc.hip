@@ -896,3 +896,164 @@ extern "C" int lthm_rows_move(const void* src, int64_t src_ld_bytes, const int32
   LTHM_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- shared pad prefix
+// Encoder over left-padded histories (query_tower.py:99-110 after encoder.py:52's flip): with
+// causal attention, no dropout and a position-0 token that is the same for every sequence, a
+// pad position p of sequence b attends to positions 0 .. p only, all pads, so its state at
+// every layer depends on p alone.  The encoder then runs a "packed" token set: the chain
+// (positions 0 .. P of the longest prefix, once) and each sequence's positions past its pads.
+//   pad_prefix_stats_k  per sequence: npad (leading mask bytes set) and whether the mask is a
+//                       prefix; batch totals into stats {ok, valid, max npad, argmax}
+//   pad_prefix_maps_k   full row (b, p) -> packed row (pof; pof_x: -1 at the pad rows of every
+//                       sequence but the chain's owner) and packed row -> full row (fop)
+//   pad_prefix_sum_k    chain row p of a packed gradient = sum over the sequences with
+//                       npad >= p of their row p (fixed order: per 32-sequence chunk, then
+//                       the chunks in order), the valid rows copied from their full rows
+namespace lthm {
+__global__ __launch_bounds__(256) void pad_prefix_stats_k(const uint8_t* __restrict__ mask, int64_t mstride, int B,
+                                                          int T, int* __restrict__ npad, int* __restrict__ stats) {
+  for (int b = blockIdx.x * 256 + threadIdx.x; b < B; b += gridDim.x * 256) {
+    const uint8_t* m = mask + (int64_t)b * mstride;
+    int n = 0;
+    while (n < T && m[n]) ++n;
+    bool ok = true;
+    for (int t = n; t < T; ++t) ok = ok && !m[t];
+    npad[b] = n;
+    if (!ok) atomicAnd(stats, 0);
+    atomicAdd(stats + 1, T - n);
+    atomicMax(stats + 2, n);
+  }
+}
+__global__ void pad_prefix_init_k(int* __restrict__ stats, int B) {
+  if (threadIdx.x == 0) {
+    stats[0] = 1;
+    stats[1] = 0;
+    stats[2] = 0;
+    stats[3] = B;
+  }
+}
+__global__ __launch_bounds__(256) void pad_prefix_owner_k(const int* __restrict__ npad, int B, int* __restrict__ stats) {
+  for (int b = blockIdx.x * 256 + threadIdx.x; b < B; b += gridDim.x * 256)
+    if (npad[b] == stats[2]) atomicMin(stats + 3, b);
+}
+// Tp = T + 1 positions (0 = the shared first token); voff[b] = packed row of b's first valid position
+__global__ __launch_bounds__(256) void pad_prefix_maps_k(const int* __restrict__ npad, const int64_t* __restrict__ voff,
+                                                         int B, int Tp, int P, int owner, int32_t* __restrict__ pof,
+                                                         int32_t* __restrict__ pof_x, int32_t* __restrict__ fop) {
+  const int64_t n = (int64_t)B * Tp;
+  for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < n; f += (int64_t)gridDim.x * 256) {
+    const int b = (int)(f / Tp), p = (int)(f - (int64_t)b * Tp);
+    const int np = npad[b];
+    if (p <= np) {  // position 0 and the pads: the chain row p
+      pof[f] = p;
+      pof_x[f] = b == owner ? p : -1;
+      if (b == owner) fop[p] = (int32_t)f;
+    } else {
+      const int32_t r = (int32_t)(P + 1 + voff[b] + (p - np - 1));
+      pof[f] = r;
+      pof_x[f] = r;
+      fop[r] = (int32_t)f;
+    }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void ld8f(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const u32x4 u = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(u[k] << 16);
+      v[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+  }
+}
+// pass 1: grid (chain rows, sequence chunks of 32); 8 columns per thread
+template <typename T>
+__global__ __launch_bounds__(256) void pad_prefix_part_k(const T* __restrict__ src, int W, const int* __restrict__ npad,
+                                                         int B, int Tp, float* __restrict__ part, int P) {
+  const int p = blockIdx.x, ch = blockIdx.y;
+  const int b0 = ch * 32, b1 = min(b0 + 32, B);
+  float* out = part + ((int64_t)ch * (P + 1) + p) * W;
+  for (int c = threadIdx.x * 8; c < W; c += 256 * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = b0; b < b1; ++b) {
+      if (npad[b] < p) continue;
+      float v[8];
+      ld8f<T>(src + ((int64_t)b * Tp + p) * W + c, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+    *reinterpret_cast<float4*>(out + c) = float4{acc[0], acc[1], acc[2], acc[3]};
+    *reinterpret_cast<float4*>(out + c + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
+  }
+}
+// pass 2: chain row p = the chunks' partial sums in order
+template <typename T>
+__global__ __launch_bounds__(256) void pad_prefix_fold_k(const float* __restrict__ part, int nch, int W, int P,
+                                                         T* __restrict__ dst) {
+  const int64_t n = (int64_t)(P + 1) * W;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < nch; ++k) s += part[(int64_t)k * n + e];
+    if constexpr (sizeof(T) == 2) dst[e] = f2bf(s);
+    else dst[e] = s;
+  }
+}
+}  // namespace lthm
+
+extern "C" int lthm_pad_prefix_stats(const uint8_t* mask, int64_t mask_stride, int32_t B, int32_t T, int32_t* npad,
+                                     int32_t* stats, void* stream) {
+  LTHM_REQUIRE(B > 0 && T > 0 && mask_stride >= T && mask && npad && stats);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pad_prefix_init_k, dim3(1), dim3(64), 0, s, stats, B);
+  LTHM_CHECK_LAUNCH();
+  const int grid = (B + 255) / 256;
+  hipLaunchKernelGGL(pad_prefix_stats_k, dim3(grid), dim3(256), 0, s, mask, mask_stride, B, T, npad, stats);
+  LTHM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pad_prefix_owner_k, dim3(grid), dim3(256), 0, s, (const int*)npad, B, stats);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_pad_prefix_maps(const int32_t* npad, const int64_t* voff, int32_t B, int32_t Tp, int32_t P,
+                                    int32_t owner, int32_t* pof, int32_t* pof_x, int32_t* fop, void* stream) {
+  LTHM_REQUIRE(B > 0 && Tp > 1 && P >= 0 && P < Tp && owner >= 0 && owner < B && (int64_t)B * Tp < (1ll << 31));
+  hipLaunchKernelGGL(pad_prefix_maps_k, dim3(grid_for((int64_t)B * Tp, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                     (const int*)npad, voff, B, Tp, P, owner, pof, pof_x, fop);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t lthm_pad_prefix_ws_bytes(int32_t B, int32_t P, int32_t W) {
+  if (B <= 0 || P < 0 || W <= 0) return -1;
+  return (int64_t)((B + 31) / 32) * (P + 1) * W * 4;
+}
+
+extern "C" int lthm_pad_prefix_sum(const void* src, int32_t dtype, int32_t W, const int32_t* npad, int32_t B, int32_t Tp,
+                                   int32_t P, void* dst, void* ws, int64_t ws_bytes, void* stream) {
+  LTHM_REQUIRE(src && dst && npad && W > 0 && W % 8 == 0 && B > 0 && Tp > 1 && P >= 0 && P < Tp);
+  LTHM_REQUIRE(ws && ws_bytes >= lthm_pad_prefix_ws_bytes(B, P, W));
+  LTHM_REQUIRE(dtype == LTHM_BF16 || dtype == LTHM_F32);
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = (B + 31) / 32;
+  float* part = (float*)ws;
+  const dim3 g1(P + 1, nch);
+  const int g2 = grid_for((int64_t)(P + 1) * W, 256, 2048);
+  if (dtype == LTHM_BF16) {
+    hipLaunchKernelGGL(pad_prefix_part_k<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)src, W, (const int*)npad, B, Tp,
+                       part, P);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL(pad_prefix_fold_k<bf16_t>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (bf16_t*)dst);
+  } else {
+    hipLaunchKernelGGL(pad_prefix_part_k<float>, g1, dim3(256), 0, s, (const float*)src, W, (const int*)npad, B, Tp,
+                       part, P);
+    LTHM_CHECK_LAUNCH();
+    hipLaunchKernelGGL(pad_prefix_fold_k<float>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (float*)dst);
+  }
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from .... import kernels as K
-from ...._lib import STRUCTS, TIMER_RECORDS, call, dcode, load, ptr, stream, sub_events
+from ...._lib import STRUCTS, TIMER_RECORDS, call, dcode, load, ptr, stream, sub_events, timer_on
 from ....commons.base_model_wrapper import BaseModelWrapper
 from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
@@ -107,8 +107,9 @@ class ContrastiveLossFn(torch.autograd.Function):
             d.main_ev0, d.main_ev1 = ev[0].cuda_event, ev[1].cuda_event
         call("lthm_contrastive_fwd", ctypes.addressof(d), ptr(stats), nstat, ptr(ks_dev), len(ks),
              1.0 / n_mb, stream(), _key="cl_fwd_k", _work=work, _unit="flop")
-        if vc is not None and ev is not None:
-            # the timer's work of both compact passes: 2 x 2 m^2 De per (mini-batch, head)
+        if vc is not None and timer_on():
+            # the timer's work of both compact passes: 2 x 2 m^2 De per (mini-batch, head); kept
+            # for the backward's record also when this forward's passes are not timed
             mv = vc[:NH * n_mb * 4].view(torch.int32).clone()
             vwork = lambda: 4.0 * De * float((mv.double() ** 2).sum())  # noqa: E731
             want = {"cl_fr32_k", "cl_fwd_k"}  # this call's two records, the latest of their keys

@@ -403,3 +403,55 @@ def test_item_prefetch_matches_inline(dev, sharded):
     la, _ = m.train_step(a, out)
     lb, _ = ref_m.train_step(a, exp)
     assert torch.equal(la.detach(), lb.detach())
+
+
+@pytest.mark.parametrize("ckpt", [False, True])
+def test_pad_prefix_matches_full_encoder(dev, ckpt):
+    """No context token (n_cat = 0, the C5 / reference model): the encoder runs the shared pad
+    chain once plus each history's positions past its pads (recommendations_amd/pad_prefix.py).
+    The step's outputs and every gradient match the full [B, T+1] encoder (forward rows go
+    through the same kernels: bit-exact except where the GEMM tiling sees another M; the
+    gradients sum the pad rows in another order: within 1e-2)."""
+    import copy
+    from recommendations_amd.data import synthetic_lthm_batch
+    from recommendations_amd.models.lthm.sequence import query_tower as qt
+    cfg, m = _model(dev, T=48, d=128, L=2, H=2, n_cat=0, gradient_checkpointing=ckpt)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    ref_m = copy.deepcopy(m)
+    batch = synthetic_lthm_batch(96, 48, n_cat=0, seed=31, device=dev, min_len=1)
+    batch["product_ids"][5, :] = 0                                    # a fully padded history
+    batch["product_ids"][7, 30:] = 0
+    prefix = {}
+    orig = qt.PadPrefix.build
+
+    def spy(mask, min_gain=0.1):
+        pp = orig(mask, min_gain)
+        prefix["pp"] = pp
+        return pp
+    qt.PadPrefix.build = staticmethod(spy)
+    try:
+        assert qt._PAD_PREFIX
+        torch.manual_seed(3)
+        out = m(batch)
+        loss, _ = m.train_step(batch, out)
+        loss.backward()
+        qt._PAD_PREFIX = False
+        torch.manual_seed(3)
+        exp = ref_m(batch)
+        loss_ref, _ = ref_m.train_step(batch, exp)
+        loss_ref.backward()
+    finally:
+        qt._PAD_PREFIX = True
+        qt.PadPrefix.build = orig
+    pp = prefix["pp"]
+    assert pp is not None and pp.M < 0.9 * pp.B * pp.Tp, "the packed path did not run"
+    check("next_token_emb", relerr(out["next_token_emb"].float(), exp["next_token_emb"].float()), 2e-3)
+    check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 2e-3)
+    sd = dict(ref_m.named_parameters())
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        check(f"grad {n}", relerr(p.grad, sd[n].grad), 1e-2)
