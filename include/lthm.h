@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 35 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 36 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -272,6 +272,20 @@ typedef struct lthm_attn_desc {
   int64_t mask_batch_stride;  /* 0 broadcasts one mask over the batch */
   int64_t mask_head_stride;   /* 0 broadcasts over the heads */
   int64_t mask_row_stride;    /* >= T */
+  /* packed rows (shared pad prefix, lthm_pad_prefix_*; T > 256, E = 64, no mask): when row_map
+   * is set the batch strides are unused and row t of sequence b is row row_map[b * T + t] of
+   * q / k / v (and of out / dout / dq through live_map, -1 = not this sequence's row: its dout
+   * reads as zero, its out / dq are not written, and query tiles with no live row are skipped).
+   * dK / dV of a key in the chain (row < chain_rows) go to dk_chain / dv_chain row
+   * b * chain_rows + t (token stride chain_ts, head stride = k / v head stride), the others to
+   * dk / dv at their packed row. */
+  const int32_t* row_map;
+  const int32_t* live_map;
+  void* dk_chain;
+  void* dv_chain;
+  int64_t chain_ts;
+  int32_t chain_rows;
+  int32_t pad1;
 } lthm_attn_desc;
 
 /* bf16 q/k/v/out, f32 table [table_rows, H] (row q-k+T), lse f32 [B, H, T].
@@ -353,15 +367,15 @@ int lthm_rows_move(const void* src, int64_t src_ld_bytes, const int32_t* idx, in
  *           fop[r] = the full row of packed row r (chain rows: the owner's).  voff[b] = exclusive
  *           prefix sum of T - npad.
  *   sum:    dst[p] (p <= P, packed chain rows) = sum over b with npad[b] >= p of src[b Tp + p]
- *           (rows of W elements, bf16 or f32, W % 8 == 0; fixed order); ws of
- *           lthm_pad_prefix_ws_bytes bytes. */
+ *           (W elements of rows src_ld / dst_ld elements apart, bf16 or f32, W, src_ld, dst_ld
+ *           multiples of 8; fixed order); ws of lthm_pad_prefix_ws_bytes bytes. */
 int lthm_pad_prefix_stats(const uint8_t* mask, int64_t mask_stride, int32_t B, int32_t T, int32_t* npad,
                           int32_t* stats, void* stream);
 int lthm_pad_prefix_maps(const int32_t* npad, const int64_t* voff, int32_t B, int32_t Tp, int32_t P, int32_t owner,
                          int32_t* pof, int32_t* pof_x, int32_t* fop, void* stream);
 int64_t lthm_pad_prefix_ws_bytes(int32_t B, int32_t P, int32_t W);
-int lthm_pad_prefix_sum(const void* src, int32_t dtype, int32_t W, const int32_t* npad, int32_t B, int32_t Tp,
-                        int32_t P, void* dst, void* ws, int64_t ws_bytes, void* stream);
+int lthm_pad_prefix_sum(const void* src, int64_t src_ld, int32_t dtype, int32_t W, const int32_t* npad, int32_t B,
+                        int32_t Tp, int32_t P, void* dst, int64_t dst_ld, void* ws, int64_t ws_bytes, void* stream);
 
 /* dW[rows[t, i]] += dY[t, :] for all tokens t, slots i < nidx <= 64 (0xffff = skip).
  * LDS-privatised EmbeddingBag / Embedding backward for tables of R < 65535 rows.

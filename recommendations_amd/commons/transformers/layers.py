@@ -129,7 +129,10 @@ class TransformerBlockFn(torch.autograd.Function):
             K.dropout_rows_(qkv, 3, pa, seed)  # the attention sees (and the backward saves) the scaled q / k / v
         tab = None if table is None else table.detach().contiguous()
         mop = K.attn_mask_operand(mask, B, H, T)
-        if pack is not None:
+        if pack is not None and K.attn_packed_ok(T, E, mop):
+            qkv_f, o_f = qkv, None  # the kernels read the packed rows through the pad-prefix maps
+            o, lse = K.attn_fwd_qkv(qkv, B, T, H, E, tab, causal, mop, pack=pack)
+        elif pack is not None:
             qkv_f = pack.unpack(qkv)
             o_f, lse = K.attn_fwd_qkv(qkv_f, B, T, H, E, tab, causal, mop)
             o = pack.pack(o_f)
@@ -226,7 +229,9 @@ class TransformerBlockFn(torch.autograd.Function):
         dwp = K.linear_wgrad(dx1b, o)
         dbp = K.colsum(dx1r) if has_bp else None
         do = K.linear_dgrad(dx1b, wp_b)
-        if pack is not None:
+        if pack is not None and ctx.o_full is None:
+            dqkv, dtab = K.attn_bwd_qkv(qkv, o, do, lse, B, T, H, E, tab, causal, ctx.mop, pack=pack)
+        elif pack is not None:
             # dO only at the rows the packed output read (the chain from its owner); K / V
             # gradients at pad rows summed over the sequences into the chain rows
             dqkv_f, dtab = K.attn_bwd_qkv(qkv, ctx.o_full, pack.unpack_owner(do), lse, B, T, H, E, tab, causal,

@@ -36,7 +36,33 @@ struct AttnArgs {
   const float* mask;         // additive [., ., T, T] or null (VALU kernels only)
   int64_t m_bs, m_hs, m_rs;
   int tail;                  // attn_bwd32_k: the last query as a vector pass (bwd32_tail_mode)
+  // packed rows (shared pad prefix; the long-T' 32x32x16 kernels): row t of sequence b is row
+  // rmap[b T + t] of q / k / v (batch strides unused); wmap the same with -1 where the row is not
+  // the sequence's own (a pad of a sequence other than the chain's owner): its dO reads as zero,
+  // its O / dQ are not stored, query tiles with no own row are skipped.  dK / dV of chain rows
+  // (packed row < chain) go to dk_chain / dv_chain row b chain + t (token stride chain_ts).
+  const int* rmap;
+  const int* wmap;
+  bf16_t *dk_chain, *dv_chain;
+  int64_t chain_ts;
+  int chain;
 };
+
+// the packed row of (b, t) through `map` (rmap / wmap), or t + the batch offset when unmapped
+__device__ __forceinline__ int64_t row_of(const int* map, int64_t b, int T, int t, int64_t bs_rows) {
+  return map ? (int64_t)map[b * T + t] : b * bs_rows + t;
+}
+
+// the first query tile holding a row the sequence owns (0 unless packed): tiles before it are
+// pads of a sequence other than the chain's owner, whose outputs and gradients nobody reads
+__device__ __forceinline__ int first_own_tile(const AttnArgs& a, int b, int T) {
+  if (!a.wmap) return 0;
+  const int* w = a.wmap + (int64_t)b * T;
+  const int nt = (T + 31) >> 5;
+  int t = 0;
+  while (t < nt && w[min(32 * t + 31, T - 1)] < 0) ++t;
+  return t;
+}
 
 __device__ __forceinline__ const float* mask_head(const AttnArgs& a, int b, int h) {
   return a.mask ? a.mask + (int64_t)b * a.m_bs + (int64_t)h * a.m_hs : nullptr;
@@ -756,13 +782,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // image of rows [0, Tk) (row r at src + r * ts; rows >= T zero) by LDS-DMA: 1-KiB pieces of
 // 8 rows, the lane loading the chunk that the swizzle puts in its lane-linear slot
+// map (packed rows): row r at src + map[r] * ts, a zero row where map[r] < 0
 __device__ __forceinline__ void stage_img32(unsigned char* img, const bf16_t* __restrict__ src, int64_t ts, int T,
-                                            int Tk, int wave, int lane, int nw) {
+                                            int Tk, int wave, int lane, int nw, const int* map = nullptr) {
   for (int d = wave; d < Tk / 8; d += nw) {
     const int row = 8 * d + (lane >> 3), slot = lane & 7;
     const int u = row >> 1;
     const int ch = slot ^ (((u & 1) << 2) | ((u >> 1) & 3));
-    const void* p = row < T ? (const void*)(src + (int64_t)row * ts + ch * 8) : (const void*)attn_zero16;
+    const int64_t rr = row < T ? (map ? (int64_t)map[row] : (int64_t)row) : -1;
+    const void* p = rr >= 0 ? (const void*)(src + rr * ts + ch * 8) : (const void*)attn_zero16;
     glds16(p, img + d * 1024);
   }
 }
@@ -841,11 +869,14 @@ __device__ __forceinline__ bf16x8v tr_at(const unsigned char* lo, const unsigned
 
 // 32 x 32 transposed-gradient accumulator (row e = 32 nd + 8 g + 4 hh + j in the registers,
 // column = the token r0 + (lane & 31)) stored as 8-byte runs of the token's row
+// map (packed rows): token r stored at row map[r], not at all where map[r] < 0
 __device__ __forceinline__ void store_accT32(const f32x16& x, float scale, bf16_t* __restrict__ base, int64_t ts,
-                                             int r0, int nd, int T, int lane) {
+                                             int r0, int nd, int T, int lane, const int* map = nullptr) {
   const int r = r0 + (lane & 31), hh = lane >> 5;
   if (r >= T) return;
-  bf16_t* row = base + (int64_t)r * ts + 32 * nd + 4 * hh;
+  const int64_t rr = map ? (int64_t)map[r] : (int64_t)r;
+  if (rr < 0) return;
+  bf16_t* row = base + rr * ts + 32 * nd + 4 * hh;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const uint2 w = {pk_bf16_rne(x[4 * g] * scale, x[4 * g + 1] * scale),
@@ -934,15 +965,16 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
   const int q0 = 32 * i, q = q0 + r32;
   bf16x8v gq[4], gd[4];
   if constexpr (G) {
-    const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
-    const bf16_t* dg = a.dout + b * a.o_bs + h * a.o_hs;
+    const bool pk = a.rmap != nullptr;
+    const bf16_t* qg = a.q + (pk ? 0 : b * a.q_bs) + h * a.q_hs;
+    const bf16_t* dg = a.dout + (pk ? 0 : b * a.o_bs) + h * a.o_hs;
+    const int64_t rq = q < Tu ? (pk ? (int64_t)a.rmap[(int64_t)b * T + q] : (int64_t)q) : 0;
+    const int64_t rd = q < Tu ? (pk ? (int64_t)a.wmap[(int64_t)b * T + q] : (int64_t)q) : -1;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       u32x4 u = {0u, 0u, 0u, 0u}, v = u;
-      if (q < Tu) {
-        u = *reinterpret_cast<const u32x4*>(qg + (int64_t)q * a.q_ts + 16 * s + 8 * hh);
-        v = *reinterpret_cast<const u32x4*>(dg + (int64_t)q * a.o_ts + 16 * s + 8 * hh);
-      }
+      if (q < Tu) u = *reinterpret_cast<const u32x4*>(qg + rq * a.q_ts + 16 * s + 8 * hh);
+      if (rd >= 0) v = *reinterpret_cast<const u32x4*>(dg + rd * a.o_ts + 16 * s + 8 * hh);
       gq[s] = __builtin_bit_cast(bf16x8v, u);
       gd[s] = __builtin_bit_cast(bf16x8v, v);
     }
@@ -1018,9 +1050,11 @@ __device__ __forceinline__ void bwd32_rows(const AttnArgs& a, const Bwd32Smem& m
     const int d = 32 * (i - jend) + r32 + T;
     if (hh == 0 && d >= 0 && d <= 2 * T) atomicAdd(&m.dbias[d], carry);
   }
-  bf16_t* dqg = a.dq + b * a.q_bs + h * a.q_hs;
+  const bool pk = G && a.wmap != nullptr;
+  bf16_t* dqg = a.dq + (pk ? 0 : b * a.q_bs) + h * a.q_hs;
 #pragma unroll
-  for (int nd = 0; nd < 2; ++nd) store_accT32(dq[nd], rs, dqg, a.q_ts, q0, nd, T, lane);
+  for (int nd = 0; nd < 2; ++nd)
+    store_accT32(dq[nd], rs, dqg, a.q_ts, q0, nd, T, lane, pk ? a.wmap + (int64_t)b * T : nullptr);
 }
 
 // columns unit: dK, dV of key tile j
@@ -1051,22 +1085,24 @@ __device__ __forceinline__ void cols_math(f32x16& sx, f32x16& px, const float* b
 // holds only the Q / dO images)
 template <bool G = false>
 __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m, const Frag32Off& fo, int b, int h,
-                                           int j, int lane, int Tu) {
+                                           int j, int lane, int Tu, int ilo = 0) {
   constexpr float L2E = 1.4426950408889634f;
   const int T = a.T, nt = (Tu + 31) >> 5, hh = lane >> 5, r32 = lane & 31;
   const float rs = rsqrtf((float)E_BWD32), c2 = rs * L2E;
   const bool ragged = (Tu & 31) != 0;
   const int k0 = 32 * j, k = k0 + r32;
   bf16x8v gk[4], gv[4];
+  const bool pkd = G && a.rmap != nullptr;
+  const int64_t rk = k < Tu ? (pkd ? (int64_t)a.rmap[(int64_t)b * T + k] : (int64_t)k) : 0;
   if constexpr (G) {
-    const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
-    const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
+    const bf16_t* kg = a.k + (pkd ? 0 : b * a.k_bs) + h * a.k_hs;
+    const bf16_t* vg = a.v + (pkd ? 0 : b * a.v_bs) + h * a.v_hs;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       u32x4 u = {0u, 0u, 0u, 0u}, v = u;
       if (k < Tu) {
-        u = *reinterpret_cast<const u32x4*>(kg + (int64_t)k * a.k_ts + 16 * s + 8 * hh);
-        v = *reinterpret_cast<const u32x4*>(vg + (int64_t)k * a.v_ts + 16 * s + 8 * hh);
+        u = *reinterpret_cast<const u32x4*>(kg + rk * a.k_ts + 16 * s + 8 * hh);
+        v = *reinterpret_cast<const u32x4*>(vg + rk * a.v_ts + 16 * s + 8 * hh);
       }
       gk[s] = __builtin_bit_cast(bf16x8v, u);
       gv[s] = __builtin_bit_cast(bf16x8v, v);
@@ -1082,7 +1118,7 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
       dk[nd][v] = 0.f;
       dv[nd][v] = 0.f;
     }
-  const int i0 = a.causal ? j : 0;
+  const int i0 = max(a.causal ? j : 0, ilo);
   // bias of (q0 + 4 hh + jj, k): ascending copy, 32 entries on per tile
   const int e0 = 32 * i0 + 4 * hh - k + T + BPAD;
   const float* bp = m.bfw + (e0 & 1) * m.ne + (e0 & ~1);
@@ -1139,6 +1175,20 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
           dv[nd][4 * g + jj] = fmaf(pk, of[jj], dv[nd][4 * g + jj]);
         }
       }
+  }
+  if (pkd) {
+    // a chain key's gradient is one sequence's share of the chain row's: to the chain buffer
+    // (summed over the sequences afterwards), the others to their packed row
+    if (k >= T) return;
+    const bool ch = rk < a.chain;
+    bf16_t* dkg = ch ? a.dk_chain + ((int64_t)b * a.chain + k) * a.chain_ts + h * a.k_hs : a.dk + rk * a.k_ts + h * a.k_hs;
+    bf16_t* dvg = ch ? a.dv_chain + ((int64_t)b * a.chain + k) * a.chain_ts + h * a.v_hs : a.dv + rk * a.v_ts + h * a.v_hs;
+#pragma unroll
+    for (int nd = 0; nd < 2; ++nd) {
+      store_accT32(dk[nd], rs, dkg - (int64_t)(k0 + r32) * a.k_ts, a.k_ts, k0, nd, T, lane);
+      store_accT32(dv[nd], 1.f, dvg - (int64_t)(k0 + r32) * a.v_ts, a.v_ts, k0, nd, T, lane);
+    }
+    return;
   }
   bf16_t* dkg = a.dk + b * a.k_bs + h * a.k_hs;
   bf16_t* dvg = a.dv + b * a.v_bs + h * a.v_hs;
@@ -1450,9 +1500,11 @@ __global__ __launch_bounds__(256) void attn_delta_k(AttnArgs a) {
     const int q = (int)(bq % a.T);
     const int64_t b = bq / a.T;
     float d = 0.f;
-    if (r < n) {
-      const bf16_t* dp = a.dout + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ts + c * 8;
-      const bf16_t* op = a.o + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ts + c * 8;
+    const int64_t rr = r < n ? (a.wmap ? (int64_t)a.wmap[b * a.T + q] : (int64_t)q) : -1;
+    if (rr >= 0) {
+      const int64_t bo = a.wmap ? 0 : b * a.o_bs;
+      const bf16_t* dp = a.dout + bo + h * a.o_hs + rr * a.o_ts + c * 8;
+      const bf16_t* op = a.o + bo + h * a.o_hs + rr * a.o_ts + c * 8;
       const u32x4 u = *reinterpret_cast<const u32x4*>(dp);
       const u32x4 v = *reinterpret_cast<const u32x4*>(op);
 #pragma unroll
@@ -1794,13 +1846,17 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
   const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool pk = a.rmap != nullptr;
+  const int* rm = pk ? a.rmap + (int64_t)b * T : nullptr;
+  const int* wm = pk ? a.wmap + (int64_t)b * T : nullptr;
   if (ROWS) {
-    stage_img32(I0, a.k + b * a.k_bs + h * a.k_hs, a.k_ts, T, Ti, wave, lane, NW);
-    stage_img32(I1, a.v + b * a.v_bs + h * a.v_hs, a.v_ts, T, Ti, wave, lane, NW);
+    stage_img32(I0, a.k + (pk ? 0 : b * a.k_bs) + h * a.k_hs, a.k_ts, T, Ti, wave, lane, NW, rm);
+    stage_img32(I1, a.v + (pk ? 0 : b * a.v_bs) + h * a.v_hs, a.v_ts, T, Ti, wave, lane, NW, rm);
   } else {
-    stage_img32(I0, a.q + b * a.q_bs + h * a.q_hs, a.q_ts, T, Ti, wave, lane, NW);
-    stage_img32(I1, a.dout + b * a.o_bs + h * a.o_hs, a.o_ts, T, Ti, wave, lane, NW);
+    stage_img32(I0, a.q + (pk ? 0 : b * a.q_bs) + h * a.q_hs, a.q_ts, T, Ti, wave, lane, NW, rm);
+    stage_img32(I1, a.dout + (pk ? 0 : b * a.o_bs) + h * a.o_hs, a.o_ts, T, Ti, wave, lane, NW, wm);
   }
+  const int tl0 = first_own_tile(a, b, T);  // query tiles before tl0: no own row, skipped
   for (int c = 0; c < 2; ++c)
     for (int y = tid; y < ne; y += 64 * NW) {
       const int x = ROWS ? ne - 1 - (y + c) - BPAD : y + c - BPAD;
@@ -1826,7 +1882,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
     int load[NW] = {};
     for (int c = nt; c >= 1; --c) {
       const int t = ROWS ? c - 1 : nt - c;
-      const int cost = (a.causal ? c : nt) + 1;
+      if (ROWS && t < tl0) continue;
+      const int cost = (ROWS ? (a.causal ? c : nt) : nt - max(a.causal ? t : 0, tl0)) + 1;
       int w = 0;
 #pragma unroll
       for (int j = 1; j < NW; ++j)
@@ -1839,7 +1896,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd32l_k(AttnArgs a) {
     const int t = ROWS ? c - 1 : nt - c;
     if (!((mk[t >> 5] >> (t & 31)) & 1u)) continue;
     if (ROWS) bwd32_rows<true>(a, m, fo, b, h, t, lane, T);
-    else bwd32_cols<true>(a, m, fo, b, h, t, lane, T);
+    else bwd32_cols<true>(a, m, fo, b, h, t, lane, T, tl0);
   }
   if (ROWS && a.dtable_part) {
     __syncthreads();
@@ -1876,11 +1933,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
   const int bh = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bh / a.H, h = bh - (bh / a.H) * a.H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, r32 = lane & 31;
-  const bf16_t* qg = a.q + b * a.q_bs + h * a.q_hs;
-  const bf16_t* kg = a.k + b * a.k_bs + h * a.k_hs;
-  const bf16_t* vg = a.v + b * a.v_bs + h * a.v_hs;
-  stage_img32(IK, kg, a.k_ts, T, Ti, wave, lane, NW);
-  stage_img32(IV, vg, a.v_ts, T, Ti, wave, lane, NW);
+  const bool pk = a.rmap != nullptr;
+  const int* rm = pk ? a.rmap + (int64_t)b * T : nullptr;
+  const int* wm = pk ? a.wmap + (int64_t)b * T : nullptr;
+  const bf16_t* qg = a.q + (pk ? 0 : b * a.q_bs) + h * a.q_hs;
+  const bf16_t* kg = a.k + (pk ? 0 : b * a.k_bs) + h * a.k_hs;
+  const bf16_t* vg = a.v + (pk ? 0 : b * a.v_bs) + h * a.v_hs;
+  stage_img32(IK, kg, a.k_ts, T, Ti, wave, lane, NW, rm);
+  stage_img32(IV, vg, a.v_ts, T, Ti, wave, lane, NW, rm);
+  const int tl0 = first_own_tile(a, b, T);  // query tiles before tl0: no own row, skipped
   for (int c = 0; c < 2; ++c)
     for (int y = tid; y < ne; y += 64 * NW) {
       const int xr = ne - 1 - (y + c) - BPAD;
@@ -1896,7 +1957,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
   uint32_t lo_mask = 0, hi_mask = 0;  // up to 64 tiles
   {
     int load[NW] = {};
-    for (int t = nt - 1; t >= 0; --t) {
+    for (int t = nt - 1; t >= tl0; --t) {
       const int cost = (a.causal ? t + 1 : nt) + 1;
       int w = 0;
 #pragma unroll
@@ -1909,8 +1970,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
       }
     }
   }
-  bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
+  bf16_t* og = a.o + (pk ? 0 : b * a.o_bs) + h * a.o_hs;
   float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  for (int q = tid; q < 32 * tl0 && q < T; q += 64 * NW) lse_g[q] = 0.f;  // skipped rows: finite, unread
   for (int t = nt - 1; t >= 0; --t) {
     if (!((t < 32 ? lo_mask >> t : hi_mask >> (t - 32)) & 1u)) continue;
     const int i = t, q0 = 32 * i, q = q0 + r32;
@@ -1918,7 +1980,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (q < T) v = *reinterpret_cast<const u32x4*>(qg + (int64_t)q * a.q_ts + 16 * s + 8 * hh);
+      if (q < T) v = *reinterpret_cast<const u32x4*>(qg + (rm ? (int64_t)rm[q] : (int64_t)q) * a.q_ts + 16 * s + 8 * hh);
       qf[s] = __builtin_bit_cast(bf16x8v, v);
     }
     f32x16 o[2];
@@ -1994,7 +2056,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd32_k(AttnArgs a) {
     l += __shfl_xor(l, 32, 64);
     const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int nd = 0; nd < 2; ++nd) store_accT32(o[nd], inv, og, a.o_ts, q0, nd, T, lane);
+    for (int nd = 0; nd < 2; ++nd) store_accT32(o[nd], inv, og, a.o_ts, q0, nd, T, lane, wm);
     if (hh == 0 && q < T) lse_g[q] = l > 0.f ? (m + __log2f(l)) * LN2 : -INFINITY;
   }
 }
@@ -2030,6 +2092,12 @@ static int attn_launch_bwd32l(const AttnArgs& a, int B, hipStream_t s) {
 }
 
 static int attn_dispatch(const AttnArgs& a, int B, int E, bool bwd, hipStream_t s) {
+  if (a.rmap) {  // packed rows: the long-T' 32x32x16 kernels only
+    if (a.mask || !attn_windowed(a.T) || E != 64 || !a.wmap) return (int)hipErrorInvalidValue;
+    if (!bwd) return fwd32_ok(a) ? attn_launch_fwd32(a, B, s) : (int)hipErrorInvalidValue;
+    if (!a.dk_chain || !a.dv_chain || a.chain <= 0) return (int)hipErrorInvalidValue;
+    return bwd32l_ok(a) ? attn_launch_bwd32l(a, B, s) : (int)hipErrorInvalidValue;
+  }
   if (a.mask) {  // general additive mask: the whole-head VALU kernels
     if (a.T > 256) return (int)hipErrorInvalidValue;
     switch (E) {
@@ -2079,6 +2147,9 @@ static void fill_common(AttnArgs& a, const lthm_attn_desc* d) {
   a.m_bs = d->mask_batch_stride;
   a.m_hs = d->mask_head_stride;
   a.m_rs = d->mask_row_stride;
+  a.rmap = d->row_map; a.wmap = d->live_map;
+  a.dk_chain = (bf16_t*)d->dk_chain; a.dv_chain = (bf16_t*)d->dv_chain;
+  a.chain_ts = d->chain_ts; a.chain = d->chain_rows;
 }
 
 static int check_desc(const lthm_attn_desc* d) {

@@ -973,8 +973,9 @@ __device__ __forceinline__ void ld8f(const T* p, float* v) {
 }
 // pass 1: grid (chain rows, sequence chunks of 32); 8 columns per thread
 template <typename T>
-__global__ __launch_bounds__(256) void pad_prefix_part_k(const T* __restrict__ src, int W, const int* __restrict__ npad,
-                                                         int B, int Tp, float* __restrict__ part, int P) {
+__global__ __launch_bounds__(256) void pad_prefix_part_k(const T* __restrict__ src, int64_t ld, int W,
+                                                         const int* __restrict__ npad, int B, int Tp,
+                                                         float* __restrict__ part, int P) {
   const int p = blockIdx.x, ch = blockIdx.y;
   const int b0 = ch * 32, b1 = min(b0 + 32, B);
   float* out = part + ((int64_t)ch * (P + 1) + p) * W;
@@ -983,7 +984,7 @@ __global__ __launch_bounds__(256) void pad_prefix_part_k(const T* __restrict__ s
     for (int b = b0; b < b1; ++b) {
       if (npad[b] < p) continue;
       float v[8];
-      ld8f<T>(src + ((int64_t)b * Tp + p) * W + c, v);
+      ld8f<T>(src + ((int64_t)b * Tp + p) * ld + c, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += v[k];
     }
@@ -994,13 +995,14 @@ __global__ __launch_bounds__(256) void pad_prefix_part_k(const T* __restrict__ s
 // pass 2: chain row p = the chunks' partial sums in order
 template <typename T>
 __global__ __launch_bounds__(256) void pad_prefix_fold_k(const float* __restrict__ part, int nch, int W, int P,
-                                                         T* __restrict__ dst) {
+                                                         T* __restrict__ dst, int64_t ld) {
   const int64_t n = (int64_t)(P + 1) * W;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
     float s = 0.f;
     for (int k = 0; k < nch; ++k) s += part[(int64_t)k * n + e];
-    if constexpr (sizeof(T) == 2) dst[e] = f2bf(s);
-    else dst[e] = s;
+    const int64_t r = e / W, c = e - r * W;
+    if constexpr (sizeof(T) == 2) dst[r * ld + c] = f2bf(s);
+    else dst[r * ld + c] = s;
   }
 }
 }  // namespace lthm
@@ -1033,9 +1035,12 @@ extern "C" int64_t lthm_pad_prefix_ws_bytes(int32_t B, int32_t P, int32_t W) {
   return (int64_t)((B + 31) / 32) * (P + 1) * W * 4;
 }
 
-extern "C" int lthm_pad_prefix_sum(const void* src, int32_t dtype, int32_t W, const int32_t* npad, int32_t B, int32_t Tp,
-                                   int32_t P, void* dst, void* ws, int64_t ws_bytes, void* stream) {
-  LTHM_REQUIRE(src && dst && npad && W > 0 && W % 8 == 0 && B > 0 && Tp > 1 && P >= 0 && P < Tp);
+extern "C" int lthm_pad_prefix_sum(const void* src, int64_t src_ld, int32_t dtype, int32_t W, const int32_t* npad,
+                                   int32_t B, int32_t Tp, int32_t P, void* dst, int64_t dst_ld, void* ws,
+                                   int64_t ws_bytes, void* stream) {
+  LTHM_REQUIRE(src && dst && npad && W > 0 && W % 8 == 0 && B > 0 && Tp > 0 && P >= 0 && P < Tp);
+  LTHM_REQUIRE(src_ld >= W && dst_ld >= W && src_ld % 8 == 0 && dst_ld % 8 == 0);
+  LTHM_REQUIRE(((uintptr_t)src % 16) == 0);
   LTHM_REQUIRE(ws && ws_bytes >= lthm_pad_prefix_ws_bytes(B, P, W));
   LTHM_REQUIRE(dtype == LTHM_BF16 || dtype == LTHM_F32);
   hipStream_t s = (hipStream_t)stream;
@@ -1044,15 +1049,17 @@ extern "C" int lthm_pad_prefix_sum(const void* src, int32_t dtype, int32_t W, co
   const dim3 g1(P + 1, nch);
   const int g2 = grid_for((int64_t)(P + 1) * W, 256, 2048);
   if (dtype == LTHM_BF16) {
-    hipLaunchKernelGGL(pad_prefix_part_k<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)src, W, (const int*)npad, B, Tp,
-                       part, P);
+    hipLaunchKernelGGL(pad_prefix_part_k<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)src, src_ld, W, (const int*)npad,
+                       B, Tp, part, P);
     LTHM_CHECK_LAUNCH();
-    hipLaunchKernelGGL(pad_prefix_fold_k<bf16_t>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (bf16_t*)dst);
+    hipLaunchKernelGGL(pad_prefix_fold_k<bf16_t>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (bf16_t*)dst,
+                       dst_ld);
   } else {
-    hipLaunchKernelGGL(pad_prefix_part_k<float>, g1, dim3(256), 0, s, (const float*)src, W, (const int*)npad, B, Tp,
-                       part, P);
+    hipLaunchKernelGGL(pad_prefix_part_k<float>, g1, dim3(256), 0, s, (const float*)src, src_ld, W, (const int*)npad,
+                       B, Tp, part, P);
     LTHM_CHECK_LAUNCH();
-    hipLaunchKernelGGL(pad_prefix_fold_k<float>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (float*)dst);
+    hipLaunchKernelGGL(pad_prefix_fold_k<float>, dim3(g2), dim3(256), 0, s, (const float*)part, nch, W, P, (float*)dst,
+                       dst_ld);
   }
   LTHM_CHECK_LAUNCH();
   return 0;

@@ -671,16 +671,20 @@ def attn_mask_operand(mask, B, H, T):
     return m, (0 if m.shape[0] == 1 else m.stride(0)), (0 if m.shape[1] == 1 else m.stride(1)), m.stride(2)
 
 
-def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs, mask=None):
+def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs, mask=None, pack=None):
     from ._lib import STRUCTS
     _check(min(B, T, H, E) >= 1 and T <= 4096 and (T <= 256 or E in (32, 64, 128)),
            f"attention takes 1 <= T <= 4096 (E in 32/64/128 beyond T = 256; got B={B} T={T} H={H} E={E})")
-    _need(q, (B - 1) * T * q_ts + (T - 1) * q_ts + (H - 1) * E + E, "q")
-    _need(k, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "k")
-    _need(v, (B - 1) * T * kv_ts + (T - 1) * kv_ts + (H - 1) * kv_hs + E, "v")
-    _need(out, B * T * H * E, "out")
+    rows = pack.M if pack is not None else B * T  # packed rows: the maps index M rows
+    _need(q, (rows - 1) * q_ts + (H - 1) * E + E, "q")
+    _need(k, (rows - 1) * kv_ts + (H - 1) * kv_hs + E, "k")
+    _need(v, (rows - 1) * kv_ts + (H - 1) * kv_hs + E, "v")
+    _need(out, rows * H * E, "out")
     _need(lse, B * H * T, "lse")
     d = STRUCTS["lthm_attn_desc"]()
+    if pack is not None:
+        _check(attn_packed_ok(T, E, mask) and pack.B == B and pack.Tp == T, "packed attention: T > 256, E = 64, no mask")
+        d.row_map, d.live_map = ptr(pack.pof), ptr(pack.pof_x)
     d.q, d.k, d.v = ptr(q), ptr(k), ptr(v)
     d.q_tok_stride, d.k_tok_stride, d.v_tok_stride = q_ts, kv_ts, kv_ts
     d.q_head_stride, d.k_head_stride, d.v_head_stride = E, kv_hs, kv_hs
@@ -695,16 +699,23 @@ def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs,
     return d
 
 
-def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True, mask=None):
-    """qkv bf16 [B*T, 3*H*E] (c_attn output) -> out bf16 [B*T, H*E], lse f32 [B, H, T]."""
+def attn_packed_ok(T, E, mask=None):
+    """The attention kernels read packed rows (a shared pad prefix's row maps) directly: the
+    long-T' 32x32x16 kernels (T > 256, E = 64, no general mask)."""
+    return T > 256 and E == 64 and mask is None
+
+
+def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True, mask=None, pack=None):
+    """qkv bf16 [B*T, 3*H*E] (c_attn output) -> out bf16 [B*T, H*E], lse f32 [B, H, T].
+    pack (recommendations_amd/pad_prefix.py, attn_packed_ok): qkv and out are the packed rows."""
     import ctypes
     C = H * E
-    out = torch.empty((B * T, C), dtype=torch.bfloat16, device=qkv.device)
+    out = torch.empty((qkv.shape[0] if pack is not None else B * T, C), dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
     q = qkv
     k = qkv[:, C:]
     v = qkv[:, 2 * C:]
-    d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask)
+    d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask, pack=pack)
     call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
          _unit="flop")
     return out, lse
@@ -725,8 +736,10 @@ def attn_fwd_mqa(q, kv, B, T, H, E, table=None, causal=True, mask=None):
     return out, lse
 
 
-def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=None):
-    """-> dqkv bf16 [B*T, 3C], dtable f32 [2T+1, H] (or None)."""
+def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=None, pack=None):
+    """-> dqkv bf16 [B*T, 3C], dtable f32 [2T+1, H] (or None).  pack: qkv / out / dout / dqkv
+    are packed rows; the chain keys' dK / dV shares land in a [B, P+1, 2C] buffer whose
+    per-sequence rows are then summed into the chain rows."""
     import ctypes
     C = H * E
     dqkv = torch.empty_like(qkv)
@@ -734,11 +747,19 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=
     parts = int(load().lthm_attn_bwd_parts(B, T))
     part = torch.empty((parts, 2 * T + 1, H), dtype=torch.float32, device=qkv.device) if table is not None else None
     delta = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device) if T > 256 else None
-    d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask)
+    d = _attn_desc(qkv, qkv[:, C:], qkv[:, 2 * C:], B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask,
+                   pack=pack)
     d.dout, d.dq, d.dk, d.dv = ptr(dout), ptr(dqkv), ptr(dqkv[:, C:]), ptr(dqkv[:, 2 * C:])
+    chain = None
+    if pack is not None:
+        _check(dout.shape == out.shape and dout.is_contiguous(), "attn_bwd_qkv: packed dout")
+        chain = torch.empty((B * (pack.P + 1), 2 * C), dtype=torch.bfloat16, device=qkv.device)
+        d.dk_chain, d.dv_chain, d.chain_ts, d.chain_rows = ptr(chain), ptr(chain[:, C:]), 2 * C, pack.P + 1
     d.dtable_part, d.delta = ptr(part), ptr(delta)
     call("lthm_attn_bwd", ctypes.addressof(d), stream(), _key="attn_bwd_k", _work=10.0 * B * H * T * T * E,
          _unit="flop")
+    if chain is not None:
+        pack.chain_sum(chain, 2 * C, pack.P + 1, dqkv[:, C:])
     dtab = None
     if part is not None:
         dtab = colsum(part.view(parts, (2 * T + 1) * H)).view(2 * T + 1, H)

@@ -65,11 +65,16 @@ class PadPrefix:
         sequences with npad >= p."""
         W = full2d.shape[1]
         dst = K.rows_gather(full2d, self.fop)
-        wsb = load().lthm_pad_prefix_ws_bytes(self.B, self.P, W)
-        ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=full2d.device)
-        call("lthm_pad_prefix_sum", ptr(full2d), dcode(full2d), W, ptr(self.npad), self.B, self.Tp, self.P, ptr(dst),
-             ptr(ws), ws.numel() * 4, stream(), _key="pad_prefix_sum")
+        self.chain_sum(full2d, W, self.Tp, dst)
         return dst
+
+    def chain_sum(self, src, W, rows_per_seq, dst):
+        """dst rows 0 .. P (leading dim dst.stride(0)) = the chain sums of src viewed as
+        [B, rows_per_seq, src.stride(0)] (the first W columns of each row)."""
+        wsb = load().lthm_pad_prefix_ws_bytes(self.B, self.P, W)
+        ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=src.device)
+        call("lthm_pad_prefix_sum", ptr(src), src.stride(0), dcode(src), W, ptr(self.npad), self.B, rows_per_seq,
+             self.P, ptr(dst), dst.stride(0), ptr(ws), ws.numel() * 4, stream(), _key="pad_prefix_sum")
 
 
 class PackFn(torch.autograd.Function):

@@ -405,23 +405,25 @@ def test_item_prefetch_matches_inline(dev, sharded):
     assert torch.equal(la.detach(), lb.detach())
 
 
-@pytest.mark.parametrize("ckpt", [False, True])
-def test_pad_prefix_matches_full_encoder(dev, ckpt):
+@pytest.mark.parametrize("T,ckpt", [(48, False), (48, True), (300, False), (300, True)])
+def test_pad_prefix_matches_full_encoder(dev, T, ckpt):
     """No context token (n_cat = 0, the C5 / reference model): the encoder runs the shared pad
     chain once plus each history's positions past its pads (recommendations_amd/pad_prefix.py).
     The step's outputs and every gradient match the full [B, T+1] encoder (forward rows go
     through the same kernels: bit-exact except where the GEMM tiling sees another M; the
-    gradients sum the pad rows in another order: within 1e-2)."""
+    gradients sum the pad rows in another order: within 1e-2).  T = 300 (T' > 256, E = 64): the
+    attention kernels read the packed rows through the maps and skip the query tiles of other
+    sequences' pads."""
     import copy
     from recommendations_amd.data import synthetic_lthm_batch
     from recommendations_amd.models.lthm.sequence import query_tower as qt
-    cfg, m = _model(dev, T=48, d=128, L=2, H=2, n_cat=0, gradient_checkpointing=ckpt)
+    cfg, m = _model(dev, T=T, d=128, L=2, H=2, n_cat=0, gradient_checkpointing=ckpt)
     m.train()
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
     ref_m = copy.deepcopy(m)
-    batch = synthetic_lthm_batch(96, 48, n_cat=0, seed=31, device=dev, min_len=1)
+    batch = synthetic_lthm_batch(96, T, n_cat=0, seed=31, device=dev, min_len=1)
     batch["product_ids"][5, :] = 0                                    # a fully padded history
     batch["product_ids"][7, 30:] = 0
     prefix = {}
