@@ -1148,6 +1148,139 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 tiles for K-contiguous A and B at K >= 512 (the MFMA-bound forms: the ranker MLPs,
+// the C5 encoder's K = 512 / 2,048 GEMMs, the K = 1,024 dgrad of C2's MLP).  8 waves as
+// 2 (M) x 4 (N), each wave a 128 x 64 block of C = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16
+// (128 accumulator registers).  K-tiles of 64 ride two LDS buffers of four 16-KiB halves
+// (A rows 0-127 / 128-255, B rows 0-127 / 128-255), each half 16 LDS-DMA pieces of 8 rows
+// x 128 B, the 16-B chunk c of row r at slot c ^ ((r >> 1) & 7): conflict-free for the
+// 16-row ds_read_b128 fragment reads.  One barrier per K-tile: behind it every wave issues the
+// next K-tile's DMA into the other buffer (read by all waves before they reached the barrier)
+// and computes this K-tile in four quadrant phases (64 x 32 of the wave's block, 16 MFMAs
+// each; A and B fragments re-read per phase, B of quadrant columns 0 kept across phases 1 and
+// 4).  Epilogue: 16-row slices restaged through the drained buffers, the generic 8-wide epilogue.
+constexpr int PP_BK = 64;
+constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k bf16)
+
+
+__global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * PP_HALF];  // [buf][A0, A1, B0, B1]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nblk = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int64_t m0 = (int64_t)(lid / tiles_n) * 256, n0 = (int64_t)(lid % tiles_n) * 256;
+  const int nk = (int)(g.K / PP_BK);
+  const int wr = wave >> 2, wc = wave & 3;
+  // this lane's DMA rows: piece d = wave + 8 u of a half, row 8 d + lane / 8, slot lane % 8
+  const int prow0 = 8 * wave + (lane >> 3), slot = lane & 7;
+  auto issue = [&](int kt, int buf) {
+    const int64_t k = (int64_t)kt * PP_BK;
+#pragma unroll
+    for (int hf = 0; hf < 4; ++hf) {
+      const bool isA = hf < 2;
+      const bf16_t* P = isA ? g.A : g.B;
+      const int64_t ld = isA ? g.lda : g.ldb, rows = isA ? g.M : g.N;
+      const int64_t r0 = (isA ? m0 : n0) + 128 * (hf & 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row = prow0 + 64 * u;
+        const int c = slot ^ ((row >> 1) & 7);
+        const int64_t gr = r0 + row;
+        const void* src = gr < rows ? (const void*)(P + gr * ld + k + c * 8) : (const void*)gemm_zero16;
+        glds16(src, sh + (buf * 4 + hf) * PP_HALF + (wave + 8 * u) * 1024);
+      }
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  retire_loads();
+  issue(0, 0);
+  const int r16 = lane & 15, c4 = lane >> 4;
+  // lane-constant fragment offsets: rows 16 i + r16 share the swizzle of r16
+  const int fa = r16 * 128, sw = (r16 >> 1) & 7;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const unsigned char* Ah = sh + (buf * 4 + wr) * PP_HALF;
+    const unsigned char* Bh = sh + (buf * 4 + 2 + (wc >> 1)) * PP_HALF + (wc & 1) * 64 * 128;
+    bf16x8v b0[2][2], b1[2][2];  // [j within the quadrant][k-step]
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int mi = ph >> 1;            // quadrant rows 64 mi ..
+      const int nj = (ph == 1 || ph == 2) ? 1 : 0;  // columns 32 nj .. (order 0, 1, 1, 0)
+      bf16x8v af[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          af[i][s2] = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(
+                                                      Ah + (64 * mi + 16 * i) * 128 + fa + (((4 * s2 + c4) ^ sw) << 4)));
+      if (ph == 0 || ph == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8v v = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4*>(
+                                                    Bh + (32 * nj + 16 * j) * 128 + fa + (((4 * s2 + c4) ^ sw) << 4)));
+            if (ph == 0) b0[j][s2] = v;
+            else b1[j][s2] = v;
+          }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * mi + i][2 * nj + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                af[i][s2], nj ? b1[j][s2] : b0[j][s2], acc[4 * mi + i][2 * nj + j], 0, 0, 0);
+    }
+  }
+  // epilogue: the buffers are free once every wave's last fragment reads are done
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // each wave's 128 x 64 block in two 64-row halves through its 16-KiB slice of the buffers
+  // (column groups of 16 XOR-rotated by row / 4: conflict-free stores), then a row loop with the
+  // generic epilogue (one copy of its code: the accumulator indices stay static)
+  float* stg = reinterpret_cast<float*>(sh) + wave * 64 * 64;
+  const int cq = (lane & 7) * 8;  // this lane's 8 columns of the wave's 64
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * c4 + r, col = 16 * j + r16;
+          stg[row * 64 + (col ^ (((row >> 2) & 3) << 4))] = acc[4 * hb + i][j][r];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    for (int lr = lane >> 3; lr < 64; lr += 8) {
+      const int64_t row = m0 + wr * 128 + hb * 64 + lr;
+      const int64_t col0 = n0 + wc * 64 + cq;
+      const float* sp = stg + lr * 64 + (cq ^ (((lr >> 2) & 3) << 4));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(sp);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(sp + 4);
+      float v[8] = {lo.x * g.alpha, lo.y * g.alpha, lo.z * g.alpha, lo.w * g.alpha,
+                    hi.x * g.alpha, hi.y * g.alpha, hi.z * g.alpha, hi.w * g.alpha};
+      if (row < g.M && col0 < g.N) epilogue8(g, v, row, col0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
 }  // namespace lthm
 
 using namespace lthm;
@@ -1181,6 +1314,16 @@ static int lthm_gemm_bt_mode() {
   if (mode < 0) {
     const char* e = getenv("LTHM_GEMM_BT");
     mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  return mode;
+}
+
+// 256 x 256 kernel (gemm_pp_k) for K-contiguous operands at K >= 512: LTHM_GEMM_PP=0 turns it off
+static int lthm_gemm_pp_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("LTHM_GEMM_PP");
+    mode = e ? atoi(e) : 1;
   }
   return mode;
 }
@@ -1314,6 +1457,18 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
 #undef LTHM_PS8
     LTHM_CHECK_LAUNCH();
     return 0;
+  }
+  if (lthm_gemm_pp_mode() && d->ab_dtype != LTHM_FP8_E4M3 && ka && kb && splits == 1 && d->batch == 1 &&
+      g.fast_ok && d->K >= 512 && d->K % PP_BK == 0 && d->M >= 256 && d->N >= 256) {
+    // (K = 256 forms stay on the persistent kernel: the C2 qkv / proj / fc forwards ran 5-26 %
+    // slower here, profiles/r04z_gemm_*; from K = 512 on this kernel wins: C4 fc1 forward 0.456 ->
+    // 0.349 ms, its dgrad 0.701 -> 0.376, C5 fc2 forward 1.456 -> 1.133, 4096^3 767 -> 1,179 TF)
+    const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
+    GemmArgs gp = g;
+    gp.ws = nullptr;
+    hipLaunchKernelGGL(gemm_pp_k, dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
+    LTHM_CHECK_LAUNCH();
+    return amax_after();
   }
   if (lthm_gemm_bt_mode() && d->ab_dtype != LTHM_FP8_E4M3 && ka && kb && splits == 1 && d->batch == 1 &&
       g.fast_ok && d->K > 4 * BK &&

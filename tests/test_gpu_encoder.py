@@ -112,6 +112,30 @@ def test_gemm_large_nt(dev, M, N, Kd, act):
         assert (pre.float().cpu() - z).abs().max() < 0.05
 
 
+@pytest.mark.parametrize("M,N,Kd,act,res2", [(777, 600, 512, 2, False), (4099, 1100, 2176, 1, True),
+                                              (65536, 1024, 2176, 0, False), (300, 2176, 1024, 5, False)])
+def test_gemm_256_tiles(dev, M, N, Kd, act, res2):
+    """The 256 x 256 kernel (K-contiguous operands, K >= 512): ragged row and column tiles,
+    bias, the activations with their saved aux, one or two residuals, f32 and bf16 outputs."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + 3 * N + Kd)
+    A = bf(torch.randn(M, Kd, generator=g))
+    W = bf(torch.randn(N, Kd, generator=g) / math.sqrt(Kd))
+    bias = torch.randn(N, generator=g)
+    r1 = torch.randn(M, N, generator=g)
+    r2 = torch.randn(M, N, generator=g) if res2 else None
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    out = K.linear_fwd(A.to(dev), W.to(dev), bias=bias.to(dev), act=act, aux_out=pre if act else None,
+                       res1=r1.to(dev), res2=r2.to(dev) if res2 else None, out_dtype=torch.float32)
+    z = A.float() @ W.float().T + bias
+    exp = {0: z, 1: F.gelu(z, approximate="tanh"), 2: ref.quick_gelu(z), 5: F.gelu(z, approximate="tanh")}[act] + r1
+    if res2:
+        exp = exp + r2
+    check("256-tile out", relerr(out, exp), 1e-5)
+    outb = K.linear_fwd(A.to(dev), W.to(dev))
+    check("256-tile bf16 out", relerr(outb.float(), bf(A.float() @ W.float().T).float()), 1e-3)
+
+
 @pytest.mark.parametrize("M,N,Kd", [(70001, 768, 256), (30000, 256, 1024)])
 def test_gemm_large_dgrad(dev, M, N, Kd):
     """dX = dY W (K-strided B) at step size, with the GELU-grad epilogue."""
