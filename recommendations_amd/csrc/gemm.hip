@@ -1164,6 +1164,15 @@ constexpr int PP_BK = 64;
 constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k bf16)
 
 
+// F8: A and B are e4m3 bytes with K and the leading dims in 2-byte units (a K-tile row is 128 k
+// of fp8): one v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per fragment pair and
+// K-tile, lane group c4 taking chunks 2 c4 and 2 c4 + 1 of the row; the per-tensor scales fold
+// into alpha.
+// SPREAD: the next K-tile's four half images are issued one per quadrant phase (2 DMAs each)
+// instead of all eight DMAs behind the barrier
+// PRIO: each phase's MFMAs at raised wave priority (s_setprio), so the partner wave's fragment
+// reads and DMA issue fill the MFMA gaps instead of delaying the chain
+template <bool F8, bool SPREAD = false, bool PRIO = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * PP_HALF];  // [buf][A0, A1, B0, B1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1174,23 +1183,24 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
   const int wr = wave >> 2, wc = wave & 3;
   // this lane's DMA rows: piece d = wave + 8 u of a half, row 8 d + lane / 8, slot lane % 8
   const int prow0 = 8 * wave + (lane >> 3), slot = lane & 7;
-  auto issue = [&](int kt, int buf) {
+  auto issue_half = [&](int kt, int buf, int hf) {
     const int64_t k = (int64_t)kt * PP_BK;
+    const bool isA = hf < 2;
+    const bf16_t* P = isA ? g.A : g.B;
+    const int64_t ld = isA ? g.lda : g.ldb, rows = isA ? g.M : g.N;
+    const int64_t r0 = (isA ? m0 : n0) + 128 * (hf & 1);
 #pragma unroll
-    for (int hf = 0; hf < 4; ++hf) {
-      const bool isA = hf < 2;
-      const bf16_t* P = isA ? g.A : g.B;
-      const int64_t ld = isA ? g.lda : g.ldb, rows = isA ? g.M : g.N;
-      const int64_t r0 = (isA ? m0 : n0) + 128 * (hf & 1);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int row = prow0 + 64 * u;
-        const int c = slot ^ ((row >> 1) & 7);
-        const int64_t gr = r0 + row;
-        const void* src = gr < rows ? (const void*)(P + gr * ld + k + c * 8) : (const void*)gemm_zero16;
-        glds16(src, sh + (buf * 4 + hf) * PP_HALF + (wave + 8 * u) * 1024);
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int row = prow0 + 64 * u;
+      const int c = slot ^ ((row >> 1) & 7);
+      const int64_t gr = r0 + row;
+      const void* src = gr < rows ? (const void*)(P + gr * ld + k + c * 8) : (const void*)gemm_zero16;
+      glds16(src, sh + (buf * 4 + hf) * PP_HALF + (wave + 8 * u) * 1024);
     }
+  };
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int hf = 0; hf < 4; ++hf) issue_half(kt, buf, hf);
   };
   f32x4 acc[8][4];
 #pragma unroll
@@ -1208,12 +1218,51 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const bool more = kt + 1 < nk;
+    if (!SPREAD && more) issue(kt + 1, buf ^ 1);
     const unsigned char* Ah = sh + (buf * 4 + wr) * PP_HALF;
     const unsigned char* Bh = sh + (buf * 4 + 2 + (wc >> 1)) * PP_HALF + (wc & 1) * 64 * 128;
+    if constexpr (F8) {
+      i32x8v b0[2], b1[2];  // [j within the quadrant]
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        if (SPREAD && more) issue_half(kt + 1, buf ^ 1, ph);
+        const int mi = ph >> 1;
+        const int nj = (ph == 1 || ph == 2) ? 1 : 0;
+        i32x8v af[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned char* ra = Ah + (64 * mi + 16 * i) * 128 + fa;
+          const u32x4 lo = *reinterpret_cast<const u32x4*>(ra + (((2 * c4) ^ sw) << 4));
+          const u32x4 hi = *reinterpret_cast<const u32x4*>(ra + (((2 * c4 + 1) ^ sw) << 4));
+          af[i] = i32x8v{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        }
+        if (ph == 0 || ph == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const unsigned char* rb = Bh + (32 * nj + 16 * j) * 128 + fa;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(rb + (((2 * c4) ^ sw) << 4));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(rb + (((2 * c4 + 1) ^ sw) << 4));
+            const i32x8v v = {(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            if (ph == 0) b0[j] = v;
+            else b1[j] = v;
+          }
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * mi + i][2 * nj + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                af[i], nj ? b1[j] : b0[j], acc[4 * mi + i][2 * nj + j], 0, 0, 0, 127, 0, 127);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+      }
+      continue;
+    }
     bf16x8v b0[2][2], b1[2][2];  // [j within the quadrant][k-step]
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
+      if (SPREAD && more) issue_half(kt + 1, buf ^ 1, ph);
       const int mi = ph >> 1;            // quadrant rows 64 mi ..
       const int nj = (ph == 1 || ph == 2) ? 1 : 0;  // columns 32 nj .. (order 0, 1, 1, 0)
       bf16x8v af[4][2];
@@ -1234,6 +1283,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
             else b1[j][s2] = v;
           }
       }
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1242,6 +1292,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
           for (int j = 0; j < 2; ++j)
             acc[4 * mi + i][2 * nj + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 af[i][s2], nj ? b1[j][s2] : b0[j][s2], acc[4 * mi + i][2 * nj + j], 0, 0, 0);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   // epilogue: the buffers are free once every wave's last fragment reads are done
@@ -1253,6 +1304,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
   // generic epilogue (one copy of its code: the accumulator indices stay static)
   float* stg = reinterpret_cast<float*>(sh) + wave * 64 * 64;
   const int cq = (lane & 7) * 8;  // this lane's 8 columns of the wave's 64
+  const float alpha = F8 ? g.alpha * *g.sa * *g.sb : g.alpha;
 #pragma unroll
   for (int hb = 0; hb < 2; ++hb) {
 #pragma unroll
@@ -1272,8 +1324,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
       const float* sp = stg + lr * 64 + (cq ^ (((lr >> 2) & 3) << 4));
       const f32x4 lo = *reinterpret_cast<const f32x4*>(sp);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(sp + 4);
-      float v[8] = {lo.x * g.alpha, lo.y * g.alpha, lo.z * g.alpha, lo.w * g.alpha,
-                    hi.x * g.alpha, hi.y * g.alpha, hi.z * g.alpha, hi.w * g.alpha};
+      float v[8] = {lo.x * alpha, lo.y * alpha, lo.z * alpha, lo.w * alpha,
+                    hi.x * alpha, hi.y * alpha, hi.z * alpha, hi.w * alpha};
       if (row < g.M && col0 < g.N) epilogue8(g, v, row, col0, 0, 0);
     }
     __builtin_amdgcn_wave_barrier();
@@ -1318,12 +1370,23 @@ static int lthm_gemm_bt_mode() {
   return mode;
 }
 
-// 256 x 256 kernel (gemm_pp_k) for K-contiguous operands at K >= 512: LTHM_GEMM_PP=0 turns it off
+// 256 x 256 kernel (gemm_pp_k) for K-contiguous operands at K >= 512: LTHM_GEMM_PP=0 turns it off;
+// A/B: 2 the per-phase DMA issue, 3 the MFMA priority raise, 4 both
 static int lthm_gemm_pp_mode() {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("LTHM_GEMM_PP");
     mode = e ? atoi(e) : 1;
+  }
+  return mode;
+}
+
+// the fp8 form of gemm_pp_k: LTHM_GEMM_PP_F8=1 (off until measured against the persistent kernel)
+static int lthm_gemm_pp_f8() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("LTHM_GEMM_PP_F8");
+    mode = (e && e[0] == '1') ? 1 : 0;
   }
   return mode;
 }
@@ -1429,6 +1492,21 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     GemmArgs g8 = g;
     g8.K = d->K / 2; g8.lda = d->lda / 2; g8.ldb = d->ldb / 2;
     g8.sa = d->a_scale; g8.sb = d->b_scale;
+    if (lthm_gemm_pp_mode() && lthm_gemm_pp_f8() && d->K >= 512 && d->K % (2 * PP_BK) == 0 && d->M >= 256 &&
+        d->N >= 256 && !d->amax_out) {
+      // 256 x 256 tiles (the bf16 kernel's geometry in 2-byte units)
+      const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
+      g8.ws = nullptr;
+      g8.amax = nullptr;
+      switch (lthm_gemm_pp_mode()) {
+        case 2: hipLaunchKernelGGL((gemm_pp_k<true, true, false>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
+        case 3: hipLaunchKernelGGL((gemm_pp_k<true, false, true>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
+        case 4: hipLaunchKernelGGL((gemm_pp_k<true, true, true>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
+        default: hipLaunchKernelGGL((gemm_pp_k<true, false, false>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn);
+      }
+      LTHM_CHECK_LAUNCH();
+      return 0;
+    }
     if (lthm_gemm_bt_mode() && d->K > 256 && d->K % 128 == 0 && d->M >= 4096 && d->N >= 512 && !d->amax_out) {
       // 256 x 256 tiles (the persistent kernel's 128 x 128 tile re-reads the LDS per flop at K >= 512)
       const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
@@ -1466,7 +1544,12 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     GemmArgs gp = g;
     gp.ws = nullptr;
-    hipLaunchKernelGGL(gemm_pp_k, dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
+    switch (lthm_gemm_pp_mode()) {
+      case 2: hipLaunchKernelGGL((gemm_pp_k<false, true, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
+      case 3: hipLaunchKernelGGL((gemm_pp_k<false, false, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
+      case 4: hipLaunchKernelGGL((gemm_pp_k<false, true, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
+      default: hipLaunchKernelGGL((gemm_pp_k<false, false, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
+    }
     LTHM_CHECK_LAUNCH();
     return amax_after();
   }

@@ -49,12 +49,18 @@ def main():
         t3t = timeit(lambda: K.linear_fwd(dy, wt))
         t4 = timeit(lambda: K.linear_wgrad(dy, a), iters=5)
         t5 = timeit(lambda: torch.matmul(dy.T, a), iters=5)
+        t8 = float("nan")
+        if os.environ.get("GEMM_BENCH_FP8") and k % 128 == 0:
+            xq, xs = K.quantize_fp8(a)
+            wq, ws = K.quantize_fp8(w)
+            t8 = timeit(lambda: K.linear_fwd_fp8(xq, xs, wq, ws))
         byts = 2.0 * (m * k + n * k + m * n)  # bf16 A + W + C, each once
         print(f"{name:7s} M={m} N={n} K={k}: fwd {t0:.3f} ms ({fl / t0 / 1e9:.0f} TF, "
               f"{byts / t0 / 1e6:.0f} GB/s)  +gelu {t1:.3f}  "
               f"hipblaslt {t2:.3f} ({fl / t2 / 1e9:.0f} TF) | dgrad {t3:.3f} ({fl / t3 / 1e9:.0f} TF) "
               f"via W^T {t3t:.3f} ({fl / t3t / 1e9:.0f} TF) | "
-              f"wgrad {t4:.3f} ({fl / t4 / 1e9:.0f} TF) hipblaslt {t5:.3f}", flush=True)
+              f"wgrad {t4:.3f} ({fl / t4 / 1e9:.0f} TF) hipblaslt {t5:.3f} | fp8 fwd {t8:.3f} ({fl / t8 / 1e9:.0f} TF)",
+              flush=True)
 
 
 if __name__ == "__main__":
