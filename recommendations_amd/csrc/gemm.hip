@@ -995,6 +995,85 @@ __global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int
       }
 }
 
+// The same product in 64-k stages: two LDS buffers of four [64 k][128 cols] sub-images (16 KiB,
+// 256-B k-rows, the T10(b) swizzle), one barrier per stage behind which every wave issues the
+// next stage's DMA into the other buffer (its last readers passed that barrier) and runs 64
+// MFMAs (two k-steps of the 4 x 8 fragment grid) -- the gemm_pp_k schedule on K-strided
+// operands (BK 32 -> 64 halves the barriers per MFMA).  Rows of the k-range past K read a zero
+// chunk, so any K works (the packed rows of a shared pad prefix have no alignment).
+constexpr int WG2_BK = 64;
+constexpr int WG2_SUB = 64 * 256;  // one [64 k][128 cols] sub-image (16 KiB)
+
+__global__ __launch_bounds__(512, 1) void gemm_wg2_k(GemmArgs g, int tiles_m, int tiles_n, int splits, int64_t kps) {
+  __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * WG2_SUB];  // [buf][A0, A1, B0, B1]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nblk = tiles_m * tiles_n * splits;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int split = lid / (tiles_m * tiles_n), tile = lid - split * (tiles_m * tiles_n);
+  const int64_t m0 = (int64_t)(tile / tiles_n) * 256, n0 = (int64_t)(tile % tiles_n) * 256;
+  const int64_t kb = (int64_t)split * kps, ke = min(g.K, kb + kps);
+  const int S = ke > kb ? (int)((ke - kb + WG2_BK - 1) / WG2_BK) : 0;
+  // stage st: 64 pieces (1 KiB = 4 k-rows x 256 B of one sub-image); wave w issues w + 8 u
+  auto issue = [&](int st, int buf) {
+    const int64_t k = kb + (int64_t)st * WG2_BK;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int piece = wave + 8 * u;
+      const int sub = piece >> 4, d = piece & 15;
+      const bool isA = sub < 2;
+      const bf16_t* P = isA ? g.A : g.B;
+      const int64_t ld = isA ? g.lda : g.ldb, cols = isA ? g.M : g.N;
+      const int64_t c0 = (isA ? m0 : n0) + (sub & 1) * 128;
+      const int kr = 4 * d + (lane >> 4);
+      const int ch = (lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+      const int64_t gc = c0 + ch * 8;
+      const void* src = (gc < cols && k + kr < ke) ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
+      glds16(src, sh + (buf * 4 + sub) * WG2_SUB + d * 1024);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;  // rows wm*64.., cols wn*128..
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  retire_loads();
+  if (S > 0) issue(0, 0);
+  for (int st = 0; st < S; ++st) {
+    const int buf = st & 1;
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + 1 < S) issue(st + 1, buf ^ 1);
+    const unsigned char* sa = sh + (buf * 4 + (wm >> 1)) * WG2_SUB;  // A rows wm*64: sub-image wm/2, cols (wm&1)*64
+    const unsigned char* sb = sh + (buf * 4 + 2 + wn) * WG2_SUB;      // B cols wn*128..: sub-image 2 + wn
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8v af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<false>(sa, (wm & 1) * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bf16x8v bfr = read_frag<false>(sb, j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  float* ws = g.ws + (int64_t)split * g.M * g.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t col = n0 + wn * 128 + j * 16 + (lane & 15);
+        if (row < g.M && col < g.N) ws[row * g.N + col] = g.alpha * acc[i][j][r];
+      }
+}
+
 // ---------------------------------------------------------------- 256 x 256 forward / dgrad GEMM
 // Both operands K-contiguous (Y = X W^T, dX = dY W^T on a W^T copy) at K > 256, where the
 // persistent kernel's resident B slab no longer fits and its 128 x 128 tile re-reads the
@@ -1381,6 +1460,16 @@ static int lthm_gemm_pp_mode() {
   return mode;
 }
 
+// the 64-k-stage weight-gradient kernel (gemm_wg2_k): LTHM_GEMM_WG2=1 (off until measured)
+static int lthm_gemm_wg2_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("LTHM_GEMM_WG2");
+    mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  return mode;
+}
+
 // the fp8 form of gemm_pp_k: LTHM_GEMM_PP_F8=1 (off until measured against the persistent kernel)
 static int lthm_gemm_pp_f8() {
   static int mode = -1;
@@ -1439,20 +1528,23 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
   hipStream_t s = (hipStream_t)stream;
   // weight gradients: 256 x 256 split-K tiles (splits bounded by the caller's workspace)
-  if (lthm_gemm_ps_mode() && !ka && !kb && d->batch == 1 && d->workspace && d->K % WG_BK == 0 && g.fast_ok &&
-      d->M % 8 == 0 && d->N % 8 == 0 && d->act == LTHM_ACT_NONE && !d->bias && d->M * d->N > 0) {
+  const bool wg2 = lthm_gemm_wg2_mode() != 0;
+  if (lthm_gemm_ps_mode() && !ka && !kb && d->batch == 1 && d->workspace && (wg2 || d->K % WG_BK == 0) &&
+      g.fast_ok && d->M % 8 == 0 && d->N % 8 == 0 && d->act == LTHM_ACT_NONE && !d->bias && d->M * d->N > 0) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     const int64_t cap = (int64_t)(d->workspace_bytes / ((size_t)d->M * d->N * 4));
+    const int bk = wg2 ? WG2_BK : WG_BK;
     int64_t sp = std::min<int64_t>(std::max(1, lthm_cu_count() / (tm * tn)), cap);
-    sp = std::min<int64_t>(sp, d->K / (WG_BK * 8));  // >= 8 stages per split
+    sp = std::min<int64_t>(sp, d->K / (bk * (wg2 ? 4 : 8)));  // >= 8 32-k (4 64-k) stages per split
     if (sp >= 2 && tm * tn <= lthm_cu_count()) {
       int64_t kpw = (d->K + sp - 1) / sp;
-      kpw = (kpw + WG_BK - 1) / WG_BK * WG_BK;
+      kpw = (kpw + bk - 1) / bk * bk;
       const int spl = (int)((d->K + kpw - 1) / kpw);
       GemmArgs gw = g;
       gw.ws = d->workspace;
       gw.res1 = nullptr; gw.res2 = nullptr;
-      hipLaunchKernelGGL(gemm_wg_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
+      if (wg2) hipLaunchKernelGGL(gemm_wg2_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
+      else hipLaunchKernelGGL(gemm_wg_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
       LTHM_CHECK_LAUNCH();
       GemmArgs gr = g;
       gr.ws = d->workspace;

@@ -78,6 +78,18 @@ def test_gemm_dgrad_wgrad(dev, M, N, Kd):
     check('dw, dy.float().T @ X.float()', relerr(dw, dy.float().T @ X.float()), 1e-5)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(263001, 512, 1536), (70003, 768, 256), (4100, 2048, 512)])
+def test_gemm_wgrad_ragged_rows(dev, M, N, Kd):
+    """dW = dY^T X with a row count of no alignment (the packed rows of a shared pad prefix):
+    the split-K weight-gradient kernel zero-fills the k rows past the end."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + N)
+    dy = bf(torch.randn(M, N, generator=g))
+    X = bf(torch.randn(M, Kd, generator=g))
+    dw = K.linear_wgrad(dy.to(dev), X.to(dev))
+    check("ragged-row wgrad", relerr(dw, dy.double().T @ X.double()), 1e-5)
+
+
 def test_gemm_wgrad_splitk_large(dev):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(3)
