@@ -914,8 +914,9 @@ __global__ __launch_bounds__(PS_THREADS, 1) void gemm_ps_k(GemmArgs g, int tiles
 // the operands is fetched from HBM once and re-read from that XCD's L2.  Each
 // workgroup writes its raw f32 partial tile to the split-K slab; splitk_reduce_k
 // applies alpha's epilogue (accumulate / output dtype).
-// Requires: A and B K-strided, batch 1, K % 32 == 0, 16-B aligned operands and
-// leading dims % 8 == 0.
+// Requires: A and B K-strided, batch 1, 16-B aligned operands and leading dims % 8 == 0; any
+// K (k rows past the end read a zero chunk).  A 64-k-stage, two-buffer form of this kernel
+// (the gemm_pp_k schedule) measured 5-10 % slower on every wgrad shape (profiles/r04ac/).
 constexpr int WG_NST = 4;
 constexpr int WG_BK = 32;
 constexpr int WG_SUB = 32 * 256;  // one [32 k][128 cols] sub-image (8 KiB)
@@ -931,7 +932,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int
   const int split = lid / (tiles_m * tiles_n), tile = lid - split * (tiles_m * tiles_n);
   const int64_t m0 = (int64_t)(tile / tiles_n) * 256, n0 = (int64_t)(tile % tiles_n) * 256;
   const int64_t kb = (int64_t)split * kps, ke = min(g.K, kb + kps);
-  const int S = ke > kb ? (int)((ke - kb) / WG_BK) : 0;
+  const int S = ke > kb ? (int)((ke - kb + WG_BK - 1) / WG_BK) : 0;
   // stage s: pieces 0..31 (1 KiB each, 4 k-rows x 256 B of one sub-image); wave w issues w, w+8, w+16, w+24
   auto issue = [&](int st) {
     const int64_t k = kb + (int64_t)st * WG_BK;
@@ -947,7 +948,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int
       const int kr = 4 * d + (lane >> 4);
       const int ch = (lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
       const int64_t gc = c0 + ch * 8;
-      const void* src = gc < cols ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
+      const void* src = (gc < cols && k + kr < ke) ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
       glds16(src, base + sub * WG_SUB + d * 1024);
     }
   };
@@ -982,85 +983,6 @@ __global__ __launch_bounds__(512, 1) void gemm_wg_k(GemmArgs g, int tiles_m, int
     }
   }
   // raw alpha * partial tile -> split-K slab [split][M][N] (16 lanes = 64 contiguous bytes)
-  float* ws = g.ws + (int64_t)split * g.M * g.N;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        const int64_t col = n0 + wn * 128 + j * 16 + (lane & 15);
-        if (row < g.M && col < g.N) ws[row * g.N + col] = g.alpha * acc[i][j][r];
-      }
-}
-
-// The same product in 64-k stages: two LDS buffers of four [64 k][128 cols] sub-images (16 KiB,
-// 256-B k-rows, the T10(b) swizzle), one barrier per stage behind which every wave issues the
-// next stage's DMA into the other buffer (its last readers passed that barrier) and runs 64
-// MFMAs (two k-steps of the 4 x 8 fragment grid) -- the gemm_pp_k schedule on K-strided
-// operands (BK 32 -> 64 halves the barriers per MFMA).  Rows of the k-range past K read a zero
-// chunk, so any K works (the packed rows of a shared pad prefix have no alignment).
-constexpr int WG2_BK = 64;
-constexpr int WG2_SUB = 64 * 256;  // one [64 k][128 cols] sub-image (16 KiB)
-
-__global__ __launch_bounds__(512, 1) void gemm_wg2_k(GemmArgs g, int tiles_m, int tiles_n, int splits, int64_t kps) {
-  __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * WG2_SUB];  // [buf][A0, A1, B0, B1]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nblk = tiles_m * tiles_n * splits;
-  const int lid = xcd_remap(blockIdx.x, nblk);
-  const int split = lid / (tiles_m * tiles_n), tile = lid - split * (tiles_m * tiles_n);
-  const int64_t m0 = (int64_t)(tile / tiles_n) * 256, n0 = (int64_t)(tile % tiles_n) * 256;
-  const int64_t kb = (int64_t)split * kps, ke = min(g.K, kb + kps);
-  const int S = ke > kb ? (int)((ke - kb + WG2_BK - 1) / WG2_BK) : 0;
-  // stage st: 64 pieces (1 KiB = 4 k-rows x 256 B of one sub-image); wave w issues w + 8 u
-  auto issue = [&](int st, int buf) {
-    const int64_t k = kb + (int64_t)st * WG2_BK;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int piece = wave + 8 * u;
-      const int sub = piece >> 4, d = piece & 15;
-      const bool isA = sub < 2;
-      const bf16_t* P = isA ? g.A : g.B;
-      const int64_t ld = isA ? g.lda : g.ldb, cols = isA ? g.M : g.N;
-      const int64_t c0 = (isA ? m0 : n0) + (sub & 1) * 128;
-      const int kr = 4 * d + (lane >> 4);
-      const int ch = (lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
-      const int64_t gc = c0 + ch * 8;
-      const void* src = (gc < cols && k + kr < ke) ? (const void*)(P + (k + kr) * ld + gc) : (const void*)gemm_zero16;
-      glds16(src, sh + (buf * 4 + sub) * WG2_SUB + d * 1024);
-    }
-  };
-  const int wm = wave >> 1, wn = wave & 1;  // rows wm*64.., cols wn*128..
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  retire_loads();
-  if (S > 0) issue(0, 0);
-  for (int st = 0; st < S; ++st) {
-    const int buf = st & 1;
-    wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (st + 1 < S) issue(st + 1, buf ^ 1);
-    const unsigned char* sa = sh + (buf * 4 + (wm >> 1)) * WG2_SUB;  // A rows wm*64: sub-image wm/2, cols (wm&1)*64
-    const unsigned char* sb = sh + (buf * 4 + 2 + wn) * WG2_SUB;      // B cols wn*128..: sub-image 2 + wn
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8v af[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<false>(sa, (wm & 1) * 64 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bf16x8v bfr = read_frag<false>(sb, j * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
-      }
-    }
-  }
   float* ws = g.ws + (int64_t)split * g.M * g.N;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1248,10 +1170,9 @@ constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k 
 // K-tile, lane group c4 taking chunks 2 c4 and 2 c4 + 1 of the row; the per-tensor scales fold
 // into alpha.
 // SPREAD: the next K-tile's four half images are issued one per quadrant phase (2 DMAs each)
-// instead of all eight DMAs behind the barrier
-// PRIO: each phase's MFMAs at raised wave priority (s_setprio), so the partner wave's fragment
-// reads and DMA issue fill the MFMA gaps instead of delaying the chain
-template <bool F8, bool SPREAD = false, bool PRIO = false>
+// instead of all eight DMAs behind the barrier (bf16: C4 forms 4-6 % faster; the fp8 form ran
+// 3x slower so, and raising the MFMA phases' wave priority lost 5-7 %, profiles/r04ab/)
+template <bool F8, bool SPREAD = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * PP_HALF];  // [buf][A0, A1, B0, B1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1327,14 +1248,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
             else b1[j] = v;
           }
         }
-        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[4 * mi + i][2 * nj + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
                 af[i], nj ? b1[j] : b0[j], acc[4 * mi + i][2 * nj + j], 0, 0, 0, 127, 0, 127);
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
       }
       continue;
     }
@@ -1362,7 +1281,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
             else b1[j][s2] = v;
           }
       }
-      if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1371,7 +1289,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
           for (int j = 0; j < 2; ++j)
             acc[4 * mi + i][2 * nj + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 af[i][s2], nj ? b1[j][s2] : b0[j][s2], acc[4 * mi + i][2 * nj + j], 0, 0, 0);
-      if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   // epilogue: the buffers are free once every wave's last fragment reads are done
@@ -1449,8 +1366,8 @@ static int lthm_gemm_bt_mode() {
   return mode;
 }
 
-// 256 x 256 kernel (gemm_pp_k) for K-contiguous operands at K >= 512: LTHM_GEMM_PP=0 turns it off;
-// A/B: 2 the per-phase DMA issue, 3 the MFMA priority raise, 4 both
+// 256 x 256 kernel (gemm_pp_k) for K-contiguous operands at K >= 512: LTHM_GEMM_PP=0 turns it off,
+// 2 issues the next K-tile's DMA all behind the barrier instead of per phase (A/B)
 static int lthm_gemm_pp_mode() {
   static int mode = -1;
   if (mode < 0) {
@@ -1460,22 +1377,12 @@ static int lthm_gemm_pp_mode() {
   return mode;
 }
 
-// the 64-k-stage weight-gradient kernel (gemm_wg2_k): LTHM_GEMM_WG2=1 (off until measured)
-static int lthm_gemm_wg2_mode() {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("LTHM_GEMM_WG2");
-    mode = (e && e[0] == '1') ? 1 : 0;
-  }
-  return mode;
-}
-
-// the fp8 form of gemm_pp_k: LTHM_GEMM_PP_F8=1 (off until measured against the persistent kernel)
+// the fp8 form of gemm_pp_k (K >= 1,024): LTHM_GEMM_PP_F8=0 turns it off
 static int lthm_gemm_pp_f8() {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("LTHM_GEMM_PP_F8");
-    mode = (e && e[0] == '1') ? 1 : 0;
+    mode = (e && e[0] == '0') ? 0 : 1;
   }
   return mode;
 }
@@ -1528,23 +1435,22 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
   const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
   hipStream_t s = (hipStream_t)stream;
   // weight gradients: 256 x 256 split-K tiles (splits bounded by the caller's workspace)
-  const bool wg2 = lthm_gemm_wg2_mode() != 0;
-  if (lthm_gemm_ps_mode() && !ka && !kb && d->batch == 1 && d->workspace && (wg2 || d->K % WG_BK == 0) &&
-      g.fast_ok && d->M % 8 == 0 && d->N % 8 == 0 && d->act == LTHM_ACT_NONE && !d->bias && d->M * d->N > 0) {
+  // (any K: the packed rows of a shared pad prefix have no alignment; k rows past K read zeros)
+  static const bool wg_ragged = !(getenv("LTHM_WG_RAGGED") && getenv("LTHM_WG_RAGGED")[0] == '0');  // A/B
+  if (lthm_gemm_ps_mode() && !ka && !kb && d->batch == 1 && d->workspace && g.fast_ok && d->M % 8 == 0 &&
+      d->N % 8 == 0 && d->act == LTHM_ACT_NONE && !d->bias && d->M * d->N > 0 && (wg_ragged || d->K % WG_BK == 0)) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     const int64_t cap = (int64_t)(d->workspace_bytes / ((size_t)d->M * d->N * 4));
-    const int bk = wg2 ? WG2_BK : WG_BK;
     int64_t sp = std::min<int64_t>(std::max(1, lthm_cu_count() / (tm * tn)), cap);
-    sp = std::min<int64_t>(sp, d->K / (bk * (wg2 ? 4 : 8)));  // >= 8 32-k (4 64-k) stages per split
+    sp = std::min<int64_t>(sp, d->K / (WG_BK * 8));  // >= 8 stages per split
     if (sp >= 2 && tm * tn <= lthm_cu_count()) {
       int64_t kpw = (d->K + sp - 1) / sp;
-      kpw = (kpw + bk - 1) / bk * bk;
+      kpw = (kpw + WG_BK - 1) / WG_BK * WG_BK;
       const int spl = (int)((d->K + kpw - 1) / kpw);
       GemmArgs gw = g;
       gw.ws = d->workspace;
       gw.res1 = nullptr; gw.res2 = nullptr;
-      if (wg2) hipLaunchKernelGGL(gemm_wg2_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
-      else hipLaunchKernelGGL(gemm_wg_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
+      hipLaunchKernelGGL(gemm_wg_k, dim3(tm * tn * spl), dim3(512), 0, s, gw, tm, tn, spl, kpw);
       LTHM_CHECK_LAUNCH();
       GemmArgs gr = g;
       gr.ws = d->workspace;
@@ -1584,18 +1490,15 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     GemmArgs g8 = g;
     g8.K = d->K / 2; g8.lda = d->lda / 2; g8.ldb = d->ldb / 2;
     g8.sa = d->a_scale; g8.sb = d->b_scale;
-    if (lthm_gemm_pp_mode() && lthm_gemm_pp_f8() && d->K >= 512 && d->K % (2 * PP_BK) == 0 && d->M >= 256 &&
+    if (lthm_gemm_pp_mode() && lthm_gemm_pp_f8() && d->K >= 1024 && d->K % (2 * PP_BK) == 0 && d->M >= 256 &&
         d->N >= 256 && !d->amax_out) {
-      // 256 x 256 tiles (the bf16 kernel's geometry in 2-byte units)
+      // 256 x 256 tiles (the bf16 kernel's geometry in 2-byte units).  From K = 1,024 on (8 K-tiles):
+      // C5 fc2 (K = 2,048) 0.767 -> 0.660 ms, 4096^3 0.091 -> 0.065 ms (2.1 PF); the K = 512 forms
+      // ran 17-24 % slower here than on the persistent kernel (profiles/r04ab/)
       const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
       g8.ws = nullptr;
       g8.amax = nullptr;
-      switch (lthm_gemm_pp_mode()) {
-        case 2: hipLaunchKernelGGL((gemm_pp_k<true, true, false>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
-        case 3: hipLaunchKernelGGL((gemm_pp_k<true, false, true>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
-        case 4: hipLaunchKernelGGL((gemm_pp_k<true, true, true>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn); break;
-        default: hipLaunchKernelGGL((gemm_pp_k<true, false, false>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn);
-      }
+      hipLaunchKernelGGL((gemm_pp_k<true, false>), dim3(tm * tn), dim3(512), 0, s, g8, tm, tn);
       LTHM_CHECK_LAUNCH();
       return 0;
     }
@@ -1636,12 +1539,8 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     GemmArgs gp = g;
     gp.ws = nullptr;
-    switch (lthm_gemm_pp_mode()) {
-      case 2: hipLaunchKernelGGL((gemm_pp_k<false, true, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
-      case 3: hipLaunchKernelGGL((gemm_pp_k<false, false, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
-      case 4: hipLaunchKernelGGL((gemm_pp_k<false, true, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn); break;
-      default: hipLaunchKernelGGL((gemm_pp_k<false, false, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
-    }
+    if (lthm_gemm_pp_mode() == 2) hipLaunchKernelGGL((gemm_pp_k<false, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
+    else hipLaunchKernelGGL((gemm_pp_k<false, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
     LTHM_CHECK_LAUNCH();
     return amax_after();
   }
