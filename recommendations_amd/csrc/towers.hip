@@ -900,7 +900,7 @@ __global__ __launch_bounds__(512) void cve_tab_bwd_k(const uint16_t* __restrict_
 // ------------------------------------------------------------------ token assembly
 // x0[b, 0]   = wpe[T] (+ ctx[b])
 // x0[b, t+1] = (mask ? pad : P[b,t] + act[lab] + hod[.] + how[.] + dow[.]) + wpe[T-1-t]
-template <typename TP>
+template <typename TP, bool VEC>
 __global__ __launch_bounds__(256) void tokens_fwd_k(lthm_tokens_desc d) {
   // A wave takes 64 rows at a time: lane l first derives the table indices of row r0 + l
   // (the label / timestamp loads and the 64-bit floor-div / mod chains of all 64 rows in
@@ -946,10 +946,12 @@ __global__ __launch_bounds__(256) void tokens_fwd_k(lthm_tokens_desc d) {
       }
     }
     const int nr = (int)min((int64_t)64, rows - r0);
-    if (D == 256) {
-      // 4 rows per step, every load of the 4 rows issued before the first store
+    if (VEC) {  // D == 256
+      // 4 rows per step, every load of the 4 rows issued before the first store; lane l owns
+      // columns 4 l .. 4 l + 3 (16-B table / x0 accesses, 8-B bf16 P accesses)
+      const int c = 4 * lane;
       for (int k0 = 0; k0 < nr; k0 += 4) {
-        float v[4][4];
+        f32x4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int k = min(k0 + u, nr - 1);
@@ -957,27 +959,30 @@ __global__ __launch_bounds__(256) void tokens_fwd_k(lthm_tokens_desc d) {
           const int a0 = __shfl(ia, k, 64), a1 = __shfl(ih, k, 64), a2 = __shfl(iw, k, 64), a3 = __shfl(idw, k, 64);
           const int64_t bk = (int64_t)__shfl((int)b, k, 64);
           const int64_t sk = ((int64_t)__shfl((int)(src >> 32), k, 64) << 32) | (uint32_t)__shfl((int)src, k, 64);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int c = lane + 64 * q;
-            float x;
-            if (kk == 0) {
-              x = d.ctx ? d.ctx[bk * 256 + c] : 0.f;
-            } else if (kk == 1) {
-              x = d.pad[c];
+          f32x4 x;
+          if (kk == 0) {
+            x = d.ctx ? *reinterpret_cast<const f32x4*>(d.ctx + bk * 256 + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+          } else if (kk == 1) {
+            x = *reinterpret_cast<const f32x4*>(d.pad + c);
+          } else {
+            if constexpr (sizeof(TP) == 2) {
+              const u32x2 w = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(d.P) + sk * 256 + c);
+              x = f32x4{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u),
+                        __uint_as_float(w[1] << 16), __uint_as_float(w[1] & 0xffff0000u)};
             } else {
-              x = Elem<TP>::ld(reinterpret_cast<const TP*>(d.P) + sk * 256 + c);
-              x = x + d.act[a0 * 256 + c] + d.hod[a1 * 256 + c] + d.how[a2 * 256 + c] + d.dow[a3 * 256 + c];
+              x = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(d.P) + sk * 256 + c);
             }
-            v[u][q] = x + d.wpe[(int64_t)wr * 256 + c];
+            // the same left-to-right sum as the scalar path: P + act + hod + how + dow
+            x = x + *reinterpret_cast<const f32x4*>(d.act + a0 * 256 + c);
+            x = x + *reinterpret_cast<const f32x4*>(d.hod + a1 * 256 + c);
+            x = x + *reinterpret_cast<const f32x4*>(d.how + a2 * 256 + c);
+            x = x + *reinterpret_cast<const f32x4*>(d.dow + a3 * 256 + c);
           }
+          v[u] = x + *reinterpret_cast<const f32x4*>(d.wpe + (int64_t)wr * 256 + c);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (k0 + u < nr) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) d.x0[(r0 + k0 + u) * 256 + lane + 64 * q] = v[u][q];
-          }
+          if (k0 + u < nr) *reinterpret_cast<f32x4*>(d.x0 + (r0 + k0 + u) * 256 + c) = v[u];
       }
       continue;
     }
@@ -1019,7 +1024,14 @@ __global__ __launch_bounds__(256) void tokens_bwd_k(lthm_tokens_desc d, const fl
       continue;
     }
     const bool masked = d.mask[b * d.T_full + d.trim + tp - 1] != 0;
-    for (int c = lane; c < D; c += 64) dP[(b * T + tp - 1) * D + c] = f2bf(masked ? 0.f : dx0[r * D + c]);
+    if ((D & 3) == 0 && (((uintptr_t)dx0 | (uintptr_t)dP) & 15) == 0) {  // uniform: 16-B reads, 8-B writes
+      for (int c = 4 * lane; c < D; c += 256) {
+        const f32x4 v = masked ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(dx0 + r * D + c);
+        *reinterpret_cast<u32x2*>(dP + (b * T + tp - 1) * D + c) = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+      }
+    } else {
+      for (int c = lane; c < D; c += 64) dP[(b * T + tp - 1) * D + c] = f2bf(masked ? 0.f : dx0[r * D + c]);
+    }
   }
 }
 
@@ -1035,7 +1047,14 @@ __global__ __launch_bounds__(256) void outcome_fwd_k(const float* __restrict__ x
     const int tp = (int)(r - b * Tp);
     const int64_t lab = (tp < T) ? labels[b * T_full + trim + tp] : future;
     const int64_t o = pymod64(lab, noc);
-    for (int c = lane; c < D; c += 64) out[r * D + c] = f2bf(x[r * D + c] + oc[o * D + c]);
+    if ((D & 3) == 0 && (((uintptr_t)x | (uintptr_t)oc | (uintptr_t)out) & 15) == 0) {  // uniform
+      for (int c = 4 * lane; c < D; c += 256) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * D + c) + *reinterpret_cast<const f32x4*>(oc + o * D + c);
+        *reinterpret_cast<u32x2*>(out + r * D + c) = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+      }
+    } else {
+      for (int c = lane; c < D; c += 64) out[r * D + c] = f2bf(x[r * D + c] + oc[o * D + c]);
+    }
     if (lane == 0 && rows) rows[r] = (uint16_t)o;
   }
 }
@@ -1355,10 +1374,18 @@ extern "C" int lthm_tokens_fwd(const lthm_tokens_desc* d, void* stream) {
   if (d->B == 0) return 0;
   const int64_t rows = d->B * (d->T_full - d->trim + 1);
   hipStream_t s = (hipStream_t)stream;
-  if (d->p_dtype == LTHM_BF16)
-    hipLaunchKernelGGL((tokens_fwd_k<bf16_t>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
-  else
-    hipLaunchKernelGGL((tokens_fwd_k<float>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
+  // the D = 256 path reads 16-B table chunks: every operand base 16-B aligned (rows are 1 KiB)
+  bool vec = d->d == 256;
+  for (const void* q : {(const void*)d->act, (const void*)d->hod, (const void*)d->how, (const void*)d->dow,
+                        (const void*)d->wpe, (const void*)d->pad, (const void*)d->ctx, (const void*)d->x0, d->P})
+    vec = vec && ((uintptr_t)q % 16) == 0;
+  if (d->p_dtype == LTHM_BF16) {
+    if (vec) hipLaunchKernelGGL((tokens_fwd_k<bf16_t, true>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
+    else hipLaunchKernelGGL((tokens_fwd_k<bf16_t, false>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
+  } else {
+    if (vec) hipLaunchKernelGGL((tokens_fwd_k<float, true>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
+    else hipLaunchKernelGGL((tokens_fwd_k<float, false>), dim3(grid_for(rows, 256, 256 * 8)), dim3(256), 0, s, *d);
+  }
   LTHM_CHECK_LAUNCH();
   return 0;
 }
