@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 36 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 37 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -231,6 +231,12 @@ int lthm_layernorm_bwd_blocks(int64_t M);
 int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D,
                        const float* w, const float* mean, const float* rstd, const float* res1,
                        const float* res2, float* dx, void* dx_bf16, float* partials, void* stream);
+/* flags bit 0 (D % 4 == 0): dx (f32) = LN'(dy) + 2 res1 + res2 while dx_bf16 = LN'(dy) + res1 + res2:
+ * the double-residual block's ln_2 backward hands ln_1's backward its two residual gradients
+ * as one f32 tensor (query_tower.py:135, x + block(x)) */
+int lthm_layernorm_bwd_ex(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D,
+                          const float* w, const float* mean, const float* rstd, const float* res1,
+                          const float* res2, float* dx, void* dx_bf16, float* partials, int32_t flags, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Attention with relative position bias + causal mask                       */

@@ -219,7 +219,12 @@ class TransformerBlockFn(torch.autograd.Function):
             dw1 = K.linear_wgrad(dpre, h2)
             db1 = K.colsum(dpre) if has_b1 else None
             dh2 = K.linear_dgrad(dpre, w1_b)
-        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b)
+        # double residual, no residual dropout, no c_proj bias: ln_1's backward needs dx1 + dy only
+        # (dx = LN1'(dh1) + dx1 + dy), so ln_2's backward writes that sum as its f32 output (the
+        # bf16 copy, the attention branch's input, stays dx1): one f32 read less per element
+        fold = dbl and pr == 0.0 and not has_bp and d % 4 == 0
+        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b,
+                                                  res1_twice=fold)
         # attention half (dx1r: the gradient behind the residual dropout)
         if pr > 0.0:
             dx1r = K.dropout(dx1, pr, seed + 1)
@@ -245,7 +250,7 @@ class TransformerBlockFn(torch.autograd.Function):
         dbqkv = K.colsum(dqkv) if has_bqkv else None
         dh1 = K.linear_dgrad(dqkv, wqkv_b)
         dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1, need_bias=has_ln1b,
-                                                res2=dy if dbl else None)
+                                                res2=dy if dbl and not fold else None)
         _stash_grad_bf16(dx, dxb)
         dtable = None
         if tshape is not None:

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v4_k(const TDY* __restrict__ dy, c
                                                    const float* __restrict__ rstd, const float* __restrict__ res1,
                                                    const float* __restrict__ res2, float* __restrict__ dx,
                                                    bf16_t* __restrict__ dx_bf16, float* __restrict__ dw_part,
-                                                   float* __restrict__ db_part) {
+                                                   float* __restrict__ db_part, int res1_twice) {
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
   const int64_t wave = blockIdx.x * 4 + wv_;
@@ -250,8 +250,12 @@ __global__ __launch_bounds__(256) void ln_bwd_v4_k(const TDY* __restrict__ dy, c
         if (res2) ld4(res2 + r * D + c, r2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = rs * (g[k][i] - s1 - xh[k][i] * s2) + r1[i] + r2[i];
-        store_vec<float, 4>(dx + r * D + c, o);
         if (dx_bf16) store_vec<bf16_t, 4>(dx_bf16 + r * D + c, o);
+        if (res1_twice) {  // the f32 output carries res1 once more (the next LayerNorm's two residuals)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] += r1[i];
+        }
+        store_vec<float, 4>(dx + r * D + c, o);
       }
     }
   }
@@ -358,10 +362,11 @@ extern "C" int lthm_layernorm_fwd_amax(const float* x, int64_t M, int32_t D, con
 
 extern "C" int lthm_layernorm_bwd_blocks(int64_t M) { return grid_for(M, 4, 256 * 4); }
 
-extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D, const float* w,
-                                  const float* mean, const float* rstd, const float* res1, const float* res2, float* dx,
-                                  void* dx_bf16, float* partials, void* stream) {
+static int ln_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D, const float* w,
+                  const float* mean, const float* rstd, const float* res1, const float* res2, float* dx,
+                  void* dx_bf16, float* partials, int res1_twice, void* stream) {
   LTHM_REQUIRE(M >= 0 && D > 0 && D <= 1024 && w != nullptr && partials != nullptr);
+  LTHM_REQUIRE(!res1_twice || (res1 != nullptr && D % 4 == 0));
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = grid_for(M, 4, 256 * 4);
@@ -373,10 +378,10 @@ extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float*
     if (D <= 256 * NK) {                                                                                       \
       if (dy_dtype == LTHM_BF16)                                                                               \
         hipLaunchKernelGGL((ln_bwd_v4_k<NK, bf16_t>), dim3(nblk), dim3(256), 0, s, (const bf16_t*)dy, x, M, D, w, \
-                           mean, rstd, res1, res2, dx, xb, dwp, dbp);                                          \
+                           mean, rstd, res1, res2, dx, xb, dwp, dbp, res1_twice);                              \
       else                                                                                                     \
         hipLaunchKernelGGL((ln_bwd_v4_k<NK, float>), dim3(nblk), dim3(256), 0, s, (const float*)dy, x, M, D, w,  \
-                           mean, rstd, res1, res2, dx, xb, dwp, dbp);                                          \
+                           mean, rstd, res1, res2, dx, xb, dwp, dbp, res1_twice);                              \
       LTHM_CHECK_LAUNCH();                                                                                     \
       return 0;                                                                                                \
     }
@@ -391,4 +396,18 @@ extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float*
   if (npl <= 4) return ln_bwd_launch<4>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
   if (npl <= 8) return ln_bwd_launch<8>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
   return ln_bwd_launch<16>(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, xb, partials, nblk, s);
+}
+
+extern "C" int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D, const float* w,
+                                  const float* mean, const float* rstd, const float* res1, const float* res2, float* dx,
+                                  void* dx_bf16, float* partials, void* stream) {
+  return ln_bwd(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, dx_bf16, partials, 0, stream);
+}
+
+extern "C" int lthm_layernorm_bwd_ex(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D,
+                                     const float* w, const float* mean, const float* rstd, const float* res1,
+                                     const float* res2, float* dx, void* dx_bf16, float* partials, int32_t flags,
+                                     void* stream) {
+  LTHM_REQUIRE((flags & ~1) == 0);
+  return ln_bwd(dy, dy_dtype, x, M, D, w, mean, rstd, res1, res2, dx, dx_bf16, partials, flags & 1, stream);
 }

@@ -630,7 +630,9 @@ def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True):
+def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True, res1_twice=False):
+    """dx = LN'(dy) + res1 + res2 (f32) and its bf16 copy.  res1_twice: the f32 dx carries res1
+    once more than the bf16 copy (lthm_layernorm_bwd_ex flag 1)."""
     from ._lib import load
     M, D = x2d.shape
     for t, nm in ((dy2d, "dy"), (res1, "res1"), (res2, "res2")):
@@ -646,8 +648,13 @@ def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True
     # statistics read, the per-block weight-gradient partials written
     nb = float(M * D * (dy2d.element_size() + x2d.element_size() + 4 + (4 if res1 is not None else 0)
                         + (4 if res2 is not None else 0) + (2 if want_bf16 else 0)) + 8 * M + part.numel() * 4)
-    call("lthm_layernorm_bwd", ptr(dy2d), dcode(dy2d), ptr(x2d), M, D, ptr(w), ptr(mean), ptr(rstd), ptr(res1),
-         ptr(res2), ptr(dx), ptr(dxb), ptr(part), stream(), _work=nb, _unit="byte")
+    if res1_twice:
+        _check(res1 is not None and D % 4 == 0, "layernorm_bwd(res1_twice): res1 and D % 4 == 0")
+        call("lthm_layernorm_bwd_ex", ptr(dy2d), dcode(dy2d), ptr(x2d), M, D, ptr(w), ptr(mean), ptr(rstd), ptr(res1),
+             ptr(res2), ptr(dx), ptr(dxb), ptr(part), 1, stream(), _key="lthm_layernorm_bwd", _work=nb, _unit="byte")
+    else:
+        call("lthm_layernorm_bwd", ptr(dy2d), dcode(dy2d), ptr(x2d), M, D, ptr(w), ptr(mean), ptr(rstd), ptr(res1),
+             ptr(res2), ptr(dx), ptr(dxb), ptr(part), stream(), _work=nb, _unit="byte")
     dw = colsum(part[0])
     db = colsum(part[1]) if need_bias else None
     return dx, dxb, dw, db
