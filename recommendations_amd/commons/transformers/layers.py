@@ -72,6 +72,8 @@ _MLP_TRAIN = os.environ.get("LTHM_MLP_TRAIN", "1") == "1"
 # ln_2 inside the fused MLP kernel (LTHM_MLP_LN=1); default: the LayerNorm kernel, then the MLP
 # kernel (C2: 81,718 vs 81,523 samples/s, mlp_fwd 0.90 + ln 0.17 vs 1.10 ms, profiles/r04d_*)
 _MLP_LN = os.environ.get("LTHM_MLP_LN", "0") == "1"
+# ln_2's backward writes dx1 + dy as its f32 output for ln_1's backward (LTHM_LN_FOLD=0: separately)
+_LN_FOLD = os.environ.get("LTHM_LN_FOLD", "0") == "1"
 
 
 class TransformerBlockFn(torch.autograd.Function):
@@ -222,7 +224,7 @@ class TransformerBlockFn(torch.autograd.Function):
         # double residual, no residual dropout, no c_proj bias: ln_1's backward needs dx1 + dy only
         # (dx = LN1'(dh1) + dx1 + dy), so ln_2's backward writes that sum as its f32 output (the
         # bf16 copy, the attention branch's input, stays dx1): one f32 read less per element
-        fold = dbl and pr == 0.0 and not has_bp and d % 4 == 0
+        fold = _LN_FOLD and dbl and pr == 0.0 and not has_bp and d % 4 == 0
         dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b,
                                                   res1_twice=fold)
         # attention half (dx1r: the gradient behind the residual dropout)
