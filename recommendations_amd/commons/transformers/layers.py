@@ -73,7 +73,7 @@ _MLP_TRAIN = os.environ.get("LTHM_MLP_TRAIN", "1") == "1"
 # kernel (C2: 81,718 vs 81,523 samples/s, mlp_fwd 0.90 + ln 0.17 vs 1.10 ms, profiles/r04d_*)
 _MLP_LN = os.environ.get("LTHM_MLP_LN", "0") == "1"
 # ln_2's backward writes dx1 + dy as its f32 output for ln_1's backward (LTHM_LN_FOLD=0: separately)
-_LN_FOLD = os.environ.get("LTHM_LN_FOLD", "0") == "1"
+_LN_FOLD = os.environ.get("LTHM_LN_FOLD", "1") == "1"
 
 
 class TransformerBlockFn(torch.autograd.Function):
