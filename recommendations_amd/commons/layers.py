@@ -424,10 +424,16 @@ class MLP(nn.Module):
         return self._forward_eager(x)
 
     @torch.jit.unused
-    def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
+    def _forward_eager(self, x: torch.Tensor, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
         lins = [m for m in self.model if isinstance(m, nn.Linear)]
         acts = [K.ACT_QGELU] * (len(lins) - 1) + [K.ACT_NONE]
-        return K.mlp_chain(x, lins, acts, out_f32=True)
+        return K.mlp_chain(x, lins, acts, out_f32=True, x2=x2)
+
+    @torch.jit.unused
+    def forward_concat(self, x: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+        """forward(torch.cat([x, x2.reshape(len(x), -1)], 1)) with the concatenation built in bf16
+        (the first GEMM's operand dtype); x's gradient stays in x's dtype."""
+        return self._forward_eager(x, x2)
 
 
 class PatternFromTimelocal(nn.Module):

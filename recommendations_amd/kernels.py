@@ -994,11 +994,19 @@ class MLPChainFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, acts, out_f32, *wb):
+    def forward(ctx, x, x2, acts, out_f32, *wb):
+        """x2 (optional, [.., K2]): concatenated after x's features as the first GEMM's operand
+        (the ranker's [dense | categorical] input, built once in bf16, the GEMM operand dtype,
+        instead of as an f32 concatenation the GEMM would cast again)."""
         require_gpu(x)
         shp = x.shape
         h = x.contiguous().view(-1, shp[-1])
         h = h if h.dtype == torch.bfloat16 else cast(h, torch.bfloat16)
+        ctx.k1 = None
+        if x2 is not None:
+            ctx.k1 = h.shape[1]
+            h = torch.cat([h, x2.reshape(h.shape[0], -1).to(torch.bfloat16)], dim=1)
+            shp = tuple(shp[:-1]) + (h.shape[1],)
         n = len(wb) // 2
         ws = [cast(wb[2 * i].detach().contiguous(), torch.bfloat16) for i in range(n)]
         hs, pres = [h], []
@@ -1043,14 +1051,17 @@ class MLPChainFn(torch.autograd.Function):
                 gb = linear_dgrad(gb, ws[i], act_grad=ag, aux=pres[i - 1])
             else:
                 dx = linear_dgrad(gb, ws[0], out_dtype=torch.float32 if xdt == torch.float32 else torch.bfloat16)
-        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, *grads)
+        if ctx.k1 is not None:  # the two inputs' parts of dx (x2's cast to its dtype by autograd)
+            k1 = ctx.k1
+            return (dx[:, :k1].reshape(*shp[:-1], k1), dx[:, k1:], None, None, *grads)
+        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, None, *grads)
 
 
-def mlp_chain(x, linears, acts, out_f32=True):
+def mlp_chain(x, linears, acts, out_f32=True, x2=None):
     wb = []
     for lin in linears:
         wb += [lin.weight, lin.bias]
-    return MLPChainFn.apply(x, tuple(acts), out_f32, *wb)
+    return MLPChainFn.apply(x, x2, tuple(acts), out_f32, *wb)
 
 
 class ActivationFn(torch.autograd.Function):

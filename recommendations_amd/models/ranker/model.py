@@ -37,8 +37,9 @@ class RankerModel(nn.Module):
         B = dense.shape[0]
         e_dense = self.dense_mapper.forward_matrix(dense)              # [B, emb_dim] f32
         e_cat = self.cat_tables(cat.contiguous())                      # [B, F, D] bf16
-        x = torch.cat([e_dense, e_cat.reshape(B, -1).float()], dim=1)  # [B, emb_dim + F*D]
-        return {"logits": self.interaction(x)}
+        # the MLP input [e_dense | e_cat] ([B, emb_dim + F*D]) is assembled in bf16 inside the MLP
+        # op: the same values the first GEMM reads from an f32 concatenation, without it
+        return {"logits": self.interaction.forward_concat(e_dense, e_cat.reshape(B, -1))}
 
 
 class RankerModelWrapper(BaseModelWrapper):
