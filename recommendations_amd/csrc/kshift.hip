@@ -422,6 +422,59 @@ static int launch_item_artifact(const int64_t* ids, int64_t n, const void* W, in
   return 0;
 }
 
+// K = 1 (flat lookups: FlatEmbedding, the C4 ranker's table-batched tables): one row per item,
+// so a lane group takes KS1_U consecutive items at once -- their ids, rows and row loads all in
+// flight before the first store (the general kernel holds one row load per lane between two
+// barriers).  Same per-item arithmetic (the row, /1 or L2-normalised), no LDS.
+constexpr int KS1_U = 8;
+template <typename TW, typename TO, int VB>
+__global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k1_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
+                                                          const TW* __restrict__ W, int64_t P, int D, int mode,
+                                                          TO* __restrict__ out, float* __restrict__ norms,
+                                                          int LPR_LOG2) {
+  constexpr int NE = VB / (int)sizeof(TW);
+  const int LPR = 1 << LPR_LOG2;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (LPR - 1);
+  const int64_t groups = (int64_t)gridDim.x * (KS_BLOCK >> LPR_LOG2);
+  const int64_t group = (int64_t)blockIdx.x * (KS_BLOCK >> LPR_LOG2) + (threadIdx.x >> LPR_LOG2);
+  for (int64_t base = group * KS1_U; base < n_items; base += groups * KS1_U) {
+    int64_t rows[KS1_U];
+#pragma unroll
+    for (int u = 0; u < KS1_U; ++u) {
+      const int64_t item = base + u;
+      rows[u] = item < n_items ? ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], 0, P) : -1;
+    }
+    float v[KS1_U][NE];
+#pragma unroll
+    for (int u = 0; u < KS1_U; ++u) {
+      if (rows[u] >= 0) load_vec<TW, VB>(W + rows[u] * D + (size_t)gl * NE, v[u]);
+      else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[u][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KS1_U; ++u) {
+      if (mode == LTHM_KSHIFT_NORMALIZE) {
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) ss += v[u][e] * v[u][e];
+        for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        const float nrm = sqrtf(ss);
+        const float den = fmaxf(nrm, 1e-12f);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[u][e] = v[u][e] / den;
+        if (rows[u] >= 0 && norms != nullptr && gl == 0) norms[base + u] = nrm;
+      } else if (mode == LTHM_KSHIFT_SCALE) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[u][e] = v[u][e] / 1.f;
+      }
+      if (rows[u] >= 0) store_vec<TO, NE>(out + (base + u) * D + (size_t)gl * NE, v[u]);
+    }
+  }
+}
+
 template <typename TW, typename TO>
 static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W, int64_t P, int D, int K,
                       int mode, void* out, float* norms, hipStream_t s, const int64_t* xrows = nullptr) {
@@ -434,6 +487,23 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
   const int ipb = ipw * (KS_BLOCK / 64);
   const int grid = grid_for(n_items, ipb, 256 * 32);
   const float scale = (float)__builtin_sqrt((double)K);
+  static const bool k1_off = getenv("LTHM_KSHIFT_K1") && getenv("LTHM_KSHIFT_K1")[0] == '0';  // A/B
+  if (K == 1 && xrows == nullptr && !k1_off) {
+    const int g1 = grid_for(n_items, ipb * KS1_U, 256 * 32);
+    if (vb == 16)
+      hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 16>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
+                         P, D, mode, (TO*)out, norms, l2);
+    else if (vb == 8)
+      hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 8>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
+                         P, D, mode, (TO*)out, norms, l2);
+    else if (vb == 4)
+      hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 4>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
+                         P, D, mode, (TO*)out, norms, l2);
+    else
+      return (int)hipErrorInvalidValue;
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   if (vb == 16)
     hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 16>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
                        (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2, xrows);
