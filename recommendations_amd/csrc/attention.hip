@@ -1268,7 +1268,10 @@ __host__ __device__ __forceinline__ int bwd32_slack(int T, int Tu) {
 }
 __host__ __device__ __forceinline__ int bwd32_slack(int T) { return bwd32_slack(T, T); }
 
-constexpr int BWD32_NW = 4, BWD32_WPE = 2;  // waves per (b, h); waves per SIMD the registers allow
+#ifndef LTHM_BWD32_NW
+#define LTHM_BWD32_NW 4  // A/B builds: tools/build_variant.sh ... -DLTHM_BWD32_NW=8
+#endif
+constexpr int BWD32_NW = LTHM_BWD32_NW, BWD32_WPE = 2;  // waves per (b, h); waves per SIMD the registers allow
 
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_WPE, BWD32_WPE))) void attn_bwd32_k(AttnArgs a) {
