@@ -1539,7 +1539,11 @@ extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {
     const int tm = (int)((d->M + 255) / 256), tn = (int)((d->N + 255) / 256);
     GemmArgs gp = g;
     gp.ws = nullptr;
-    if (lthm_gemm_pp_mode() == 2) hipLaunchKernelGGL((gemm_pp_k<false, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
+    // per-phase DMA issue where there are several column tiles (C4: 4-6 % faster); a single
+    // 256-column tile (C2's N = 256 dgrads) runs ~2 % faster with the DMA behind the barrier
+    // (profiles/r04am_ab.log)
+    if (lthm_gemm_pp_mode() == 2 || d->N <= 256)
+      hipLaunchKernelGGL((gemm_pp_k<false, false>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
     else hipLaunchKernelGGL((gemm_pp_k<false, true>), dim3(tm * tn), dim3(512), 0, s, gp, tm, tn);
     LTHM_CHECK_LAUNCH();
     return amax_after();
