@@ -49,17 +49,26 @@ PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call 
     "gemm_k<0,0>": ["gemm_k<false, false>", "gemm_wg_k", "splitk_reduce_k"],
     "cve_tab_bwd_k": ["cve_tab_bwd_k<", "seg_tab_reduce_k"],
     "lthm_product_tower_fwd": ["ptower_"],
+    # the fused MLP calls (tagged enc:mlp_*): each is ONE kernel of one shape
+    "mlp_fwd": ["mlp_fwd_k<"],
+    "mlp_bwd": ["mlp_bwdp_k<", "mlp_bwd_k<", "mlp_bwdx_k<"],
+    "mlp_wgrad": ["mlp_wgrad_k<"],
 }
 PMC_STEPS = 3  # tools/pmc_passes.sh profiles `bench.py --steps 2 --warmup 1 --no-kernel-timing`
 # Timer keys that are NOT one kernel: C-ABI calls that launch several kernels (the loss calls:
 # their main passes are timed alone as cl_fr32_k / cl_bwd32_k) and GEMM keys that pool several
-# shapes / templates ("enc:" tags, untagged gemm_k forms).  The roofline object prices the
-# single kernel with the largest share of the step, the rocprof-dominant kernel.
+# shapes / templates ("enc:" GEMM tags, untagged gemm_k forms).  The roofline object prices the
+# single kernel with the largest share of the step, the rocprof-dominant kernel.  The fused MLP
+# keys (enc:mlp_fwd / enc:mlp_bwd / enc:mlp_wgrad) ARE single kernels of a single shape per step
+# (one launch per layer, every layer the same M x d x 4d), so they compete.
 MULTI_KERNEL_KEYS = {"cl_fwd_k", "cl_bwd_k", "lthm_product_tower_fwd", "cve_tab_bwd_k", "attn_bwd_k"}
+SINGLE_KERNEL_TAGGED = ("mlp_fwd", "mlp_bwd", "mlp_wgrad")
 
 
 def single_kernel_key(k: str) -> bool:
-    return not (k in MULTI_KERNEL_KEYS or k.startswith("enc:") or k.startswith("gemm_k<") or k == "gemm_fp8")
+    if k.startswith("enc:"):
+        return k.split(":")[-1] in SINGLE_KERNEL_TAGGED
+    return not (k in MULTI_KERNEL_KEYS or k.startswith("gemm_k<") or k == "gemm_fp8")
 PROF_STEPS = 2  # untimed per-kernel profiling steps between warm-up and the timed region
 
 
@@ -554,6 +563,12 @@ def main():
         else:
             peak = pk_mfma
             ach, unit, bound = per_launch / avg_s / 1e12, "TFLOP/s", "mfma"
+        both = {}
+        if s["unit"] != "byte" and s.get("bytes") and s["work"]:
+            # a kernel that declares flops AND compulsory bytes: both fractions, the binding one in `frac`
+            both = {"mfma_frac": round(per_launch / avg_s / 1e12 / pk_mfma, 4),
+                    "hbm_frac": round(s["bytes"] / s["calls"] / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "flop_per_launch": per_launch, "bytes_per_launch": s["bytes"] / s["calls"]}
         if ":" in dom and prof is not None:
             # a tagged GEMM form (enc:...): the counters see the kernel, not the tag, so the
             # traffic is the form's average over all its launches (tagged or not)
@@ -569,7 +584,7 @@ def main():
                            "traffic": round(traffic) if traffic is not None else None,
                            "traffic_unit": "bytes/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic is not None else None,
-                           "avg_launch_ms": round(s["ms"] / s["calls"], 4)}
+                           "avg_launch_ms": round(s["ms"] / s["calls"], 4), **both}
         if "kshift_fwd_k" in summ:
             g = summ["kshift_fwd_k"]
             res["embedding_gather_c2"] = {"kernel": "kshift_fwd_k", "bound": "hbm",

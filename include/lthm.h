@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 37 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 38 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -307,6 +307,10 @@ int lthm_attn_fwd(const lthm_attn_desc* desc, void* stream);
  * delta: f32 [B, H, T] workspace, required when T > 256. */
 int lthm_attn_bwd(const lthm_attn_desc* desc, void* stream);
 int64_t lthm_attn_bwd_parts(int32_t B, int32_t T);
+/* 1 when lthm_attn_fwd / lthm_attn_bwd take PACKED rows (row_map set) at this T and E with no
+ * mask: the long-T' 32x32x16 kernels serve it (T > 256, E = 64, both LDS images fit, not
+ * switched off by the A/B environment switches); 0: the caller unpacks to full sequences. */
+int lthm_attn_packed_ok(int32_t T, int32_t E);
 
 /* ------------------------------------------------------------------------- */
 /* LTHM towers (models/lthm/sequence/ encoder, product and query towers)     */
@@ -625,9 +629,10 @@ int64_t lthm_contrastive_vc_ws_bytes(int64_t B, int32_t T, int32_t n_heads, int3
 /* bytes of lthm_contrastive_desc.stats_ws for one forward launch (-1: invalid sizes) */
 int64_t lthm_contrastive_ws_bytes(int32_t n_mb, int32_t n_max, int32_t heads);
 
-/* Forward for one head (or heads_run consecutive heads) over all mini-batches.  stats [n_mb, nstat] f32 per head:
- * {mean CE, used rows, mean negatives, min negatives, mean rank, median rank,
- *  offset, hit@ks[0..nk)}; loss_scale multiplies the row weights (1 / n_mb).
+/* Forward for one head (or heads_run consecutive heads) over all mini-batches.  stats [n_mb, nstat] f32 per head
+ * (nstat >= 8 + nk): {mean CE over the used tokens, used rows (effective batch), mean negatives, min negatives,
+ *  mean rank, median rank, offset, used tokens, hit@ks[0..nk)}; a used row whose CE is NaN leaves the mean and
+ *  the used tokens (wrapper.py:210-214); loss_scale multiplies the row weights (1 / n_mb).
  * Training at the fixed shift (2 / tau <= 80, no logq) with y_raw / y_norm / dy given (heads 0 .. n_heads - 1,
  * mb_size <= 4096 sequences): one pass per row block computes the forward AND the row side of the backward,
  * writing dy for a unit upstream gradient; the backward is then called with rows_done = 1. */

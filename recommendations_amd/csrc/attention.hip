@@ -2173,6 +2173,16 @@ static int check_desc(const lthm_attn_desc* d) {
 
 extern "C" int64_t lthm_attn_bwd_parts(int32_t B, int32_t T) { return attn_parts(B, T); }
 
+// the packed-row dispatch's own test (attn_dispatch, a.rmap set), exported so that the caller
+// unpacks instead of failing where it does not hold
+extern "C" int lthm_attn_packed_ok(int32_t T, int32_t E) {
+  if (T <= 0 || T > 4096 || E != 64 || !attn_windowed(T)) return 0;
+  AttnArgs a{};
+  a.T = T;
+  a.delta = reinterpret_cast<float*>(16);  // bwd32l_ok asks only whether a delta workspace is given
+  return fwd32_ok(a) && bwd32l_ok(a) ? 1 : 0;
+}
+
 extern "C" int lthm_attn_fwd(const lthm_attn_desc* d, void* stream) {
   LTHM_REQUIRE(check_desc(d) == 0 && d->lse != nullptr && d->out != nullptr);
   if (d->B == 0) return 0;

@@ -412,16 +412,20 @@ __global__ __launch_bounds__(256) void cl_shift_k(ClArgs a0) {
 // Three launches, any n (the rank histogram and the per-row flags live in HBM, no
 // per-block limit on the rows of a mini-batch):
 //  cl_rowstats_k  (CL_SROWS rows per block): per row, used = not pad and >= 1 finite
-//                 negative (wrapper.py:193-201); block partial sums {CE, negatives, ranks,
-//                 used, min negatives} in fixed order (f64), used flag into w, one integer
-//                 atomic per used row into the rank histogram (order-free, deterministic);
+//                 negative (wrapper.py:193-201); a used row whose CE is NaN is dropped from
+//                 the mean and from used_tokens (wrapper.py:210-214) but stays in the
+//                 effective batch, the negatives and the ranks, as there; block partial sums
+//                 {CE, negatives, ranks, used, min negatives, used tokens} in fixed order
+//                 (f64), the used-token flag into w, one integer atomic per used row into the
+//                 rank histogram (order-free, deterministic);
 //  cl_stats_k     (one block per (mini-batch, head)): the partials in fixed order, hits@k as
 //                 prefix counts of the histogram, the median rank from its order statistics;
-//  cl_wscale_k    row weights w_r = used_r * loss_scale / U.
-// stats[mb][*] = {mean CE, used, mean negatives, min negatives, mean rank, median rank,
-//                 offset, hits@k...}
+//  cl_wscale_k    row weights w_r = token_r * loss_scale / U_tokens.
+// stats[mb][*] = {mean CE over the used tokens, used (effective batch), mean negatives, min
+//                 negatives, mean rank, median rank, offset, used tokens, hits@k...}
 constexpr int CL_SROWS = 2048;
-constexpr int CL_NPART = 5;  // f64 partials per (head, mb, block)
+constexpr int CL_NPART = 6;  // f64 partials per (head, mb, block)
+constexpr int CL_NSTAT = 8;  // stats before hits@k
 
 __device__ __forceinline__ double block_dsum(double v, double* red) {
   const int tid = threadIdx.x;
@@ -447,17 +451,22 @@ __global__ __launch_bounds__(256) void cl_rowstats_k(ClArgs a0, int* __restrict_
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)mb * a.n_max;
   float ls = 0.f, neg = 0.f, rks = 0.f;  // <= 8 rows per thread: integer sums stay exact
-  int used = 0, mneg = 0x7fffffff;
+  int used = 0, tok = 0, mneg = 0x7fffffff;
   for (int i = 0; i < CL_SROWS / 256; ++i) {
     const int r = blockIdx.x * CL_SROWS + tid + 256 * i;
     if (r >= a.n_max) break;
-    bool u = false;
+    bool u = false, t = false;
     if (r < g.n) {
       const int nn = a.cnt[base + r] - 1;
       u = !pad_of(a, g, r) && nn > 0;
       if (u) {
         const int rk = a.rank[base + r];
-        ls += a.lse[base + r] - a.pos[base + r];
+        const float ce = a.lse[base + r] - a.pos[base + r];
+        t = !__builtin_isnan(ce);  // wrapper.py:210-211: NaN CE rows leave the mean and used_tokens
+        if (t) {
+          ls += ce;
+          tok += 1;
+        }
         neg += (float)nn;
         rks += (float)rk;
         used += 1;
@@ -465,12 +474,12 @@ __global__ __launch_bounds__(256) void cl_rowstats_k(ClArgs a0, int* __restrict_
         atomicAdd(hist + rk, 1);
       }
     }
-    a.colb[base + r] = u ? 1.f : 0.f;  // used flag into w (colb = w in the forward); cl_wscale_k scales it
+    a.colb[base + r] = t ? 1.f : 0.f;  // used-token flag into w (colb = w in the forward); cl_wscale_k scales it
   }
   __shared__ double red[256];
   __shared__ int imn[256];
   const double Ls = block_dsum(ls, red), Ns = block_dsum(neg, red), Rs = block_dsum(rks, red);
-  const double U = block_dsum(used, red);
+  const double U = block_dsum(used, red), Ut = block_dsum(tok, red);
   imn[tid] = mneg;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -478,7 +487,7 @@ __global__ __launch_bounds__(256) void cl_rowstats_k(ClArgs a0, int* __restrict_
     __syncthreads();
   }
   if (tid == 0) {
-    part[0] = Ls; part[1] = Ns; part[2] = Rs; part[3] = U; part[4] = (double)imn[0];
+    part[0] = Ls; part[1] = Ns; part[2] = Rs; part[3] = U; part[4] = (double)imn[0]; part[5] = Ut;
   }
 }
 
@@ -496,15 +505,17 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, const int* __restri
   __shared__ double red[256];
   __shared__ int ired[256];
   __shared__ int sel[2];
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  double v[4] = {0.0, 0.0, 0.0, 0.0}, vt = 0.0;
   double mn = 2147483647.0;
   for (int b = tid; b < nblk; b += 256) {  // fixed order: thread tid folds blocks tid, tid + 256, ...
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] += part[b * CL_NPART + k];
     mn = fmin(mn, part[b * CL_NPART + 4]);
+    vt += part[b * CL_NPART + 5];
   }
   const double Ls = block_dsum(v[0], red), Ns = block_dsum(v[1], red), Rs = block_dsum(v[2], red);
   const int U = (int)block_dsum(v[3], red);
+  const int Ut = (int)block_dsum(vt, red);  // used tokens: the used rows with a finite CE
   ired[tid] = (int)mn;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -519,7 +530,7 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, const int* __restri
     int h = 0;
     for (int i = tid; i < kq && i < a.n_max; i += 256) h += hist[i];
     const int H = (int)block_dsum(h, red);
-    if (tid == 0) st[7 + q] = U > 0 ? (float)((double)H / U) : 0.f;
+    if (tid == 0) st[CL_NSTAT + q] = U > 0 ? (float)((double)H / U) : 0.f;
   }
   // median of the used ranks (torch.quantile(0.5): linear interpolation between the order
   // statistics p_lo and p_hi): each thread owns a contiguous run of bins, an exclusive scan of
@@ -553,7 +564,7 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, const int* __restri
   }
   __syncthreads();
   if (tid == 0) {
-    st[0] = U > 0 ? (float)(Ls / U) : 0.f;
+    st[0] = Ut > 0 ? (float)(Ls / Ut) : 0.f;  // wrapper.py:212-217: mean over the finite rows, 0 if none
     st[1] = (float)U;
     st[2] = U > 0 ? (float)(Ns / U) : 0.f;
     st[3] = (float)(U > 0 ? Mn : 0);
@@ -565,6 +576,7 @@ __global__ __launch_bounds__(256) void cl_stats_k(ClArgs a0, const int* __restri
     }
     st[5] = med;
     st[6] = (float)g.off;
+    st[7] = (float)Ut;
   }
 }
 
@@ -572,7 +584,7 @@ __global__ __launch_bounds__(256) void cl_wscale_k(ClArgs a0, const float* __res
                                                    float loss_scale) {
   const ClArgs a = head_args(a0, blockIdx.z);
   const int mb = blockIdx.y;
-  const float U = stats[((int64_t)blockIdx.z * a0.n_mb + mb) * nstat + 1];
+  const float U = stats[((int64_t)blockIdx.z * a0.n_mb + mb) * nstat + 7];  // used tokens
   const float wr = U > 0.f ? loss_scale / U : 0.f;
   float* w = a.colb + (int64_t)mb * a.n_max;  // = the row weights w in the forward
   for (int r = blockIdx.x * 256 + threadIdx.x; r < a.n_max; r += gridDim.x * 256) w[r] = w[r] != 0.f ? wr : 0.f;
@@ -2693,7 +2705,7 @@ extern "C" int lthm_rownorm_bwd(const void* x, int32_t x_dtype, const float* nor
 extern "C" int lthm_contrastive_fwd(const lthm_contrastive_desc* d, float* stats, int32_t nstat, const int32_t* ks,
                                     int32_t nk, float loss_scale, void* stream) {
   LTHM_REQUIRE(cl_check(d) == 0 && stats && d->lse && d->pos && d->cnt && d->rank && d->diag && d->w);
-  LTHM_REQUIRE(nstat >= 7 + nk);
+  LTHM_REQUIRE(nstat >= CL_NSTAT + nk);
   // several heads per launch: no tail round per head (C2: 4096 blocks a head at 3 per CU
   // is 5.33 rounds of the 768 slots; six heads together are 32)
   const int nrun = d->heads_run > 1 ? d->heads_run : 1;

@@ -863,9 +863,11 @@ extern "C" int lthm_moe_hidden_bwd(const float* dGH, const void* H, const void* 
 // idx[i] (gather) or dst row idx[i] = src row i (scatter), rows of row_bytes (a multiple of 16),
 // 16-B lanes, a block of 256 threads walking rows.  idx[i] < 0 gathers a zero row.
 namespace lthm {
-__global__ __launch_bounds__(256) void rows_move_k(const unsigned char* __restrict__ src, int64_t sld,
+// src and dst may be the same buffer when every idx[i] is i or -1 (zeroing rows in place: each
+// thread reads its 16-B chunk before it writes the same chunk), so neither is __restrict__
+__global__ __launch_bounds__(256) void rows_move_k(const unsigned char* src, int64_t sld,
                                                    const int32_t* __restrict__ idx, int64_t count,
-                                                   unsigned char* __restrict__ dst, int64_t dld, int chunks,
+                                                   unsigned char* dst, int64_t dld, int chunks,
                                                    int scatter) {
   const int64_t total = count * chunks;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {

@@ -522,9 +522,11 @@ def mlp_fwd(x2d, w1_b, b1, w2t_b, b2, res1=None, res2=None):
     for t in (res1, res2):
         _check(t is None or (t.dtype == torch.float32 and t.numel() == M * D), "mlp_fwd: f32 [M, D] residuals")
     out = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
+    # compulsory HBM bytes: x bf16, the residuals and out f32 (the hidden never leaves the chip)
+    nbytes = M * D * (2 + 4 + 4 * sum(t is not None for t in (res1, res2)))
     call("lthm_mlp_fwd", ptr(x2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(b2), ptr(res1), ptr(res2),
          ptr(out), stream(), _key=(_GEMM_TAG[-1] + ":mlp_fwd") if _GEMM_TAG else "mlp_fwd",
-         _work=4.0 * M * D * HID, _unit="flop")
+         _work=4.0 * M * D * HID, _unit="flop", _bytes=float(nbytes))
     return out
 
 
@@ -578,9 +580,10 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
     dpre = torch.empty((M, HID), dtype=torch.bfloat16, device=dev)
     if _MLP_BWD_SPLIT and HID <= 4096:
         # recompute kernel for G / dP at two waves per SIMD, then dX = dP W1 on the GEMM
+        # compulsory HBM bytes: x, dy read (bf16), g and dpre written (bf16 [M, HID] each)
         call("lthm_mlp_bwd_hidden", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(g), ptr(dpre),
              stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd", _work=4.0 * M * D * HID,
-             _unit="flop")
+             _unit="flop", _bytes=float(M * (4 * D + 4 * HID)))
         return linear_dgrad(dpre, w1_b, out_dtype=dx_dtype), g, dpre
     dx = torch.empty((M, D), dtype=dx_dtype, device=dev)
     call("lthm_mlp_bwd", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dx), dcode(dx),
@@ -592,7 +595,8 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
 # ----------------------------------------------------------------- row gather
 def rows_gather(src2d, idx, out=None):
     """dst[i] = src2d[idx[i]] (a zero row where idx[i] < 0), idx int32 on the device, rows of a
-    multiple of 16 bytes (lthm_rows_move)."""
+    multiple of 16 bytes (lthm_rows_move).  ``out`` may be ``src2d`` itself only when every
+    idx[i] is i or negative (zeroing rows in place)."""
     require_gpu(src2d, idx)
     _check(src2d.dim() == 2 and src2d.is_contiguous() and idx.dtype == torch.int32 and idx.is_contiguous(),
            "rows_gather takes a contiguous [n, W] source and int32 indices")
@@ -706,10 +710,22 @@ def _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, q_ts, kv_ts, kv_hs,
     return d
 
 
+_PACKED_OK: dict = {}
+
+
 def attn_packed_ok(T, E, mask=None):
     """The attention kernels read packed rows (a shared pad prefix's row maps) directly: the
-    long-T' 32x32x16 kernels (T > 256, E = 64, no general mask)."""
-    return T > 256 and E == 64 and mask is None
+    long-T' 32x32x16 kernels (T > 256, E = 64, no general mask, both LDS images fit, A/B
+    switches off) -- the C dispatcher's own test (lthm_attn_packed_ok), so a shape it would
+    refuse drops to the unpack path instead of raising."""
+    if mask is not None:
+        return False
+    key = (int(T), int(E))
+    ok = _PACKED_OK.get(key)
+    if ok is None:
+        from ._lib import load
+        ok = _PACKED_OK[key] = bool(load().lthm_attn_packed_ok(key[0], key[1]))
+    return ok
 
 
 def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True, mask=None, pack=None):

@@ -35,7 +35,11 @@ class ProductTowerFn(torch.autograd.Function):
         require_gpu(ids, x)
         n_full = ids.numel()
         ctx.full = None
-        if _COMPACT and n_full > 0 and x.shape[-1] * x.element_size() % 16 == 0:
+        # compaction gathers x, emb, prod and their gradients by 16-B row pieces (rows_gather): every
+        # one of those row widths must be a multiple of 16 bytes; and it reads one count to the host,
+        # which a CUDA-graph capture cannot do
+        rows16 = (x.shape[-1] * x.element_size() % 16 == 0 and w_map.shape[0] % 8 == 0 and w_pm.shape[0] % 8 == 0)
+        if _COMPACT and n_full > 0 and rows16 and not torch.cuda.is_current_stream_capturing():
             ids_f = ids.reshape(-1)
             valid = ids_f != 0
             pos = torch.cumsum(valid, 0, dtype=torch.int32)
@@ -143,7 +147,10 @@ class ProductTowerFn(torch.autograd.Function):
                 res = K.rows_gather(res, idx)
         dw_pm = K.linear_wgrad(dpb, emb)
         de = K.linear_dgrad(dpb, w_pm_b, res1=res)  # bf16 total gradient of `emb`
-        de = K.rows_gather(de, keep, out=de)  # masked tokens: zero (each row reads itself or nothing)
+        if Dout % 8 == 0:  # masked tokens: zero (in place: each row reads itself or nothing)
+            de = K.rows_gather(de, keep, out=de)
+        else:  # rows of a width rows_gather cannot move
+            de = de.masked_fill_((keep < 0)[:, None], 0)
         dw_map = K.linear_wgrad(de, xn)
         db_map = K.colsum(de) if has_b else None
         R = R_cve + max(nb, 1)

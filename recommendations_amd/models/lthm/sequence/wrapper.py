@@ -36,7 +36,7 @@ from ....commons.layers import CascadedStreamingLogQCorrectionModule
 from ....optim import FusedAdamW, SparseRowAdamW
 from .encoder import Encoder
 
-NSTAT_BASE = 7
+NSTAT_BASE = 8  # csrc/loss.hip CL_NSTAT: stats before hits@k
 LOSS_DE = 128  # operand width the loss kernels are compiled for (csrc/loss.hip DE)
 _KS_DEV: Dict[tuple, torch.Tensor] = {}  # (metric ks, device) -> int32 device copy
 
@@ -224,7 +224,7 @@ def contrastive_step(y, tgt, mask, offs: np.ndarray, mbs: int, tau: float, ks: L
     y [B, T+1, NH, De] next_token_emb, tgt [B, T, De] current_token_emb, mask [B, T] pad
     mask, offs [n_mb, NH] the lookahead offsets drawn per helper call, mbs sequences per
     helper call (B: the whole batch).  Returns the loss (mean over helper calls of the
-    per-call sum over heads) and the device statistics [NH, n_mb, 7 + len(ks)]."""
+    per-call sum over heads) and the device statistics [NH, n_mb, 8 + len(ks)]."""
     B, T = y.shape[0], y.shape[1] - 1
     n_mb = (B + mbs - 1) // mbs
     assert offs.shape[0] == n_mb, (offs.shape, n_mb)
@@ -372,7 +372,7 @@ class StepMetrics(MutableMapping):
     """The metric dict ``train_step`` / ``val_step`` return (wrapper.py:71-112, 139-142,
     221-245: same keys, same values), built lazily from the loss kernels' device statistics.
 
-    Construction issues one non-blocking device->host copy of the [NH, n_mb, 7 + len(ks)]
+    Construction issues one non-blocking device->host copy of the [NH, n_mb, 8 + len(ks)]
     statistics into pinned memory on the current stream and records an event; nothing
     waits for the GPU until a key, the length or the repr is first read, so a training
     loop that never reads the dict pays no synchronisation.  After that it behaves as a
@@ -426,7 +426,9 @@ def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[i
 
     Per helper call (wrapper.py:139-142, 221-242): batch size, sequence length, and per head
     with a usable row the offset-keyed effective batch size, mean negatives, used tokens,
-    mean CE, mean / median hit position and hits@k, then the summed loss.  With mini-batches
+    mean CE, mean / median hit position and hits@k, then the summed loss.  A head none of whose
+    used rows has a finite CE records nothing (wrapper.py:210-214: ``used_tokens == 0``);
+    effective batch size and used tokens differ only when some CE is NaN.  With mini-batches
     (wrapper.py:95-111) each key is averaged over the helper calls that produced it and
     ``{step}_overall_batch_size`` is added; a whole-batch call returns its dict as is."""
     NH, n_mb, _ = stats.shape
@@ -437,13 +439,13 @@ def lthm_metrics(stats: np.ndarray, offs: np.ndarray, step_type: str, ks: List[i
         for h in range(NH):
             st = stats[h, mb]
             off = int(offs[mb, h])
-            used = int(st[1])
-            if used == 0:
+            used, used_tokens = int(st[1]), int(st[7])
+            if used == 0 or used_tokens == 0:
                 continue
             loss_mb += float(st[0])
             m[f"{step_type}_effective_batch_size_offset_{off}"] = used
             m[f"{step_type}_average_negatives_per_token_offset_{off}"] = float(st[2])
-            m[f"{step_type}_used_tokens_offset_{off}"] = used
+            m[f"{step_type}_used_tokens_offset_{off}"] = used_tokens
             m[f"{step_type}_loss_all_tokens_offset_{off}"] = float(st[0])
             m[f"{step_type}_average_hit_position_offset_{off}"] = float(st[4])
             m[f"{step_type}_median_hit_position_offset_{off}"] = float(st[5])

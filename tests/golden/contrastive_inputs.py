@@ -106,6 +106,13 @@ CASES: Dict[str, dict] = {
     # the reference yaml's 32-sequence mini-batch at T = 512 (C5): n = 16,384 logit rows
     "train_t512": dict(kind="exact", mode="train", B=32, T=512, De=128, lookahead=[0, 3], mbs=32,
                        tau=0.05, beta=0.0, ks=[1, 10, 100], seed=16),
+    # the NaN-row filter (wrapper.py:210-214): a NaN next_token_emb row in mini-batch 0 (head 0)
+    # and in mini-batch 1 (head 1) leaves the mean and used_tokens of its (offset, mini-batch);
+    # NaN current_token_emb rows in two sequences of mini-batch 2 make every CE of that
+    # mini-batch NaN, so it contributes no loss and no per-offset metric at all
+    "train_nan": dict(kind="exact", mode="train", B=70, T=24, De=128, lookahead=[0, 2, 5], mbs=32,
+                      tau=0.05, beta=0.0, ks=[1, 5], seed=17,
+                      nan_y=[(5, 14, 0), (40, 14, 1)], nan_t=[(64, 20), (65, 20)]),
 }
 
 
@@ -125,7 +132,14 @@ def make_inputs(case: dict) -> Dict[str, np.ndarray]:
         t = rng.standard_normal((B * T, De)).astype(np.float32)
     mask = left_pad_mask(rng, B, T)
     logq = (rng.random((B, T)) * 9.0).astype(np.float32)  # logQ = -log b, b in (1e-4, 1]
-    return dict(y=y.reshape(B, T + 1, NH, De), tgt=t.reshape(B, T, De), mask=mask, logq=logq)
+    y, t = y.reshape(B, T + 1, NH, De), t.reshape(B, T, De)
+    for b, tt, h in case.get("nan_y", []):  # NaN rows (non-pad positions) for the NaN-row filter
+        assert not mask[b, min(tt + max(case["lookahead"]), T - 1)], (b, tt)
+        y[b, tt, h, :] = np.nan
+    for b, tt in case.get("nan_t", []):
+        assert not mask[b, tt], (b, tt)
+        t[b, tt, :] = np.nan
+    return dict(y=y, tgt=t, mask=mask, logq=logq)
 
 
 def inputs_digest(inp: Dict[str, np.ndarray]) -> str:

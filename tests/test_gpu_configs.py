@@ -110,15 +110,16 @@ def test_c2_slice_vs_oracle(dev, c2):
     m._rng.setstate(state)
     offs = m.draw_offsets(1)
     loss_ref, ro = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs, return_outputs=True)
-    check("C2 slice loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 2e-2)
-    check("C2 slice next_token_emb", relerr(out["next_token_emb"].float(), ro["y"]), 3e-2)
+    # measured (r04j): loss 2.2e-5, next_token_emb 4.0e-3, gradients 8.6e-3
+    check("C2 slice loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 1e-3)
+    check("C2 slice next_token_emb", relerr(out["next_token_emb"].float(), ro["y"]), 1e-2)
     loss.backward()
     loss_ref.backward()
     n_chk = 0
     for n, p in m.named_parameters():
         if p.grad is None or n not in sd or sd[n].grad is None or float(sd[n].grad.norm()) == 0.0:
             continue
-        check(f"C2 slice grad {n}", relerr(p.grad, sd[n].grad), 6e-2)  # measured max 3.0e-2 (query_tower.pad)
+        check(f"C2 slice grad {n}", relerr(p.grad, sd[n].grad), 2e-2)  # measured max 8.6e-3 (r04j)
         n_chk += 1
     assert n_chk > 30
     m.zero_grad(set_to_none=True)

@@ -11,16 +11,19 @@ use, with the offsets the reference drew.
 Cases: three mini-batches with ragged last batch, pads, an all-pad and 1- / 2-token
 sequences; val_step over the whole batch (n = 6,400 logit rows); a negative
 train_mini_batch_size (whole batch, training); logQ with beta = 0.7; the reference
-yaml's lookahead; and the yaml's 32-sequence mini-batch at T = 512 (n = 16,384).
+yaml's lookahead; the yaml's 32-sequence mini-batch at T = 512 (n = 16,384); and NaN
+rows (train_nan: the reference's NaN-row filter, wrapper.py:210-214 -- loss, used tokens,
+effective batch and negatives match it; its rank metrics over NaN logits depend on the
+order argsort gives NaNs and are not compared, nor are the NaN gradients).
 
 Tolerances:
   * "exact" inputs (every normalisation and logit exact in fp32 and in our bf16
-    operands): loss and per-offset CE 1e-5 relative; counts exact; mean negatives
+    operands): loss and per-offset CE 1e-6 relative (measured 1.4e-7); counts exact; mean negatives
     1e-6; hit position / median / hits@k inside the interval every order of tied
     logits allows (computed from the same exact logits, and containing the
     reference's value); gradients 1e-2 relative Frobenius (dS enters the second
     MFMA as bf16);
-  * "float" inputs (random fp32, rounded to bf16 by the GPU path only): loss 2e-3,
+  * "float" inputs (random fp32, rounded to bf16 by the GPU path only): loss 1e-3 (measured 2.6e-4),
     ranks / hits within the flips that bf16 rounding of the operands causes
     (bounds below), gradients 2e-2.
 """
@@ -63,6 +66,11 @@ def _run(dev, case, fx, ydt):
 
 def _grad_checks(name, fx, dy, dt, bound):
     De = dy.shape[-1]
+    if not (np.isfinite(float(fx["dy_norm"])) and np.isfinite(float(fx["dt_norm"]))):
+        # a NaN row (train_nan): the reference's gradients are NaN (its matmul backward multiplies
+        # the filtered rows' zero dlogits by the NaN embedding), and so are ours
+        assert not (torch.isfinite(dy).all() and torch.isfinite(dt).all())
+        return
     if "dy" in fx:
         check(f"{name} d next_token_emb", relerr(dy, torch.from_numpy(fx["dy"])), bound)
         check(f"{name} d current_token_emb", relerr(dt, torch.from_numpy(fx["dt"])), bound)
@@ -87,7 +95,7 @@ def test_contrastive_vs_reference_goldens(dev, name, ydt):
     fx = golden("contrastive_" + name)
     loss, met, dy, dt = _run(dev, case, fx, torch.float32 if ydt == "f32" else torch.bfloat16)
     tag = f"{name}/{ydt}"
-    lb = 1e-5 if exact else 2e-3
+    lb = 1e-6 if exact else 1e-3  # measured (r04j): 1.4e-7 / 2.6e-4
     ref_loss = float(fx["loss"][0])
     check(f"{tag} loss", abs(float(loss) - ref_loss) / abs(ref_loss), lb)
     check_metrics(tag, met, fx, exact, lb)
@@ -102,7 +110,8 @@ def check_metrics(tag, met, fx, exact, lb):
     ref = dict(zip([str(k) for k in fx["metric_keys"]], fx["metric_values"].tolist()))
     assert set(met) == set(ref), (sorted(set(met) ^ set(ref)))
     bounds = {}
-    if exact:
+    nan_case = exact and "bound_keys" not in fx  # train_nan: no tie intervals over NaN logits
+    if exact and not nan_case:
         bounds = {str(k): (lo, hi) for k, lo, hi in zip(fx["bound_keys"], fx["bound_lo"], fx["bound_hi"])}
     for k, rv in ref.items():
         v = met[k]
@@ -112,6 +121,8 @@ def check_metrics(tag, met, fx, exact, lb):
             check(f"{tag} {k}", abs(v - rv) / max(abs(rv), 1.0), 1e-6)
         elif k.endswith("_loss") or "loss_all_tokens" in k:
             check(f"{tag} {k}", abs(v - rv) / max(abs(rv), 1e-6), lb)
+        elif nan_case:
+            continue  # rank metrics over NaN logits: argsort's order of NaNs (see the module docstring)
         elif exact:  # rank metrics: inside the tie interval (which holds the reference's value)
             lo, hi = bounds[k]
             assert lo - 1e-5 * max(1.0, abs(lo)) <= v <= hi + 1e-5 * max(1.0, abs(hi)), (k, v, lo, hi, rv)

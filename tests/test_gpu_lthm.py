@@ -134,8 +134,9 @@ def test_lthm_step_vs_oracle(dev, B, T, d, L, H):
     offs = m.draw_offsets(n_mb)
     loss_ref, ro = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs, return_outputs=True)
     # bf16 activations through 2 blocks + tau = 0.05 logits
-    check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 2e-2)
-    check('out["next_token_emb"].float(), ro["y"]', relerr(out["next_token_emb"].float(), ro["y"]), 3e-2)
+    # measured (r04j): loss 2.5e-5, next_token_emb 4.4e-3, gradients 8.4e-3
+    check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 1e-3)
+    check('out["next_token_emb"].float(), ro["y"]', relerr(out["next_token_emb"].float(), ro["y"]), 1e-2)
     metrics = m.metrics()
     assert np.isfinite(list(metrics.values())).all()
     loss.backward()
@@ -152,7 +153,7 @@ def test_lthm_step_vs_oracle(dev, B, T, d, L, H):
         gr = sd[key].grad
         if gr is None or float(gr.norm()) == 0.0:
             continue
-        check(f"grad {n}", relerr(gp, gr), 4e-2)  # measured max 2.0e-2 (r02a)
+        check(f"grad {n}", relerr(gp, gr), 2e-2)  # measured max 8.4e-3 (r04j)
         checked += 1
     assert checked > 30
 
@@ -180,7 +181,7 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     """BASELINE configs[4] (C5) shape at a small batch: T = 512 (T' = 513, the windowed
     attention), d = 512, H = 8, fp8 e4m3 forward encoder GEMMs, the yaml's 32-sequence loss
     mini-batch (here the whole 16-sequence batch: 8,192 logit rows per head), vs the fp32 oracle.  e4m3 operands (3 mantissa bits, per-tensor
-    scales): 5e-2 on the loss and the head outputs, 8e-2 relative on gradients (2x the
+    scales): 1e-3 on the loss and 1e-2 on the head outputs (measured 3.6e-6 / 4.5e-3), 8e-2 relative on gradients (2x the
     measured maximum)."""
     from recommendations_amd.data import synthetic_lthm_batch
     B, T = 16, 512
@@ -194,8 +195,9 @@ def test_lthm_c5_shape_fp8_step_vs_oracle(dev):
     m._rng.setstate(state)
     offs = m.draw_offsets((B + 31) // 32)
     loss_ref, ro = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs, return_outputs=True)
-    check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 5e-2)
-    check('out["next_token_emb"].float(), ro["y"]', relerr(out["next_token_emb"].float(), ro["y"]), 5e-2)
+    # measured (r04j): loss 3.6e-6, next_token_emb 4.5e-3
+    check("loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 1e-3)
+    check('out["next_token_emb"].float(), ro["y"]', relerr(out["next_token_emb"].float(), ro["y"]), 1e-2)
     loss.backward()
     loss_ref.backward()
     checked = 0
@@ -263,7 +265,7 @@ def test_lthm_multi_step_vs_oracle_adamw(dev):
         m._rng.setstate(state)
         offs = m.draw_offsets(4)
         loss_ref = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs)
-        check(f"step {it} loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 2e-2)
+        check(f"step {it} loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 1e-3)  # measured 6.2e-5
         loss.backward()
         loss_ref.backward()
         for o in opts:
@@ -313,7 +315,7 @@ def test_lthm_logq_step_vs_oracle(dev):
             mod.a.copy_(a)
     corr = twin.stream_correction(out["current_token_ids"], out["current_token_mask"], 32, 0, 0.5).cpu()
     loss_ref = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs, logq=corr)
-    check("logq loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 2e-2)
+    check("logq loss", abs(float(loss) - float(loss_ref)) / abs(float(loss_ref)), 1e-3)  # measured 5.3e-6
     loss_plain = lthm_ref.lthm_forward_loss(sd, cfg, batch, offs)
     assert abs(float(loss_ref) - float(loss_plain)) > 1e-3  # the correction does change the loss
 

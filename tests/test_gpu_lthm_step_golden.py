@@ -8,11 +8,13 @@ the same batch and the offsets the reference drew, and runs forward -> train_ste
 through the HIP kernels.  tests/test_lthm_step_golden_cpu.py pins the oracle to the same
 fixtures on the CPU (loss bit-equal, gradients 2e-7).
 
-Bounds (bf16 operands through the encoder GEMMs and attention against fp32; measured errors
-are recorded through tests/parity.py): next_token_emb 3e-2 relative Frobenius over the rows
-the loss reads; the loss and the per-offset CE 2e-2; counts exact; every trainable
-parameter's gradient 8e-2 relative Frobenius (the same bound as the C5-shape step against
-the oracle, test_gpu_lthm.py)."""
+Bounds (bf16 operands through the encoder GEMMs and attention against fp32; about 2x the
+errors measured on the round-4 final tree, gpurun_out/r04j_parity.json, recorded through
+tests/parity.py): next_token_emb 1e-2 relative Frobenius (measured 4.2e-3);
+current_token_emb 7e-3 (3.5e-3); the loss and the per-offset CE 1e-3, the north star's bound
+(measured 3.9e-4); counts exact; the rank metrics within the flips bf16 rounding of the
+logits causes (hit rates 5e-2 absolute, mean / median hit position 5e-2 relative); every
+trainable parameter's gradient 2e-2 relative Frobenius (measured max 9.6e-3)."""
 import numpy as np
 import pytest
 import torch
@@ -40,11 +42,11 @@ def test_hip_step_vs_reference(dev, name, monkeypatch):
     assert y.shape == ref_y.shape, (y.shape, ref_y.shape)
     mask = torch.from_numpy(fx["current_token_mask"]).reshape(ref_y.shape[0], -1)
     assert torch.equal(out["current_token_mask"].cpu().reshape(mask.shape).bool(), mask.bool())
-    check(f"{name} next_token_emb", relerr(y, ref_y), 3e-2)
+    check(f"{name} next_token_emb", relerr(y, ref_y), 1e-2)
     check(f"{name} current_token_emb", relerr(out["current_token_emb"].float().cpu(),
-                                             torch.from_numpy(fx["current_token_emb"])), 1e-2)
+                                             torch.from_numpy(fx["current_token_emb"])), 7e-3)
     ref_loss = float(fx["loss"][0])
-    check(f"{name} loss", abs(float(loss) - ref_loss) / abs(ref_loss), 2e-2)
+    check(f"{name} loss", abs(float(loss) - ref_loss) / abs(ref_loss), 1e-3)
     ref_m = dict(zip([str(k) for k in fx["metric_keys"]], fx["metric_values"].tolist()))
     assert set(metrics) == set(ref_m), sorted(set(metrics) ^ set(ref_m))
     for k, rv in ref_m.items():
@@ -52,9 +54,15 @@ def test_hip_step_vs_reference(dev, name, monkeypatch):
         if any(s in k for s in ("batch_size", "seq_len", "used_tokens", "average_negatives")):
             assert abs(v - rv) <= 1e-6 * max(1.0, abs(rv)), (k, v, rv)
         elif "loss" in k:
-            check(f"{name} {k}", abs(v - rv) / max(abs(rv), 1e-6), 2e-2)
+            check(f"{name} {k}", abs(v - rv) / max(abs(rv), 1e-6), 1e-3)
+        elif "hit_rate" in k:  # a few rank flips among the mini-batch's rows
+            check(f"{name} {k}", abs(v - rv), 5e-2)
+        elif "hit_position" in k:
+            check(f"{name} {k}", abs(v - rv) / max(abs(rv), 1.0), 5e-2)
+        else:
+            raise AssertionError(f"unchecked metric {k}")
     named = dict(m.named_parameters())
     for k, g in grads.items():
         got = named[k].grad
         assert got is not None, k
-        check(f"{name} grad {k}", relerr(got.float().cpu(), g), 8e-2)
+        check(f"{name} grad {k}", relerr(got.float().cpu(), g), 2e-2)

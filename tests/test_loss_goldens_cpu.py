@@ -39,7 +39,13 @@ def test_oracle_vs_reference_goldens(name):
     assert abs(float(loss) - ref_loss) <= 1e-5 * abs(ref_loss)
     loss.backward()
     De = y.shape[-1]
-    if "dy" in fx:
+    if not np.isfinite(float(fx["dy_norm"])):
+        # train_nan: the reference's gradients carry NaN (0 dlogits x the NaN embedding in its matmul
+        # backward); the oracle's NaN pattern is the reference's
+        ry, rt = torch.from_numpy(fx["dy_rows"]), torch.from_numpy(fx["dt_rows"])
+        assert torch.equal(torch.isnan(y.grad.reshape(-1, De)[ry]), torch.isnan(torch.from_numpy(fx["dy_sample"])))
+        assert torch.equal(torch.isnan(t.grad.reshape(-1, De)[rt]), torch.isnan(torch.from_numpy(fx["dt_sample"])))
+    elif "dy" in fx:
         gy, gt = torch.from_numpy(fx["dy"]), torch.from_numpy(fx["dt"])
         assert float((y.grad - gy).norm() / gy.norm()) < 1e-5
         assert float((t.grad - gt).norm() / gt.norm()) < 1e-5
