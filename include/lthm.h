@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 38 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 39 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -213,6 +213,19 @@ int lthm_mlp_bwd(const void* x, const void* dY, int64_t M, int32_t D, int32_t HI
  * GEMM.  HID <= 4096. */
 int lthm_mlp_bwd_hidden(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
                         const float* b1, const void* W2T, void* G, void* dP, void* stream);
+/* The training backward with NO [M, HID] operand in HBM (round 5): two recompute kernels.
+ * lthm_mlp_bwd_dx: dX = ((dY W2) * GELU'(x W1^T + b1)) W1 alone (dX in dx_dtype). */
+int lthm_mlp_bwd_dx(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                    const float* b1, const void* W2T, void* dX, int32_t dx_dtype, void* stream);
+/* lthm_mlp_wgrad: dW1 = dP^T x (f32 [HID, D], c_fc.weight's gradient), dW2 = dY^T G (f32 [D, HID],
+ * c_proj.weight's), db1 = colsum dP (f32 [HID], or NULL) with G / dP recomputed per token tile
+ * inside the kernel; partial sums per token slice go to the workspace (>= lthm_mlp_wgrad_ws_bytes)
+ * and are folded in slice order (deterministic).  HID % 128 == 0.  Replaces the c_fc / c_proj
+ * weight-gradient products of commons/transformers/layers.py:279-284's backward. */
+int64_t lthm_mlp_wgrad_ws_bytes(int64_t M, int32_t D, int32_t HID);
+int lthm_mlp_wgrad(const void* x, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                   const float* b1, const void* W2T, float* dW1, float* dW2, float* db1, void* workspace,
+                   int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm (commons/transformers/layers.py:142-149, eps 1e-5)               */

@@ -74,6 +74,11 @@ _MLP_TRAIN = os.environ.get("LTHM_MLP_TRAIN", "1") == "1"
 _MLP_LN = os.environ.get("LTHM_MLP_LN", "0") == "1"
 # ln_2's backward writes dx1 + dy as its f32 output for ln_1's backward (LTHM_LN_FOLD=0: separately)
 _LN_FOLD = os.environ.get("LTHM_LN_FOLD", "1") == "1"
+# LTHM_MLP_WG=1: the fused MLP's backward without [M, 4d] operands in HBM (round 5:
+# lthm_mlp_bwd_dx + lthm_mlp_wgrad, both recomputing the hidden; one wave per SIMD, issue-bound
+# on the GELU' VALU: C2 step 40.8-41.0 ms against 39.9 for the default, profiles/r05e/).  Default:
+# the recompute kernel writing G / dP for the dX GEMM and the two weight-gradient GEMMs (round 4)
+_MLP_WG = os.environ.get("LTHM_MLP_WG", "0") == "1"
 
 
 class TransformerBlockFn(torch.autograd.Function):
@@ -209,11 +214,15 @@ class TransformerBlockFn(torch.autograd.Function):
         if ctx.fused_mlp:
             # saved: pre -> b1 (f32 or None), g -> c_proj.weight^T (bf16); the hidden is recomputed
             b1f, w2t_b = pre, g
-            dh2, g, dpre = K.mlp_bwd(h2, dyb, w1_b, b1f, w2t_b)
-            dw2 = K.linear_wgrad(dyb, g)
+            if _MLP_WG and K.mlp_wgrad_supported(d, w1_b.shape[0]):
+                dh2 = K.mlp_bwd_dx(h2, dyb, w1_b, b1f, w2t_b)
+                dw1, dw2, db1 = K.mlp_wgrad(h2, dyb, w1_b, b1f, w2t_b, want_db1=has_b1)
+            else:
+                dh2, g, dpre = K.mlp_bwd(h2, dyb, w1_b, b1f, w2t_b)
+                dw2 = K.linear_wgrad(dyb, g)
+                dw1 = K.linear_wgrad(dpre, h2)
+                db1 = K.colsum(dpre) if has_b1 else None
             db2 = K.colsum(dym) if has_b2 else None
-            dw1 = K.linear_wgrad(dpre, h2)
-            db1 = K.colsum(dpre) if has_b1 else None
         else:
             dw2 = K.linear_wgrad(dyb, g)
             db2 = K.colsum(dym) if has_b2 else None

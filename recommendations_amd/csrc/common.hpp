@@ -226,6 +226,13 @@ __device__ __forceinline__ void glds4(const void* src, void* lds) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(src), "s"(lds_addr(lds)) : "memory");
 }
+// glds16 with the LDS byte address already in hand (wave-uniform, e.g. a base read once by
+// lds_addr plus constants): no per-call address-space cast or readfirstlane
+__device__ __forceinline__ void glds16_m0(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

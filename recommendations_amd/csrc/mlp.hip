@@ -67,6 +67,22 @@ struct MlpBwdArgs {
   int HID;
 };
 
+// The weight-gradient kernel (mlp_wgrad_k): per (token slice, hidden group) partial slabs
+struct MlpWgArgs {
+  const bf16_t* X;    // [M, D] ln_2 output (bf16)
+  const bf16_t* dY;   // [M, D] gradient of the MLP output (bf16)
+  const bf16_t* W1;   // [HID, D] c_fc.weight (bf16)
+  const bf16_t* W2T;  // [HID, D] c_proj.weight^T (bf16)
+  const float* b1;    // [HID] or null
+  float* dW1p;        // [nslice][HID][D] partial dW1 = dpre^T x
+  float* dW2Tp;       // [nslice][HID][D] partial dW2^T = g^T dy
+  float* db1p;        // [nslice][HID] partial colsum dpre (or null)
+  int64_t M;
+  int HID;
+  int nslice;         // token slices
+  int ngroup;         // hidden groups (HID / (32 NW))
+};
+
 typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
 typedef short s16x4m __attribute__((ext_vector_type(4)));
 typedef short s16x8m __attribute__((ext_vector_type(8)));
@@ -98,6 +114,47 @@ __device__ __forceinline__ void mlp_dma32(unsigned char* img, const bf16_t* P, i
     glds16(P + (int64_t)r * D + c * 8, img + (m * NTH + wbase) * 16);
   }
 }
+
+// mlp_dma32 of the rows row0 .. row0 + 31 of a [M, D] tensor, rows past nvalid read as row
+// row0 + nvalid - 1 (in bounds; the kernel zeroes their contributions)
+template <int D, int NTH>
+__device__ __forceinline__ void mlp_dma32c(unsigned char* img, const bf16_t* P, int64_t row0, int nvalid, int tid) {
+  constexpr int SLOTS = 32 * D / 8;
+  static_assert(SLOTS % NTH == 0, "image slots must divide over the workgroup");
+  const int wbase = tid & ~63;
+#pragma unroll
+  for (int m = 0; m < SLOTS / NTH; ++m) {
+    const int o = (m * NTH + tid) * 16;
+    const int r1 = o % (16 * D);
+    const int r = 8 * (o / (16 * D)) + (r1 % 512) / 64;
+    const int c = 4 * (r1 / 512) + (((r1 % 64) / 16) ^ ((r >> 2) & 3));
+    glds16(P + (row0 + min(r, nvalid - 1)) * D + c * 8, img + (m * NTH + wbase) * 16);
+  }
+}
+
+// mlp_dma32 with the per-thread source offsets precomputed (MlpDmaPlan) and the destination given
+// as an LDS byte address: per piece one 64-bit add and the DMA
+template <int D, int NTH>
+struct MlpDmaPlan {
+  static constexpr int PIECES = 32 * D / 8 / NTH;
+  int off[PIECES];  // element offset of piece m's 16 source bytes within a [32 x D] block
+  __device__ __forceinline__ void init(int tid) {
+#pragma unroll
+    for (int m = 0; m < PIECES; ++m) {
+      const int o = (m * NTH + tid) * 16;
+      const int r1 = o % (16 * D);
+      const int r = 8 * (o / (16 * D)) + (r1 % 512) / 64;
+      const int c = 4 * (r1 / 512) + (((r1 % 64) / 16) ^ ((r >> 2) & 3));
+      off[m] = r * D + c * 8;
+    }
+  }
+  // block P (32 rows of D, row stride D) into the image at LDS byte address lds (wave-uniform base
+  // of the image + the wave's 1-KiB slice: lds_img + (tid & ~63) * 16)
+  __device__ __forceinline__ void issue(const bf16_t* P, uint32_t lds_wave) const {
+#pragma unroll
+    for (int m = 0; m < PIECES; ++m) glds16_m0(P + off[m], lds_wave + m * NTH * 16);
+  }
+};
 
 // A operand of 32x32x16 from a [32][D] image: lane (r = l & 31, h = l >> 5) row r, k 16 ks + 8 h ..
 template <int D>
@@ -525,7 +582,7 @@ __global__ __launch_bounds__(256, 1) void mlp_fwd_pipe_k(MlpArgs a) {
 //                                                    transposed reads of the same W1_j image)
 // g and dp leave through the wave's LDS strip as 64-B row pieces.  One wave per SIMD (the
 // x / dy fragments and the dX accumulator are 256 registers).
-template <int D, int NW>
+template <int D, int NW, bool GH>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
   constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
   __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
@@ -584,8 +641,9 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
           gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
           dp[4 * m + e] = dH[4 * m + e] * gd;
         }
-        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
-            uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
+        if constexpr (GH)
+          *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
+              uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
       }
       const bf16x8m d0 = mlp_pack(dp), d1 = mlp_pack(dp + 8);
 #pragma unroll
@@ -594,6 +652,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
         acc[t] = mfma32(d1, mlp_tr_frag<D>(w1, lane, 1, t), acc[t]);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (!GH) continue;  // dX only (the weight gradients come from mlp_wgrad_k)
       // g and dp of the chunk: [32 tokens][32 units] bf16 through the strip (8-B writes of
       // 4 consecutive units), then 16-B row pieces: lane -> row l / 4 (+ 16), piece l % 4
 #pragma unroll
@@ -630,6 +689,170 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwd_k(MlpBwdArgs a) {
         const int64_t row = rb + pr + 8 * m;
         const f32x4 v = *reinterpret_cast<const f32x4*>(stg + (pr + 8 * m) * 32 + pc);
         if (row < lim) {
+          if (a.dx_f32) {
+            *reinterpret_cast<f32x4*>(a.dXf + row * D + 32 * t + pc) = v;
+          } else {
+            *reinterpret_cast<uint2*>(a.dXb + row * D + 32 * t + pc) =
+                uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
+// dX alone, software-pipelined (round 5; the weight gradients come from mlp_wgrad_k, so neither
+// G nor dP is written).  One wave per SIMD, a wave owns 32 token rows (x and dy in registers as B
+// operands, the dX sum in the accumulator registers); the hidden chunks' W1_j / W2T_j images ride
+// a 4-slot LDS-DMA ring.  Step j of a tile is ONE interleaved loop of KS iterations; iteration k
+// issues
+//   S'^T += W1_{j+1} . x^T, dH'^T += W2T_{j+1} . dy^T   k-step k (2 MFMAs; row reads one step ahead)
+//   dX   += dp_{j-1} . W1_{j-1}                          output tile k / 2, k-half k % 2 (1 MFMA)
+//   GELU' element(s) of chunk j from its S^T / dH^T      (the VALU in those MFMAs' issue gaps)
+// so the vector work of a chunk spreads over all 48 of its MFMAs.  The chunk stream runs on across
+// tiles (chunk index wraps); a tile's first step adds dp = 0 (exact zeros), its last step's S' / dH'
+// (of the next tile's first chunk image, with this tile's x / dy) are discarded.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_bwdx_k(MlpBwdArgs a) {
+  constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW, NS = 4;
+  static_assert(KS == 2 * NT, "one dX MFMA per k-step");
+  constexpr int EPK = 16 / KS;  // GELU' elements per iteration
+  __shared__ __attribute__((aligned(16))) unsigned char img[NS][2][IMG];  // [slot][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) float stg_all[NW][32 * 32];    // per-wave epilogue strips
+  __shared__ __attribute__((aligned(16))) float b1s[4096];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  float* stg = stg_all[wave];
+  retire_loads();
+  const int64_t ntile = (re - rs + TR - 1) / TR;
+  const int nchunk = (int)(ntile * NC);  // the workgroup's chunk stream
+  MlpDmaPlan<D, NTH> plan;
+  plan.init(tid);
+  const uint32_t lds0 = lds_addr(img[0][0]) + (uint32_t)(tid & ~63) * 16u;  // this wave's slice of slot 0
+  int sjn = 0;  // hidden chunk index of the next chunk to stage (the stream's index mod NC)
+  auto stage = [&](int c) {  // chunk c of the stream, hidden chunk sjn
+    const uint32_t d = lds0 + (uint32_t)(c & (NS - 1)) * (2u * IMG);
+    plan.issue(a.W1 + (int64_t)sjn * 32 * D, d);
+    plan.issue(a.W2T + (int64_t)sjn * 32 * D, d + IMG);
+    if (++sjn == NC) sjn = 0;
+  };
+  stage(0);
+  if (nchunk > 1) stage(1);
+  int g = 0;  // chunk index of the current step in the workgroup's stream
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    // every wave computes (a wave past the tile's rows reads the clamped first row and stores
+    // nothing): no wave-dependent branch around the accumulator updates
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform
+    bf16x8m xf[KS], df[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    // chunk g (the tile's first) landed everywhere (also: the x / dy loads above)
+    wait_vm<0>();
+    __syncthreads();
+    f32x16 S = f32x16{}, H = f32x16{};
+    {
+      const unsigned char* w1 = img[g & (NS - 1)][0];
+      const unsigned char* w2 = img[g & (NS - 1)][1];
+      bf16x8m fa = mlp_row_frag<D>(w1, lane, 0), fb = mlp_row_frag<D>(w2, lane, 0);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int kn = k + 1 < KS ? k + 1 : k;
+        const bf16x8m na = mlp_row_frag<D>(w1, lane, kn), nb = mlp_row_frag<D>(w2, lane, kn);
+        S = mfma32(fa, xf[k], S);
+        H = mfma32(fb, df[k], H);
+        fa = na;
+        fb = nb;
+        asm volatile("" ::: "memory");
+      }
+    }
+    u32x4 dp0 = {0u, 0u, 0u, 0u}, dp1 = dp0;  // packed dp of the previous chunk (zero before the first)
+    for (int j = 0; j < NC; ++j, ++g) {
+      if (j > 0) {
+        // every wave is done with step j - 1 (the slot of chunk g - 2 is free); chunk g + 1 landed
+        wait_vm<0>();
+        __syncthreads();
+        asm volatile("" ::: "memory");
+      }
+      // chunk g + 2 into the slot of chunk g - 2 (last read by step g - 1: every wave passed this
+      // step's barrier, or the tile's opening one at j = 0)
+      if (g + 2 < nchunk) stage(g + 2);
+      const unsigned char* w1p = img[(j > 0 ? g - 1 : g) & (NS - 1)][0];  // dX: chunk g - 1's W1 (or dp = 0)
+      const unsigned char* w1n = img[(g + 1) & (NS - 1)][0];              // S' / dH' of chunk g + 1
+      const unsigned char* w2n = img[(g + 1) & (NS - 1)][1];
+      const bf16x8m d0 = __builtin_bit_cast(bf16x8m, dp0), d1 = __builtin_bit_cast(bf16x8m, dp1);
+      f32x16 Sn = f32x16{}, Hn = f32x16{};
+      float dl = 0.f;
+      f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 4 * h);
+      // LDS fragments two iterations ahead (one iteration is 3 MFMAs, ~100 cycles: less than an LDS
+      // read's latency under load)
+      bf16x8m fa = mlp_row_frag<D>(w1n, lane, 0), fb = mlp_row_frag<D>(w2n, lane, 0);
+      bf16x8m bt = mlp_tr_frag<D>(w1p, lane, 0, 0);
+      bf16x8m fa1 = mlp_row_frag<D>(w1n, lane, 1), fb1 = mlp_row_frag<D>(w2n, lane, 1);
+      bf16x8m bt1 = mlp_tr_frag<D>(w1p, lane, 1, 0);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int kn = k + 2 < KS ? k + 2 : KS - 1;
+        const bf16x8m na = mlp_row_frag<D>(w1n, lane, kn), nb = mlp_row_frag<D>(w2n, lane, kn);
+        const bf16x8m nt_ = mlp_tr_frag<D>(w1p, lane, kn & 1, kn >> 1);
+        Sn = mfma32(fa, xf[k], Sn);
+        acc[k >> 1] = mfma32((k & 1) ? d1 : d0, bt, acc[k >> 1]);
+        Hn = mfma32(fb, df[k], Hn);
+#pragma unroll
+        for (int ee = 0; ee < EPK; ++ee) {
+          const int e = k * EPK + ee;  // register e: unit 8 (e >> 2) + 4 h + (e & 3) of chunk j
+          if ((e & 3) == 0 && e > 0) bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * (e >> 2) + 4 * h);
+          const float dk = H[e] * gelu_tanh_grad(S[e] + bb[e & 3]);
+          if (e & 1) {
+            uint32_t dw = pack_bf16x2(dl, dk);
+            asm volatile("" : "+v"(dw)::"memory");  // element e's VALU stays beside these MFMAs
+            if (e < 8) dp0[(e >> 1) & 3] = dw;
+            else dp1[(e >> 1) & 3] = dw;
+          } else {
+            dl = dk;
+            asm volatile("" : "+v"(dl)::"memory");
+          }
+        }
+        fa = fa1;
+        fb = fb1;
+        bt = bt1;
+        fa1 = na;
+        fb1 = nb;
+        bt1 = nt_;
+      }
+      S = Sn;
+      H = Hn;
+    }
+    {  // dX of the tile's last chunk (g - 1)
+      const unsigned char* w1p = img[(g - 1) & (NS - 1)][0];
+      const bf16x8m d0 = __builtin_bit_cast(bf16x8m, dp0), d1 = __builtin_bit_cast(bf16x8m, dp1);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] = mfma32(d0, mlp_tr_frag<D>(w1p, lane, 0, t), acc[t]);
+        acc[t] = mfma32(d1, mlp_tr_frag<D>(w1p, lane, 1, t), acc[t]);
+      }
+    }
+    // dX [32 tokens][D]: each 32-column tile through the strip, 16-B pieces out
+    const int pr = lane >> 3, pc = 4 * (lane & 7);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) stg[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r32] = acc[t][i];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t row = rb + pr + 8 * m;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stg + (pr + 8 * m) * 32 + pc);
+        if (active && row < lim) {
           if (a.dx_f32) {
             *reinterpret_cast<f32x4*>(a.dXf + row * D + 32 * t + pc) = v;
           } else {
@@ -733,6 +956,235 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
     }
+  }
+}
+
+// ---------------------------------------------------------------- weight gradients (recompute)
+// dW1 = dpre^T x, dW2^T = g^T dy, db1 = colsum dpre with g / dpre recomputed per token tile and
+// never written: the loop order is the transpose of the kernels above.  A wave OWNS 32 hidden
+// units j (its W1_j / W2T_j rows live in registers as B operands) and its dW1_j / dW2^T_j
+// [32 x D] sums live in the accumulator registers for the whole kernel; the workgroup (NW
+// waves, NW * 32 hidden units = one hidden group) walks the token tiles of its slice, each
+// [32 x D] x and dy tile staged once into LDS by LDS-DMA (3-slot ring) and read by every wave:
+//   S  = x . W1_j^T,  dH = dy . W2T_j^T      (tokens on the accumulator registers, hidden units
+//                                             on the lanes: 2 x D / 16 MFMAs)
+//   g  = GELU(S + b1), dp = dH GELU'(S + b1)  (one v_exp + one v_rcp per element)
+//   dW1_j   += dp^T . x,  dW2^T_j += g^T . dy (the packed accumulators ARE the A operands over
+//                                             the permuted token order; B = transposed reads of
+//                                             the staged tiles: 2 x D / 16 MFMAs)
+// so per token tile and wave 4 D / 16 MFMAs, no HBM traffic beyond x and dy (read once per
+// hidden group; the groups of one slice run on one XCD, so the repeats are L2 hits).  The slabs
+// [nslice][HID][D] are folded in slice order by mlp_wgrad_fold_k (no atomics, deterministic).
+template <int D, int NW, bool FULL>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_wgrad_k(MlpWgArgs a) {
+  constexpr int NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, NS = 3;
+  constexpr int DPT = 2 * (32 * D / 8) / NTH;  // DMAs per thread and tile (both images)
+  // 3-slot ring of (x, dy) tiles + each wave's W2T_j image: 160 KiB at D = 256.  The dW sums take
+  // the 256 accumulator registers and W1_j's B operands 64 of the 256 others, so W2T_j's B
+  // operands are read from LDS (a second ds_read_b128 in the dH MFMA gaps)
+  __shared__ __attribute__((aligned(16))) unsigned char img[NS][2][IMG];  // [slot][x, dy]
+  __shared__ __attribute__((aligned(16))) unsigned char wimg[NW][IMG];    // W2T_j per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  // XCD-contiguous logical order: the hidden groups of one slice share an XCD's L2
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = lid / a.ngroup, grp = lid - slice * a.ngroup;
+  const int64_t ntile_all = (a.M + 31) / 32;
+  const int64_t t_lo = ntile_all * slice / a.nslice, t_hi = ntile_all * (slice + 1) / a.nslice;
+  const int j0 = (grp * NW + wave) * 32;  // this wave's hidden units j0 .. j0 + 31
+  // B operands over d of the wave's W1 rows: lane -> unit j0 + r32, k 16 k + 8 h ..
+  bf16x8m w1f[KS];
+  {
+    const bf16_t* p1 = a.W1 + (int64_t)(j0 + r32) * D + 8 * h;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) w1f[k] = __builtin_bit_cast(bf16x8m, *reinterpret_cast<const u32x4*>(p1 + 16 * k));
+  }
+  unsigned char* w2i = wimg[wave];
+  const float bj = a.b1 ? a.b1[j0 + r32] : 0.f;
+  f32x16 acc1[NT], acc2[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc1[t] = acc2[t] = f32x16{};
+  float dbs = 0.f;
+  retire_loads();
+  const int nt = (int)(t_hi - t_lo);
+  MlpDmaPlan<D, NTH> plan;
+  plan.init(tid);
+  const uint32_t lds0 = lds_addr(img[0][0]) + (uint32_t)(tid & ~63) * 16u;  // this wave's slice of slot 0
+  auto stage = [&](int64_t ti, int slot) {
+    const int64_t r0 = ti * 32;
+    if (FULL) {  // every tile whole: the precomputed plan
+      const uint32_t d = lds0 + (uint32_t)slot * (2u * IMG);
+      plan.issue(a.X + r0 * D, d);
+      plan.issue(a.dY + r0 * D, d + IMG);
+    } else {
+      const int nv = (int)min((int64_t)32, a.M - r0);
+      mlp_dma32c<D, NTH>(img[slot][0], a.X, r0, nv, tid);
+      mlp_dma32c<D, NTH>(img[slot][1], a.dY, r0, nv, tid);
+    }
+  };
+  // Software pipeline, one wave per SIMD (the dW sums hold the 256 accumulator registers): step i
+  // runs
+  //   phase B: dW += of tile i - 1 (32 MFMAs; transposed tile reads one pair ahead)  ||  GELU of
+  //            tile i from its S / dH registers (the VALU in the MFMA issue gaps), packed to bf16
+  //   barrier; LDS-DMA of tile i + 2 into the slot of tile i - 1 (free now)
+  //   phase A: S / dH of tile i + 1 (32 MFMAs)
+  // so only one S / dH pair and two packed operand sets are live.  Tile i + 1 was staged during
+  // step i - 1 (after its barrier); tile i is not read by step i at all.
+  mlp_dma32<D, 64>(w2i, a.W2T + (int64_t)j0 * D, lane);  // the wave's own image (retired with tile 0)
+  if (nt > 0) stage(t_lo, 0);
+  if (nt > 1) stage(t_lo + 1, 1);
+  f32x16 S = f32x16{}, H = f32x16{};
+  auto phase_a = [&](const unsigned char* xn, const unsigned char* yn) {
+    bf16x8m fa = mlp_row_frag<D>(xn, lane, 0), fb = mlp_row_frag<D>(yn, lane, 0), fw = mlp_row_frag<D>(w2i, lane, 0);
+    S = f32x16{};
+    H = f32x16{};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int kn = k + 1 < KS ? k + 1 : k;
+      const bf16x8m na = mlp_row_frag<D>(xn, lane, kn), nb = mlp_row_frag<D>(yn, lane, kn);
+      const bf16x8m nw = mlp_row_frag<D>(w2i, lane, kn);
+      S = mfma32(fa, w1f[k], S);
+      H = mfma32(fb, fw, H);
+      fa = na;
+      fb = nb;
+      fw = nw;
+      asm volatile("" ::: "memory");
+    }
+  };
+  if (nt > 0) {
+    if (nt > 1) wait_vm<DPT>();
+    else wait_vm<0>();
+    __syncthreads();
+    phase_a(img[0][0], img[0][1]);
+  }
+  // packed operands of the previous tile (zero before tile 0: phase B of step 0 adds exact zeros
+  // from tile 0's finite rows)
+  u32x4 gp0 = {0u, 0u, 0u, 0u}, gp1 = gp0, dp0 = gp0, dp1 = gp0;
+  for (int i = 0; i < nt; ++i) {
+    // ---- phase B: dW of tile i - 1 || GELU of tile i
+    {
+      const int ip = i > 0 ? i - 1 : 0;
+      const unsigned char* xi = img[ip % NS][0];
+      const unsigned char* yi = img[ip % NS][1];
+      const int nv = (int)min((int64_t)32, a.M - (t_lo + i) * 32);  // valid token rows of tile i
+      const bf16x8m d0 = __builtin_bit_cast(bf16x8m, dp0), d1 = __builtin_bit_cast(bf16x8m, dp1);
+      const bf16x8m g0 = __builtin_bit_cast(bf16x8m, gp0), g1 = __builtin_bit_cast(bf16x8m, gp1);
+      float gl = 0.f, dl = 0.f;
+      bf16x8m b0 = mlp_tr_frag<D>(xi, lane, 0, 0), b1 = mlp_tr_frag<D>(xi, lane, 1, 0);
+#pragma unroll
+      for (int k = 0; k < 2 * NT; ++k) {  // step k: output tile t = k / 2, half u = k % 2 (dW1, dW2^T)
+        const int t = k >> 1, u = k & 1, tn = t + 1 < NT ? t + 1 : t;
+        const unsigned char* nimg = u == 0 ? yi : xi;
+        const int nt_ = u == 0 ? t : tn;
+        const bf16x8m n0 = mlp_tr_frag<D>(nimg, lane, 0, nt_), n1 = mlp_tr_frag<D>(nimg, lane, 1, nt_);
+        if (u == 0) {
+          acc1[t] = mfma32(d0, b0, acc1[t]);
+          acc1[t] = mfma32(d1, b1, acc1[t]);
+        } else {
+          acc2[t] = mfma32(g0, b0, acc2[t]);
+          acc2[t] = mfma32(g1, b1, acc2[t]);
+        }
+        // GELU elements of tile i beside this step's MFMAs: 16 / (2 NT) per step (register e: token
+        // row 8 (e >> 2) + 4 h + (e & 3))
+        constexpr int EPS = 16 / (2 * NT);
+#pragma unroll
+        for (int ee = 0; ee < EPS; ++ee) {
+          const int e = k * EPS + ee;
+          float gd;
+          const float gg = gelu_tanh_and_grad(S[e] + bj, gd);
+          const bool ok = FULL || 8 * (e >> 2) + 4 * h + (e & 3) < nv;  // token rows past M
+          const float gk = ok ? gg : 0.f, dk = ok ? H[e] * gd : 0.f;
+          dbs += dk;
+          if (e & 1) {
+            uint32_t gw = pack_bf16x2(gl, gk), dw = pack_bf16x2(dl, dk);
+            // pins element e's VALU into this step's scheduling region, beside its MFMAs
+            asm volatile("" : "+v"(gw), "+v"(dw), "+v"(dbs)::"memory");
+            const int q = (e >> 1) & 3;
+            if (e < 8) {
+              gp0[q] = gw;
+              dp0[q] = dw;
+            } else {
+              gp1[q] = gw;
+              dp1[q] = dw;
+            }
+          } else {
+            gl = gk;
+            dl = dk;
+            asm volatile("" : "+v"(gl), "+v"(dl), "+v"(dbs)::"memory");
+          }
+        }
+        b0 = n0;
+        b1 = n1;
+      }
+    }
+    // ---- every wave is done with tile i - 1's slot; tile i + 1 landed everywhere
+    wait_vm<0>();
+    __syncthreads();
+    asm volatile("" ::: "memory");
+    if (i + 2 < nt) stage(t_lo + i + 2, (int)((i + 2) % NS));
+    // ---- phase A: S / dH of tile i + 1 (past the last tile: a stale slot, results unused)
+    phase_a(img[(i + 1) % NS][0], img[(i + 1) % NS][1]);
+  }
+  if (nt > 0) {  // phase B of the last tile
+    const unsigned char* xi = img[(nt - 1) % NS][0];
+    const unsigned char* yi = img[(nt - 1) % NS][1];
+    const bf16x8m d0 = __builtin_bit_cast(bf16x8m, dp0), d1 = __builtin_bit_cast(bf16x8m, dp1);
+    const bf16x8m g0 = __builtin_bit_cast(bf16x8m, gp0), g1 = __builtin_bit_cast(bf16x8m, gp1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc1[t] = mfma32(d0, mlp_tr_frag<D>(xi, lane, 0, t), acc1[t]);
+      acc1[t] = mfma32(d1, mlp_tr_frag<D>(xi, lane, 1, t), acc1[t]);
+      acc2[t] = mfma32(g0, mlp_tr_frag<D>(yi, lane, 0, t), acc2[t]);
+      acc2[t] = mfma32(g1, mlp_tr_frag<D>(yi, lane, 1, t), acc2[t]);
+    }
+  }
+  // partial slabs: register v of tile t is unit j0 + 8 (v >> 2) + 4 h + (v & 3), column 32 t + r32
+  float* p1 = a.dW1p + ((int64_t)slice * a.HID + j0) * D;
+  float* p2 = a.dW2Tp + ((int64_t)slice * a.HID + j0) * D;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t o = (int64_t)(8 * (v >> 2) + 4 * h + (v & 3)) * D + 32 * t + r32;
+      p1[o] = acc1[t][v];
+      p2[o] = acc2[t][v];
+    }
+  dbs += __shfl_xor(dbs, 32, 64);
+  if (a.db1p && h == 0) a.db1p[(int64_t)slice * a.HID + j0 + r32] = dbs;
+}
+
+// dW1 [HID][D] = sum over slices of dW1p; dW2 [D][HID] = (sum of dW2Tp)^T; db1 = sum of db1p --
+// the slices in order 0, 1, ... (deterministic).  One block per 32 x 32 (unit, column) tile;
+// the transposed dW2 goes out through an LDS tile.
+__global__ __launch_bounds__(256) void mlp_wgrad_fold_k(const float* __restrict__ dW1p, const float* __restrict__ dW2Tp,
+                                                        const float* __restrict__ db1p, int nslice, int HID, int D,
+                                                        float* __restrict__ dW1, float* __restrict__ dW2,
+                                                        float* __restrict__ db1) {
+  __shared__ float tl[32][33];
+  const int u0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows of 32 per pass
+  const int64_t sl = (int64_t)HID * D;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int u = u0 + ty + 8 * q;
+    const int64_t o = (int64_t)u * D + c0 + tx;
+    float s1 = 0.f, s2 = 0.f;
+    for (int s = 0; s < nslice; ++s) {
+      s1 += dW1p[s * sl + o];
+      s2 += dW2Tp[s * sl + o];
+    }
+    dW1[o] = s1;
+    tl[ty + 8 * q][tx] = s2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + ty + 8 * q;
+    dW2[(int64_t)c * HID + u0 + tx] = tl[tx][ty + 8 * q];
+  }
+  if (db1 && blockIdx.x == 0 && threadIdx.x < 32) {
+    float s = 0.f;
+    for (int sidx = 0; sidx < nslice; ++sidx) s += db1p[(int64_t)sidx * HID + u0 + threadIdx.x];
+    db1[u0 + threadIdx.x] = s;
   }
 }
 
@@ -859,8 +1311,89 @@ extern "C" int lthm_mlp_bwd(const void* X, const void* dY, int64_t M, int32_t D,
   constexpr int NW = 4;
   const int64_t ntiles = (M + 32 * NW - 1) / (32 * NW);
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());
-  if (D == 256) hipLaunchKernelGGL((mlp_bwd_k<256, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
-  else hipLaunchKernelGGL((mlp_bwd_k<128, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
+  if (D == 256) hipLaunchKernelGGL((mlp_bwd_k<256, NW, true>), dim3(grid), dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((mlp_bwd_k<128, NW, true>), dim3(grid), dim3(64 * NW), 0, s, a);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+// waves per weight-gradient workgroup (one per SIMD: the two [32 x D] sums are 2 D / 2 registers)
+constexpr int MLP_WG_NW = 4;
+
+static void mlp_wgrad_geometry(int64_t M, int D, int HID, int* nslice, int* ngroup) {
+  *ngroup = HID / (32 * MLP_WG_NW);
+  const int64_t ntile = (M + 31) / 32;
+  // one workgroup per CU: slices x groups ~ the CU count, at least one token tile per slice
+  int ns = std::max(1, mlp_cu_count() / std::max(1, *ngroup));
+  *nslice = (int)std::max<int64_t>(1, std::min<int64_t>(ns, ntile));
+  (void)D;
+}
+
+extern "C" int64_t lthm_mlp_wgrad_ws_bytes(int64_t M, int32_t D, int32_t HID) {
+  if (!lthm_mlp_supported(D, HID) || HID % (32 * MLP_WG_NW) || M < 0) return -1;
+  int ns, ng;
+  mlp_wgrad_geometry(M, D, HID, &ns, &ng);
+  return (int64_t)ns * HID * (2 * (int64_t)D + 1) * 4;
+}
+
+extern "C" int lthm_mlp_wgrad(const void* X, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                              const float* b1, const void* W2T, float* dW1, float* dW2, float* db1, void* workspace,
+                              int64_t ws_bytes, void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && HID % (32 * MLP_WG_NW) == 0 && M >= 0);
+  LTHM_REQUIRE(X && dY && W1 && W2T && dW1 && dW2 && workspace);
+  LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)dY % 16) == 0 && ((uintptr_t)W1 % 16) == 0 &&
+               ((uintptr_t)W2T % 16) == 0 && ((uintptr_t)workspace % 16) == 0);
+  LTHM_REQUIRE(ws_bytes >= lthm_mlp_wgrad_ws_bytes(M, D, HID));
+  hipStream_t s = (hipStream_t)stream;
+  int ns, ng;
+  mlp_wgrad_geometry(M, D, HID, &ns, &ng);
+  MlpWgArgs a{};
+  a.X = (const bf16_t*)X; a.dY = (const bf16_t*)dY; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1;
+  a.dW1p = (float*)workspace;
+  a.dW2Tp = a.dW1p + (int64_t)ns * HID * D;
+  a.db1p = db1 ? a.dW2Tp + (int64_t)ns * HID * D : nullptr;
+  a.M = M; a.HID = HID; a.nslice = ns; a.ngroup = ng;
+  if (M > 0) {
+    // every token tile full (M % 32 == 0, C2's 528,384 rows): no per-element row mask
+    const bool full = M % 32 == 0;
+    if (D == 256) {
+      if (full) hipLaunchKernelGGL((mlp_wgrad_k<256, MLP_WG_NW, true>), dim3(ns * ng), dim3(64 * MLP_WG_NW), 0, s, a);
+      else hipLaunchKernelGGL((mlp_wgrad_k<256, MLP_WG_NW, false>), dim3(ns * ng), dim3(64 * MLP_WG_NW), 0, s, a);
+    } else {
+      if (full) hipLaunchKernelGGL((mlp_wgrad_k<128, MLP_WG_NW, true>), dim3(ns * ng), dim3(64 * MLP_WG_NW), 0, s, a);
+      else hipLaunchKernelGGL((mlp_wgrad_k<128, MLP_WG_NW, false>), dim3(ns * ng), dim3(64 * MLP_WG_NW), 0, s, a);
+    }
+    LTHM_CHECK_LAUNCH();
+  } else {
+    LTHM_REQUIRE(hipMemsetAsync(workspace, 0, (size_t)lthm_mlp_wgrad_ws_bytes(M, D, HID), s) == hipSuccess);
+  }
+  hipLaunchKernelGGL(mlp_wgrad_fold_k, dim3(D / 32, HID / 32), dim3(256), 0, s, (const float*)a.dW1p,
+                     (const float*)a.dW2Tp, (const float*)a.db1p, ns, HID, D, dW1, dW2, db1);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_mlp_bwd_dx(const void* X, const void* dY, int64_t M, int32_t D, int32_t HID, const void* W1,
+                               const float* b1, const void* W2T, void* dX, int32_t dx_dtype, void* stream) {
+  LTHM_REQUIRE(lthm_mlp_supported(D, HID) && M >= 0);
+  LTHM_REQUIRE(X && dY && W1 && W2T && dX && (dx_dtype == LTHM_F32 || dx_dtype == LTHM_BF16));
+  LTHM_REQUIRE(((uintptr_t)X % 16) == 0 && ((uintptr_t)dY % 16) == 0 && ((uintptr_t)W1 % 16) == 0 &&
+               ((uintptr_t)W2T % 16) == 0 && ((uintptr_t)b1 % 16) == 0 && ((uintptr_t)dX % 16) == 0);
+  if (M == 0) return 0;
+  MlpBwdArgs a{};
+  a.X = (const bf16_t*)X; a.dY = (const bf16_t*)dY; a.W1 = (const bf16_t*)W1; a.W2T = (const bf16_t*)W2T;
+  a.b1 = b1;
+  a.dx_f32 = dx_dtype == LTHM_F32;
+  a.dXf = (float*)dX; a.dXb = (bf16_t*)dX;
+  a.M = M; a.HID = HID;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int NW = 4;
+  const int64_t ntiles = (M + 32 * NW - 1) / (32 * NW);
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());
+  LTHM_REQUIRE(HID <= 4096);
+  if (D == 256) hipLaunchKernelGGL((mlp_bwdx_k<256, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((mlp_bwdx_k<128, NW>), dim3(grid), dim3(64 * NW), 0, s, a);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

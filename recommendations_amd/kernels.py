@@ -592,6 +592,62 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
     return dx, g, dpre
 
 
+def mlp_wgrad_supported(D: int, HID: int) -> bool:
+    return mlp_supported(D, HID) and HID % 128 == 0 and HID <= 4096
+
+
+def mlp_bwd_dx(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
+    """dX of the fused MLP with the hidden recomputed and nothing else written
+    (lthm_mlp_bwd_dx): x2d / dy2d [M, D] bf16 -> dx [M, D] in dx_dtype."""
+    require_gpu(x2d, dy2d, w1_b, w2t_b)
+    M, D = x2d.shape
+    HID = w1_b.shape[0]
+    _check(x2d.dtype == torch.bfloat16 and dy2d.dtype == torch.bfloat16 and w1_b.dtype == torch.bfloat16
+           and w2t_b.dtype == torch.bfloat16, "mlp_bwd_dx takes bf16 x / dy / weights")
+    _check(mlp_supported(D, HID), f"fused MLP does not take D={D} HID={HID}")
+    _check(tuple(dy2d.shape) == (M, D) and tuple(w1_b.shape) == (HID, D) and tuple(w2t_b.shape) == (HID, D),
+           "mlp_bwd_dx: shapes")
+    for t in (x2d, dy2d, w1_b, w2t_b, b1):
+        _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_bwd_dx: contiguous aligned operands")
+    _check(b1 is None or (b1.dtype == torch.float32 and b1.numel() == HID), "mlp_bwd_dx: f32 b1")
+    dx = torch.empty((M, D), dtype=dx_dtype, device=x2d.device)
+    # compulsory HBM bytes: x, dy read, dx written
+    call("lthm_mlp_bwd_dx", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dx), dcode(dx),
+         stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd", _work=6.0 * M * D * HID,
+         _unit="flop", _bytes=float(M * D * (4 + dx.element_size())))
+    return dx
+
+
+def mlp_wgrad(x2d, dy2d, w1_b, b1, w2t_b, want_db1=True):
+    """Weight gradients of the fused MLP with the hidden recomputed in the kernel (lthm_mlp_wgrad):
+    -> (dW1 f32 [HID, D] = dP^T x, dW2 f32 [D, HID] = dY^T G, db1 f32 [HID] = colsum dP or None)."""
+    from ._lib import load
+    require_gpu(x2d, dy2d, w1_b, w2t_b)
+    M, D = x2d.shape
+    HID = w1_b.shape[0]
+    _check(x2d.dtype == torch.bfloat16 and dy2d.dtype == torch.bfloat16 and w1_b.dtype == torch.bfloat16
+           and w2t_b.dtype == torch.bfloat16, "mlp_wgrad takes bf16 x / dy / weights")
+    _check(mlp_wgrad_supported(D, HID), f"mlp_wgrad does not take D={D} HID={HID}")
+    _check(tuple(dy2d.shape) == (M, D) and tuple(w1_b.shape) == (HID, D) and tuple(w2t_b.shape) == (HID, D),
+           "mlp_wgrad: shapes")
+    for t in (x2d, dy2d, w1_b, w2t_b, b1):
+        _check(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0), "mlp_wgrad: contiguous aligned operands")
+    _check(b1 is None or (b1.dtype == torch.float32 and b1.numel() == HID), "mlp_wgrad: f32 b1")
+    dev = x2d.device
+    dw1 = torch.empty((HID, D), dtype=torch.float32, device=dev)
+    dw2 = torch.empty((D, HID), dtype=torch.float32, device=dev)
+    db1 = torch.empty(HID, dtype=torch.float32, device=dev) if want_db1 else None
+    wsb = int(load().lthm_mlp_wgrad_ws_bytes(M, D, HID))
+    _check(wsb >= 0, "mlp_wgrad: workspace size")
+    ws = _workspace(dev, wsb)
+    # compulsory HBM bytes: x and dy read, the two weight gradients written (f32)
+    call("lthm_mlp_wgrad", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dw1), ptr(dw2),
+         ptr(db1), ptr(ws), ws.numel() * 4, stream(),
+         _key=(_GEMM_TAG[-1] + ":mlp_wgrad") if _GEMM_TAG else "mlp_wgrad", _work=8.0 * M * D * HID, _unit="flop",
+         _bytes=float(M * D * 4 + 8 * HID * D))
+    return dw1, dw2, db1
+
+
 # ----------------------------------------------------------------- row gather
 def rows_gather(src2d, idx, out=None):
     """dst[i] = src2d[idx[i]] (a zero row where idx[i] < 0), idx int32 on the device, rows of a

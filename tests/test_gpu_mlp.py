@@ -168,3 +168,43 @@ def test_mlp_bwd_forms_agree(dev, split, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(g1, g2) and torch.equal(p1, p2)
     check("mlp bwd split vs fused dX", relerr(dx1.cpu(), dx2.cpu()), 1e-5)
+
+
+@pytest.mark.parametrize("M,D,HID,bias", [(4096, 256, 1024, True), (1000, 256, 1024, False), (257, 128, 512, True),
+                                          (33, 256, 128, True), (5, 256, 1024, True), (70001, 128, 512, True),
+                                          (528384 // 64 + 7, 256, 1024, True)])
+def test_mlp_bwd_no_hidden_vs_fp64(dev, M, D, HID, bias):
+    """The round-5 backward with no [M, HID] operand in HBM: lthm_mlp_bwd_dx (dX) and
+    lthm_mlp_wgrad (dW1, dW2, db1 with G / dP recomputed per token tile in the kernel, partial
+    slabs per token slice folded in order) against fp64 autograd on the same bf16 operands.
+    Bounds as the split backward's (dX and the weight gradients 1e-2: G / dP enter the MFMAs as
+    bf16); the weight gradients are also bit-identical across two runs (no atomics) and match
+    the round-4 chain (recompute kernel writing G / dP + the weight-gradient GEMM) to 1e-3 (the
+    same bf16 G / dP up to the odd rounding flip, summed in another order)."""
+    from recommendations_amd import kernels as K
+    x, w1, w2, b1, _, _, _ = _operands(M, D, HID, 13 * M + D + HID, bias)
+    g = torch.Generator().manual_seed(M + 3)
+    dy = torch.randn(M, D, generator=g).to(torch.bfloat16)
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    w2t = d(w2.T.contiguous())
+    dx = K.mlp_bwd_dx(d(x), d(dy), d(w1), d(b1), w2t, dx_dtype=torch.float32)
+    dw1, dw2, db1 = K.mlp_wgrad(d(x), d(dy), d(w1), d(b1), w2t, want_db1=bias)
+    dw1b, dw2b, db1b = K.mlp_wgrad(d(x), d(dy), d(w1), d(b1), w2t, want_db1=bias)
+    _, G, dP = K.mlp_bwd(d(x), d(dy), d(w1), d(b1), w2t)
+    dw1c, dw2c = K.linear_wgrad(dP, d(x)), K.linear_wgrad(d(dy), G)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw1b) and torch.equal(dw2, dw2b) and (db1 is None or torch.equal(db1, db1b))
+    check(f"mlp wgrad dW1 vs the G/dP chain ({M},{D},{HID})", relerr(dw1.cpu(), dw1c.cpu()), 1e-3)
+    check(f"mlp wgrad dW2 vs the G/dP chain ({M},{D},{HID})", relerr(dw2.cpu(), dw2c.cpu()), 1e-3)
+    xd = x.double().requires_grad_(True)
+    w1d = w1.double().requires_grad_(True)
+    w2d = w2.double().requires_grad_(True)
+    b1d = b1.double().requires_grad_(True) if b1 is not None else None
+    pre = xd @ w1d.T + (b1d if b1d is not None else 0.0)
+    y = F.gelu(pre, approximate="tanh") @ w2d.T
+    y.backward(dy.double())
+    check(f"mlp bwd_dx dX ({M},{D},{HID})", relerr(dx.cpu().double(), xd.grad), 1e-2)
+    check(f"mlp wgrad dW1 ({M},{D},{HID})", relerr(dw1.cpu().double(), w1d.grad), 1e-2)
+    check(f"mlp wgrad dW2 ({M},{D},{HID})", relerr(dw2.cpu().double(), w2d.grad), 1e-2)
+    if bias:
+        check(f"mlp wgrad db1 ({M},{D},{HID})", relerr(db1.cpu().double(), b1d.grad), 1e-2)

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--D", type=int, default=256)
     ap.add_argument("--bwd", action="store_true")
     ap.add_argument("--fused-only", action="store_true", help="time only the fused kernels (profiling)")
+    ap.add_argument("--only", default="", help="comma list of backward entries to time (profiling), e.g. bwd_dx,bwd_wgrad")
     args = ap.parse_args()
     from recommendations_amd import kernels as K
     dev = torch.device("cuda:0")
@@ -58,15 +59,38 @@ def main():
     if not args.fused_only:
         a, b = unfused(), fused()
         out["fwd_max_abs_diff"] = float((a - b).abs().max())
-    for name, fn in ((("unfused_fwd", unfused),) if not args.fused_only else ()) + (("fused_fwd", fused),):
+    only = set(filter(None, args.only.split(",")))
+    for name, fn in ((((("unfused_fwd", unfused),) if not args.fused_only else ()) + (("fused_fwd", fused),))
+                     if not only else ()):
         ms = timed(fn, args.iters)
         out[name] = {"ms": round(ms, 4), "TFLOP/s": round(fl / ms / 1e9, 1), "frac_bf16_peak": round(fl / ms / 1e9 / 2500, 4)}
-    if args.bwd and hasattr(K, "mlp_bwd"):
+    if (args.bwd or only) and hasattr(K, "mlp_bwd"):
         dy = torch.randn(M, D, device=dev, generator=g).to(bf)
         fl_b = 7.0 * 2 * M * D * HID  # executed (recompute 1 + dH 1 + dX 1 + dW 2 + recompute 2)
-        ms = timed(lambda: K.mlp_bwd(x, dy, w1, b1, w2t), args.iters)
-        out["fused_bwd"] = {"ms": round(ms, 4), "alg_TFLOP/s": round(8.0 * M * D * HID / ms / 1e9, 1),
-                            "exec_TFLOP/s": round(fl_b / ms / 1e9, 1)}
+        if not only:
+            ms = timed(lambda: K.mlp_bwd(x, dy, w1, b1, w2t), args.iters)
+            out["fused_bwd"] = {"ms": round(ms, 4), "alg_TFLOP/s": round(8.0 * M * D * HID / ms / 1e9, 1),
+                                "exec_TFLOP/s": round(fl_b / ms / 1e9, 1)}
+        u = 2.0 * M * D * HID  # one unit: a [M, D] x [D, HID] product
+
+        def chain4():  # round 4: G / dP written, dX GEMM, two weight-gradient GEMMs, db1 colsum
+            dx, G, dP = K.mlp_bwd(x, dy, w1, b1, w2t)
+            return dx, K.linear_wgrad(dP, x), K.linear_wgrad(dy, G), K.colsum(dP)
+
+        def chain5():  # round 5: dX and the weight gradients by two recompute kernels, nothing in HBM
+            return K.mlp_bwd_dx(x, dy, w1, b1, w2t), K.mlp_wgrad(x, dy, w1, b1, w2t)
+        for name, fn, parts in (("bwd_chain_r4", chain4, None),
+                                ("bwd_chain_r5", chain5, None),
+                                ("bwd_dx", lambda: K.mlp_bwd_dx(x, dy, w1, b1, w2t), 3.0),
+                                ("bwd_wgrad", lambda: K.mlp_wgrad(x, dy, w1, b1, w2t), 4.0)):
+            if only and name not in only:
+                continue
+            ms = timed(fn, args.iters)
+            e = {"ms": round(ms, 4), "alg_TFLOP/s": round(8.0 * M * D * HID / ms / 1e9, 1)}
+            if parts:
+                e["exec_TFLOP/s"] = round(parts * u / ms / 1e9, 1)
+                e["frac_bf16_peak"] = round(parts * u / ms / 1e9 / 2500, 4)
+            out[name] = e
     print(json.dumps(out))
 
 
