@@ -31,7 +31,7 @@ FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md 
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
 # the newest committed counter passes over the default (C2) bench
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_summary.json") for r in (4, 3))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_summary.json") for r in (5, 4, 3))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03_pmc_summary.json"))
 PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
     "cl_fr32_k": ["cl_fr32_k", "cl_fr32v_k"],

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 39 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 40 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -101,6 +101,16 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
                            int32_t dy_dtype, const void* out, int32_t out_dtype,
                            const float* norms, int64_t P, int32_t D, int32_t K, int32_t mode,
                            float* dW, int32_t* flags, int64_t* list, int64_t* count, void* stream);
+/* The K = 1, plain-output case of lthm_kshift_bwd_sparse (FlatEmbedding / table-batched flat
+ * lookups, the C4 ranker: commons/layers.py:56-61's nn.Embedding backward) with the rows of
+ * first touch STORED: the item whose flag exchange returned 0 writes its row of dW (no prior
+ * contents needed: rows are stored, not accumulated), every other item of a touched row is
+ * added afterwards with f32 atomics.  dup_ws: int64 [>= n * F + 1] workspace.  Same dW / flags /
+ * list / count result as lthm_kshift_bwd_sparse with K = 1, mode LTHM_KSHIFT_SCALE, up to the
+ * f32 summation order of duplicated rows. */
+int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                                 int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list, int64_t* count,
+                                 int64_t* dup_ws, int64_t dup_cap, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* GEMM: every nn.Linear on the path (commons/transformers/layers.py:240-241,   */
@@ -250,6 +260,18 @@ int lthm_layernorm_bwd(const void* dy, int32_t dy_dtype, const float* x, int64_t
 int lthm_layernorm_bwd_ex(const void* dy, int32_t dy_dtype, const float* x, int64_t M, int32_t D,
                           const float* w, const float* mean, const float* rstd, const float* res1,
                           const float* res2, float* dx, void* dx_bf16, float* partials, int32_t flags, void* stream);
+/* The input-gradient GEMM that feeds a LayerNorm backward, fused with it (round 5): dh = dy W
+ * (dy [M, K] bf16, wt = W^T [256, K] bf16, K % 64 == 0: the block's c_fc / c_attn dgrad,
+ * commons/transformers/layers.py:271-284 and :247-265) and then lthm_layernorm_bwd_ex over
+ * dh in f32 (layers.py:142-149): dx = LN'(dh) + res1 + res2 (+ res1 again with flags bit 0),
+ * its bf16 copy (dx_bf16 may be null), and per-tile weight / bias gradient partials
+ * (partials: f32 [2, lthm_dgrad_layernorm_bwd_tiles(M), 256], rows summed by the caller).
+ * D must be 256 (one column tile holds whole rows); 16-B aligned operands. */
+int lthm_dgrad_layernorm_bwd_tiles(int64_t M);
+int lthm_dgrad_layernorm_bwd(const void* dy, const void* wt, int64_t M, int32_t D, int64_t K,
+                             const float* x, const float* w, const float* mean, const float* rstd,
+                             const float* res1, const float* res2, float* dx, void* dx_bf16,
+                             float* partials, int32_t flags, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Attention with relative position bias + causal mask                       */

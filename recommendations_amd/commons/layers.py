@@ -463,6 +463,39 @@ class HistogramEmbedding(nn.Module):
         self.emb = nn.Embedding(nbins, emb_dim)
 
 
+class NAImputationPlusQuantileEmbedding(nn.Module):
+    """commons/layers.py:84-99 with the constructor fixed (off the LTHM path,
+    no HIP kernel: torch's bucketize and gather, on whatever device x lives).
+
+    As executed by the reference, the module cannot be built or called: the embedding table is
+    1-D (``nn.Embedding.from_pretrained`` needs 2-D), ``bucketize`` returns indices up to
+    len(quantiles) for a table of len(quantiles) - 1 rows, and ``torch.where`` broadcasts the
+    [..., ] mask against the [..., 1] rows.  Build-defined resolution:
+    - the table is the reference's initial values as a column, [len(quantiles) - 1, 1];
+    - the bucket index is the reference's ``bucketize(x, quantiles)`` clamped to the last row;
+    - the NA test is the reference's ``(x - na_value) < eps`` (one-sided, as written), applied
+      per value: out[..., 0] = na_param where it holds, else the bucket's row.
+    Output [..., 1] f32; gradients reach the table rows and na_param."""
+
+    def __init__(self, na_value, quantiles, eps=1e-6):
+        super().__init__()
+        self.na_value = na_value
+        self.register_buffer("quantiles", torch.tensor(quantiles))
+        n = len(quantiles)
+        if n < 2:
+            raise ValueError("NAImputationPlusQuantileEmbedding needs at least two quantiles")
+        init = (torch.arange(0, n - 1, 1) / n - 0.5).float().view(n - 1, 1)
+        self.emb = nn.Embedding.from_pretrained(init, freeze=False)
+        self.eps = eps
+        self.na_param = nn.Parameter(torch.zeros(1,))
+
+    def forward(self, x):
+        x = x.float()
+        idx = torch.bucketize(x, self.quantiles).clamp_(max=self.emb.num_embeddings - 1)
+        y = self.emb(idx)
+        return torch.where(((x - self.na_value) < self.eps).unsqueeze(-1), self.na_param.view(1), y)
+
+
 class QREmbedding(nn.Module):
     """commons/layers.py:102-123 with the constructor fixed:
     Wq[(x mod d^2) // d mod d] + Wr[x mod d]."""

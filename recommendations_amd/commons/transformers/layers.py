@@ -211,6 +211,9 @@ class TransformerBlockFn(torch.autograd.Function):
             dyb = K.cast(dym, torch.bfloat16)
         else:
             dym, dyb = dy, _grad_bf16(dy)
+        # dh2 = dpre W1 is produced inside ln_2's backward (K.dgrad_layernorm_bwd) where it takes
+        # the shapes; dh2 None until then
+        dh2 = None
         if ctx.fused_mlp:
             # saved: pre -> b1 (f32 or None), g -> c_proj.weight^T (bf16); the hidden is recomputed
             b1f, w2t_b = pre, g
@@ -218,7 +221,7 @@ class TransformerBlockFn(torch.autograd.Function):
                 dh2 = K.mlp_bwd_dx(h2, dyb, w1_b, b1f, w2t_b)
                 dw1, dw2, db1 = K.mlp_wgrad(h2, dyb, w1_b, b1f, w2t_b, want_db1=has_b1)
             else:
-                dh2, g, dpre = K.mlp_bwd(h2, dyb, w1_b, b1f, w2t_b)
+                dh2, g, dpre = K.mlp_bwd(h2, dyb, w1_b, b1f, w2t_b, want_dx=False)
                 dw2 = K.linear_wgrad(dyb, g)
                 dw1 = K.linear_wgrad(dpre, h2)
                 db1 = K.colsum(dpre) if has_b1 else None
@@ -229,13 +232,18 @@ class TransformerBlockFn(torch.autograd.Function):
             dpre = K.linear_dgrad(dyb, w2_b, act_grad=K.ACT_MUL_AUX, aux=pre)
             dw1 = K.linear_wgrad(dpre, h2)
             db1 = K.colsum(dpre) if has_b1 else None
-            dh2 = K.linear_dgrad(dpre, w1_b)
         # double residual, no residual dropout, no c_proj bias: ln_1's backward needs dx1 + dy only
         # (dx = LN1'(dh1) + dx1 + dy), so ln_2's backward writes that sum as its f32 output (the
         # bf16 copy, the attention branch's input, stays dx1): one f32 read less per element
         fold = _LN_FOLD and dbl and pr == 0.0 and not has_bp and d % 4 == 0
-        dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy, need_bias=has_ln1b,
-                                                  res1_twice=fold)
+        if dh2 is None and K.dgrad_layernorm_bwd_ok(dpre, w1_b, x1):
+            dx1, dx1b, dln2w, dln2b = K.dgrad_layernorm_bwd(dpre, w1_b, x1, ln2w.detach(), mu2, rs2, res1=dy,
+                                                            need_bias=has_ln1b, res1_twice=fold)
+        else:
+            if dh2 is None:
+                dh2 = K.linear_dgrad(dpre, w1_b)
+            dx1, dx1b, dln2w, dln2b = K.layernorm_bwd(dh2, x1, ln2w.detach(), mu2, rs2, res1=dy,
+                                                      need_bias=has_ln1b, res1_twice=fold)
         # attention half (dx1r: the gradient behind the residual dropout)
         if pr > 0.0:
             dx1r = K.dropout(dx1, pr, seed + 1)
@@ -259,9 +267,13 @@ class TransformerBlockFn(torch.autograd.Function):
             K.dropout_rows_(dqkv, 3, pa, seed)
         dwqkv = K.linear_wgrad(dqkv, h1)
         dbqkv = K.colsum(dqkv) if has_bqkv else None
-        dh1 = K.linear_dgrad(dqkv, wqkv_b)
-        dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1, need_bias=has_ln1b,
-                                                res2=dy if dbl and not fold else None)
+        if K.dgrad_layernorm_bwd_ok(dqkv, wqkv_b, x2):
+            dx, dxb, dln1w, dln1b = K.dgrad_layernorm_bwd(dqkv, wqkv_b, x2, ln1w.detach(), mu1, rs1, res1=dx1,
+                                                          need_bias=has_ln1b, res2=dy if dbl and not fold else None)
+        else:
+            dh1 = K.linear_dgrad(dqkv, wqkv_b)
+            dx, dxb, dln1w, dln1b = K.layernorm_bwd(dh1, x2, ln1w.detach(), mu1, rs1, res1=dx1,
+                                                    need_bias=has_ln1b, res2=dy if dbl and not fold else None)
         _stash_grad_bf16(dx, dxb)
         dtable = None
         if tshape is not None:

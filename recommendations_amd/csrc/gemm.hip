@@ -1164,6 +1164,24 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
 constexpr int PP_BK = 64;
 constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k bf16)
 
+// LayerNorm-backward epilogue of the N = 256 dgrad (round 5, lthm_dgrad_layernorm_bwd): the
+// tile's 256 rows of dh = dy W are whole LayerNorm rows, so the block finishes the LayerNorm
+// backward itself (layernorm.hip ln_bwd_v4_k's arithmetic on the f32 dh) instead of writing dh
+// as bf16 for a separate pass to re-read.
+struct LnbArgs {
+  const float* x;      // LayerNorm input [M, 256] f32
+  const float* w;      // LayerNorm weight [256]
+  const float* mean;   // [M]
+  const float* rstd;   // [M]
+  const float* res1;   // [M, 256] f32 or null
+  const float* res2;   // [M, 256] f32 or null
+  float* dx;           // [M, 256] f32
+  bf16_t* dxb;         // [M, 256] bf16 copy or null
+  float* dw_part;      // [tiles, 256] per-tile weight-gradient partials
+  float* db_part;      // [tiles, 256]
+  int res1_twice;      // the f32 dx carries res1 once more than the bf16 copy
+};
+
 
 // F8: A and B are e4m3 bytes with K and the leading dims in 2-byte units (a K-tile row is 128 k
 // of fp8): one v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per fragment pair and
@@ -1172,8 +1190,8 @@ constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k 
 // SPREAD: the next K-tile's four half images are issued one per quadrant phase (2 DMAs each)
 // instead of all eight DMAs behind the barrier (bf16: C4 forms 4-6 % faster; the fp8 form ran
 // 3x slower so, and raising the MFMA phases' wave priority lost 5-7 %, profiles/r04ab/)
-template <bool F8, bool SPREAD = false>
-__global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n) {
+template <bool F8, bool SPREAD = false, bool LNB = false>
+__global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n, LnbArgs L = LnbArgs{}) {
   __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * PP_HALF];  // [buf][A0, A1, B0, B1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nblk = tiles_m * tiles_n;
@@ -1295,6 +1313,105 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if constexpr (LNB) {
+    // 128 rows x 256 f32 per half (rows 64 hb .. of both row waves), column c of row t at
+    // c ^ (((t >> 2) & 3) << 4): the accumulator stores (16 consecutive columns x 4 row groups
+    // per instruction) hit 64 distinct banks, the row reads stay 16-B contiguous
+    float* T = reinterpret_cast<float*>(sh);
+    const int c = lane * 4;
+    float wg[4], dwa[4] = {0.f, 0.f, 0.f, 0.f}, dba[4] = {0.f, 0.f, 0.f, 0.f};
+    load_vec<float, 16>(L.w + c, wg);
+    const float alpha = g.alpha;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = wr * 64 + 16 * i + 4 * c4 + r, col = wc * 64 + 16 * j + r16;
+            T[t * 256 + (col ^ (((t >> 2) & 3) << 4))] = acc[4 * hb + i][j][r] * alpha;
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // wave w: staged rows 16 w .. 16 w + 15, four rows' loads in flight at a time
+#pragma unroll 1
+      for (int q0 = 0; q0 < 16; q0 += 4) {
+        float xv[4][4], r1[4][4], r2[4][4], mu[4], rs[4];
+        int64_t grow[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = wave * 16 + q0 + u;
+          grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
+          const bool ok = grow[u] < g.M;
+          const int64_t gr = ok ? grow[u] : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { r1[u][e] = 0.f; r2[u][e] = 0.f; }
+          load_vec<float, 16>(L.x + gr * 256 + c, xv[u]);
+          if (L.res1) load_vec<float, 16>(L.res1 + gr * 256 + c, r1[u]);
+          if (L.res2) load_vec<float, 16>(L.res2 + gr * 256 + c, r2[u]);
+          mu[u] = L.mean[gr];
+          rs[u] = L.rstd[gr];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = wave * 16 + q0 + u;
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
+          const float d[4] = {d4.x, d4.y, d4.z, d4.w};
+          float gg[4], xh[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xh[e] = (xv[u][e] - mu[u]) * rs[u];
+            gg[e] = d[e] * wg[e];
+            s1 += gg[e];
+            s2 += gg[e] * xh[e];
+          }
+          s1 = wave_sum(s1) / 256.f;
+          s2 = wave_sum(s2) / 256.f;
+          if (grow[u] < g.M) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              dwa[e] += d[e] * xh[e];
+              dba[e] += d[e];
+              o[e] = rs[u] * (gg[e] - s1 - xh[e] * s2) + r1[u][e] + r2[u][e];
+            }
+            if (L.dxb) store_vec<bf16_t, 4>(L.dxb + grow[u] * 256 + c, o);
+            if (L.res1_twice) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] += r1[u][e];
+            }
+            store_vec<float, 4>(L.dx + grow[u] * 256 + c, o);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    // per-tile weight-gradient partials: the 8 waves' column sums in a fixed order
+    const int tile = lid / tiles_n;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const float* src = pass ? dba : dwa;
+      *reinterpret_cast<f32x4*>(T + wave * 256 + c) = f32x4{src[0], src[1], src[2], src[3]};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (tid < 256) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) sacc += T[v * 256 + tid];
+        (pass ? L.db_part : L.dw_part)[(int64_t)tile * 256 + tid] = sacc;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
   // each wave's 128 x 64 block in two 64-row halves through its 16-KiB slice of the buffers
   // (column groups of 16 XOR-rotated by row / 4: conflict-free stores), then a row loop with the
   // generic epilogue (one copy of its code: the accumulator indices stay static)
@@ -1385,6 +1502,32 @@ static int lthm_gemm_pp_f8() {
     mode = (e && e[0] == '0') ? 0 : 1;
   }
   return mode;
+}
+
+extern "C" int lthm_dgrad_layernorm_bwd_tiles(int64_t M) { return (int)((M + 255) / 256); }
+
+extern "C" int lthm_dgrad_layernorm_bwd(const void* dy, const void* wt, int64_t M, int32_t D, int64_t K,
+                                        const float* x, const float* w, const float* mean, const float* rstd,
+                                        const float* res1, const float* res2, float* dx, void* dx_bf16,
+                                        float* partials, int32_t flags, void* stream) {
+  LTHM_REQUIRE(D == 256 && M >= 0 && K > 0 && K % PP_BK == 0 && (flags & ~1) == 0);
+  LTHM_REQUIRE(dy && wt && x && w && mean && rstd && dx && partials && (!(flags & 1) || res1));
+  auto al16 = [](const void* p) { return ((uintptr_t)p % 16) == 0; };
+  LTHM_REQUIRE(al16(dy) && al16(wt) && al16(x) && al16(w) && al16(dx) && al16(partials) && (!res1 || al16(res1)) &&
+               (!res2 || al16(res2)) && ((uintptr_t)dx_bf16 % 8) == 0);
+  if (M == 0) return 0;
+  GemmArgs g{};
+  g.A = (const bf16_t*)dy; g.B = (const bf16_t*)wt; g.C = nullptr;
+  g.M = M; g.N = 256; g.K = K;
+  g.lda = K; g.ldb = K; g.ldc = 256;
+  g.alpha = 1.f;
+  g.act = LTHM_ACT_NONE;
+  g.fast_ok = true;
+  const int tm = lthm_dgrad_layernorm_bwd_tiles(M);
+  LnbArgs L{x, w, mean, rstd, res1, res2, dx, (bf16_t*)dx_bf16, partials, partials + (int64_t)tm * 256, flags & 1};
+  hipLaunchKernelGGL((gemm_pp_k<false, false, true>), dim3(tm), dim3(512), 0, (hipStream_t)stream, g, tm, 1, L);
+  LTHM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int lthm_gemm(const lthm_gemm_desc* d, void* stream) {

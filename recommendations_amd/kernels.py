@@ -561,9 +561,11 @@ def mlp_fwd_ln(x32, ln_w, ln_b, w1_b, b1, w2t_b, b2, res1=None, res2=None, save=
 _MLP_BWD_SPLIT = os.environ.get("LTHM_MLP_BWD", "split") != "fused"
 
 
-def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
+def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16, want_dx=True):
     """Backward of the fused MLP with the hidden recomputed (lthm_mlp_bwd): -> (dx [M, D],
-    g [M, HID] = GELU(pre) bf16, dpre [M, HID] bf16).  x2d / dy2d [M, D] bf16."""
+    g [M, HID] = GELU(pre) bf16, dpre [M, HID] bf16).  x2d / dy2d [M, D] bf16.  want_dx=False:
+    dx is None where the split path would run dX = dpre W1 on the GEMM (the caller runs it, e.g.
+    fused with the LayerNorm backward: dgrad_layernorm_bwd)."""
     require_gpu(x2d, dy2d, w1_b, w2t_b)
     M, D = x2d.shape
     HID = w1_b.shape[0]
@@ -584,7 +586,7 @@ def mlp_bwd(x2d, dy2d, w1_b, b1, w2t_b, dx_dtype=torch.bfloat16):
         call("lthm_mlp_bwd_hidden", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(g), ptr(dpre),
              stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd", _work=4.0 * M * D * HID,
              _unit="flop", _bytes=float(M * (4 * D + 4 * HID)))
-        return linear_dgrad(dpre, w1_b, out_dtype=dx_dtype), g, dpre
+        return (linear_dgrad(dpre, w1_b, out_dtype=dx_dtype) if want_dx else None), g, dpre
     dx = torch.empty((M, D), dtype=dx_dtype, device=dev)
     call("lthm_mlp_bwd", ptr(x2d), ptr(dy2d), M, D, HID, ptr(w1_b), ptr(b1), ptr(w2t_b), ptr(dx), dcode(dx),
          ptr(g), ptr(dpre), stream(), _key=(_GEMM_TAG[-1] + ":mlp_bwd") if _GEMM_TAG else "mlp_bwd",
@@ -688,6 +690,55 @@ def layernorm_fwd(x2d, w, b, y_dtype=torch.bfloat16, amax=None):
         call("lthm_layernorm_fwd", ptr(x2d), M, D, ptr(w), ptr(b), ptr(y), dcode(y), ptr(mean), ptr(rstd), stream(),
              _work=nb, _unit="byte")
     return y, mean, rstd
+
+
+def dgrad_layernorm_bwd_ok(dy2d, w_bf16, x2d) -> bool:
+    """Shapes lthm_dgrad_layernorm_bwd takes: LayerNorm width 256 (one column tile of whole
+    rows), the dgrad's reduction dim a multiple of 64, 16-B aligned contiguous operands."""
+    M, N = dy2d.shape
+    return (_LN_DGRAD and x2d.shape[1] == 256 and tuple(w_bf16.shape) == (N, 256) and N % 64 == 0
+            and dy2d.dtype == torch.bfloat16 and w_bf16.dtype == torch.bfloat16 and x2d.dtype == torch.float32
+            and dy2d.is_contiguous() and x2d.is_contiguous() and dy2d.data_ptr() % 16 == 0
+            and x2d.data_ptr() % 16 == 0 and x2d.shape[0] == M)
+
+
+def dgrad_layernorm_bwd(dy2d, w_bf16, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True,
+                        res1_twice=False):
+    """layernorm_bwd(linear_dgrad(dy2d, w_bf16), x2d, ...) in one kernel (lthm_dgrad_layernorm_bwd):
+    dh = dy W stays on chip (f32) and the 256-row GEMM tiles finish the LayerNorm backward.
+    -> (dx f32, dx bf16 or None, dw, db or None)."""
+    from ._lib import load
+    require_gpu(dy2d, w_bf16, x2d)
+    _check(dgrad_layernorm_bwd_ok(dy2d, w_bf16, x2d), "dgrad_layernorm_bwd: unsupported shapes")
+    M, N = dy2d.shape
+    D = 256
+    for t, nm in ((res1, "res1"), (res2, "res2")):
+        _need(t, M * D, nm)
+        _check(t is None or (t.dtype == torch.float32 and t.data_ptr() % 16 == 0), f"{nm}: 16-B aligned f32")
+    _need(w, D, "ln weight")
+    _check(w.dtype == torch.float32 and w.data_ptr() % 16 == 0, "ln weight: 16-B aligned f32")
+    _need(mean, M, "mean")
+    _need(rstd, M, "rstd")
+    _check(not res1_twice or res1 is not None, "dgrad_layernorm_bwd(res1_twice) needs res1")
+    wt = w_bf16.t().contiguous()
+    tiles = int(load().lthm_dgrad_layernorm_bwd_tiles(M))
+    part = torch.empty((2, tiles, D), dtype=torch.float32, device=x2d.device)
+    dx = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
+    dxb = torch.empty((M, D), dtype=torch.bfloat16, device=x2d.device) if want_bf16 else None
+    # compulsory HBM bytes: dy read, x and the residuals read, dx (and its bf16 copy) written
+    nb = float(M * N * 2 + M * D * (4 + 4 + (4 if res1 is not None else 0) + (4 if res2 is not None else 0)
+                                    + (2 if want_bf16 else 0)) + 8 * M)
+    call("lthm_dgrad_layernorm_bwd", ptr(dy2d), ptr(wt), M, D, N, ptr(x2d), ptr(w), ptr(mean), ptr(rstd), ptr(res1),
+         ptr(res2), ptr(dx), ptr(dxb), ptr(part), 1 if res1_twice else 0, stream(),
+         _key=(_GEMM_TAG[-1] + ":dgrad_ln") if _GEMM_TAG else "dgrad_ln", _work=2.0 * M * N * D, _unit="flop",
+         _bytes=nb)
+    dw = colsum(part[0])
+    db = colsum(part[1]) if need_bias else None
+    return dx, dxb, dw, db
+
+
+# LTHM_LN_DGRAD=0: the dgrad GEMM writes dh (bf16) and the LayerNorm backward runs as its own pass
+_LN_DGRAD = os.environ.get("LTHM_LN_DGRAD", "1") != "0"
 
 
 def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True, res1_twice=False):
@@ -846,6 +897,11 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=
 
 
 # ----------------------------------------------------------------- sparse KShift backward
+# LTHM_KSHIFT_FIRST=0 keeps the all-atomic K = 1 table backward (A/B switch)
+_KSHIFT_FIRST = os.environ.get("LTHM_KSHIFT_FIRST", "1") != "0"
+_dup_ws = {}
+
+
 def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0):
     """Accumulate into dense dW and append the touched rows (see include/lthm.h).
     Table-batched layout: dW and flags cover all F*P rows; rows_list must hold
@@ -859,6 +915,15 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
     _check(rows_list.dtype == torch.int64 and rows_list.numel() >= cap, f"rows_list must be int64 with >= {cap} entries")
     _check(count.dtype == torch.int64 and count.numel() >= 1, "count must be an int64 scalar buffer")
     n = ids.numel() // F
+    if _KSHIFT_FIRST and K == 1 and mode != KSHIFT_NORMALIZE and D <= 64 and 64 % D == 0 and ids.numel():
+        # first-touch rows stored, repeats added afterwards (lthm_kshift_bwd_sparse_first)
+        ws = _dup_ws.get(ids.device)
+        if ws is None or ws.numel() < ids.numel() + 1:
+            ws = torch.empty(ids.numel() + 1, dtype=torch.int64, device=ids.device)
+            _dup_ws[ids.device] = ws
+        call("lthm_kshift_bwd_sparse_first", ptr(ids), n, F, ptr(gy), dcode(gy), P, D, ptr(dW), ptr(flags),
+             ptr(rows_list), ptr(count), ptr(ws), ws.numel(), stream())
+        return
     call("lthm_kshift_bwd_sparse", ptr(ids), n, F, ptr(gy), dcode(gy),
          ptr(out) if out is not None else None, dcode(out) if out is not None else F32, ptr(norms),
          P, D, K, mode, ptr(dW), ptr(flags), ptr(rows_list), ptr(count), stream())

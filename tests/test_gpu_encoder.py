@@ -571,3 +571,49 @@ def test_attn_mask_errors(dev):
         K.attn_mask_operand(torch.zeros(3, 5, 7, device=dev), 2, 1, 7)
     with pytest.raises(RuntimeError):  # general masks: T <= 256
         K.attn_mask_operand(torch.zeros(300, 300, device=dev), 1, 1, 300)
+
+
+@pytest.mark.parametrize("M,N,res,twice", [(2048, 1024, 2, False), (1000, 768, 1, True), (257, 512, 0, False),
+                                           (5, 64, 1, False), (33000, 1024, 1, True)])
+def test_dgrad_layernorm_bwd_vs_fp64(dev, M, N, res, twice):
+    """lthm_dgrad_layernorm_bwd (the c_fc / c_attn dgrad fused with the LayerNorm backward,
+    commons/transformers/layers.py:142-149, :271-284) against fp64 on the same bf16 operands:
+    dh = dy W, dx = LN'(dh) + res1 + res2 (+ res1 with the fold flag), dw = sum dh xhat,
+    db = sum dh.  dh stays f32 on chip: 1e-5 relative Frobenius on dx (f32 accumulation
+    order), 1e-5 on dw / db; the bf16 copy 4e-3 (bf16 rounding).  Also against the unfused
+    pair (bf16 dh), within the bf16 rounding of dh."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + N + res)
+    dy = bf(torch.randn(M, N, generator=g))
+    W = bf(torch.randn(N, 256, generator=g) / math.sqrt(N))
+    x = torch.randn(M, 256, generator=g) * 2 + 0.5
+    w = torch.randn(256, generator=g) * 0.5 + 1
+    mu = x.double().mean(1)
+    rs = 1.0 / torch.sqrt(x.double().var(1, unbiased=False) + 1e-5)
+    r1 = torch.randn(M, 256, generator=g) if res >= 1 else None
+    r2 = torch.randn(M, 256, generator=g) if res >= 2 else None
+    d = lambda t: None if t is None else t.to(dev)
+    assert K.dgrad_layernorm_bwd_ok(d(dy), d(W), d(x))
+    dx, dxb, dw, db = K.dgrad_layernorm_bwd(d(dy), d(W), d(x), d(w), d(mu.float()), d(rs.float()), res1=d(r1),
+                                            res2=d(r2), res1_twice=twice)
+    torch.cuda.synchronize()
+    dh = dy.double() @ W.double()
+    xh = (x.double() - mu[:, None]) * rs[:, None]
+    gg = dh * w.double()
+    want = rs[:, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+    if r1 is not None:
+        want = want + r1.double()
+    if r2 is not None:
+        want = want + r2.double()
+    check("dx bf16 copy", relerr(dxb.float(), want), 4e-3)
+    if twice:
+        want = want + r1.double()
+    check("dx", relerr(dx, want), 1e-5)
+    check("dw", relerr(dw, (dh * xh).sum(0)), 1e-5)
+    check("db", relerr(db, dh.sum(0)), 1e-5)
+    # the unfused pair: bf16 dh written by the GEMM, then lthm_layernorm_bwd_ex
+    dh_b = K.linear_dgrad(d(dy), d(W))
+    ux, _, uw, ub = K.layernorm_bwd(dh_b, d(x), d(w), d(mu.float()), d(rs.float()), res1=d(r1), res2=d(r2),
+                                    res1_twice=twice)
+    check("dx vs unfused", relerr(dx, ux), 4e-3)
+    check("dw vs unfused", relerr(dw, uw), 4e-3)

@@ -191,6 +191,50 @@ def test_kshift_sparse_touched_rows(dev, P, D, Kk, F, n):
     assert fl[want].all() and fl.sum() == len(want)
 
 
+@pytest.mark.parametrize("first", [True, False])
+@pytest.mark.parametrize("P,D,F,n,dt", [(5000, 64, 1, 20000, torch.bfloat16), (100000, 16, 3, 7001, torch.float32),
+                                        (64, 32, 2, 1, torch.bfloat16), (300, 64, 4, 9000, torch.float32)])
+def test_kshift_sparse_k1_accumulates(dev, first, P, D, F, n, dt):
+    """K = 1 table backward (commons/layers.py:56-61's nn.Embedding backward over the C4
+    ranker's tables): lthm_kshift_bwd_sparse_first (first touch stored, repeats added) and the
+    all-atomic lthm_kshift_bwd_sparse give the fp64 per-row sums, the touched rows once in the
+    list, across two backward calls (the second over rows already flagged, gradient
+    accumulation).  f32 sums in a different order: 1e-5 of the row's |dY| mass."""
+    from oracle.ref import kshift_rows
+    old = K._KSHIFT_FIRST
+    K._KSHIFT_FIRST = first
+    try:
+        g = np.random.default_rng(P + n + D)
+        dW = torch.zeros((F * P, D), dtype=torch.float32, device=dev)
+        flags = torch.zeros(F * P, dtype=torch.int32, device=dev)
+        lst = torch.zeros(F * P, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        want = np.zeros((F * P, D))
+        mag = np.zeros((F * P, D))
+        pending = 0
+        for call in range(2):
+            ids = g.integers(-2**63, 2**63 - 1, size=(n, F), dtype=np.int64)
+            ids[: n // 5] = ids[n // 5]  # a hot row per feature
+            dy = torch.randn((n, F, D), dtype=torch.float32).to(dt)
+            K.kshift_bwd_sparse(torch.from_numpy(ids).to(dev), dy.to(dev), None, None, P, 1, 0, F, dW, flags, lst, cnt,
+                                pending=pending)
+            pending += n * F
+            rows = kshift_rows(ids.reshape(-1), P, 1).reshape(-1) + np.tile(np.arange(F) * P, n)
+            d64 = dy.double().numpy().reshape(-1, D)
+            np.add.at(want, rows, d64)
+            np.add.at(mag, rows, np.abs(d64))
+        torch.cuda.synchronize()
+        got = dW.double().cpu().numpy()
+        assert np.all(np.abs(got - want) <= 1e-5 * (mag + 1e-30))
+        touched = np.flatnonzero(mag.sum(1) > 0)
+        c = int(cnt.item())
+        np.testing.assert_array_equal(np.sort(lst[:c].cpu().numpy()), touched)
+        fl = flags.cpu().numpy()
+        assert fl[touched].all() and fl.sum() == len(touched)
+    finally:
+        K._KSHIFT_FIRST = old
+
+
 @pytest.mark.parametrize("Dout", [64, 256, 512])
 def test_product_tower_fwd_vs_oracle(dev, Dout):
     """ProductTower.forward (product_tower.py:43-62): norm mask, normalise, emb_mapper,
