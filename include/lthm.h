@@ -268,6 +268,13 @@ int lthm_layernorm_bwd_ex(const void* dy, int32_t dy_dtype, const float* x, int6
  * (partials: f32 [2, lthm_dgrad_layernorm_bwd_tiles(M), 256], rows summed by the caller).
  * D must be 256 (one column tile holds whole rows); 16-B aligned operands. */
 int lthm_dgrad_layernorm_bwd_tiles(int64_t M);
+/* The block's c_proj forward and ln_2 in one kernel (round 5): x1 = res1 + x W^T + bias
+ * (x [M, K] bf16, W [256, K] bf16 = nn.Linear weight, K % 64 == 0; transformers/layers.py:
+ * 264 + the residual of :371) written in f32, then lthm_layernorm_fwd of x1 (layers.py:142-149,
+ * eps 1e-5): h bf16 [M, 256], mean / rstd [M].  bias / res1 / ln_b may be null. */
+int lthm_linear_layernorm_fwd(const void* x, const void* w, const float* bias, const float* res1, int64_t M,
+                              int32_t D, int64_t K, const float* ln_w, const float* ln_b, float* x1,
+                              void* h, float* mean, float* rstd, void* stream);
 int lthm_dgrad_layernorm_bwd(const void* dy, const void* wt, int64_t M, int32_t D, int64_t K,
                              const float* x, const float* w, const float* mean, const float* rstd,
                              const float* res1, const float* res2, float* dx, void* dx_bf16,

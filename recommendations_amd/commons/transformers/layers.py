@@ -149,9 +149,14 @@ class TransformerBlockFn(torch.autograd.Function):
         ctx.pack, ctx.o_full = pack, o_f
         if fp8:
             K.amax_(o, am[1:2])
+        ln2_done = None  # (h2, mu2, rs2) when ln_2 ran inside the c_proj GEMM
         if pr > 0.0:
             x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None), pr,
                            seed + 1, res1=x2)
+        elif not fp8 and not _MLP_LN and K.linear_layernorm_fwd_ok(o, wp_b):
+            # c_proj + residual, then ln_2, in one kernel (its 256-row tiles hold whole rows)
+            x1, h2f, mu2f, rs2f = K.linear_layernorm_fwd(o, wp_b, _f(bp), x2, ln2w.detach(), _f(ln2b))
+            ln2_done = (h2f, mu2f, rs2f)
         else:
             x1 = lin(o, wp_b, _f(bp), res1=x2, out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None)
         if not fp8 and pr == 0.0 and K.mlp_supported(d, w1.shape[0]) and (infer or _MLP_TRAIN):
@@ -162,7 +167,7 @@ class TransformerBlockFn(torch.autograd.Function):
                 out, h2, mu2, rs2 = K.mlp_fwd_ln(x1, ln2w.detach(), _f(ln2b), w1_b, _f(b1), w2t_b, _f(b2), res1=x1,
                                                  res2=x2 if double_residual else None, save=not infer)
             else:
-                h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
+                h2, mu2, rs2 = ln2_done or K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b))
                 out = K.mlp_fwd(h2, w1_b, _f(b1), w2t_b, _f(b2), res1=x1, res2=x2 if double_residual else None)
             if infer:
                 return out if pack is not None else out.view(B, T, d)
@@ -173,7 +178,7 @@ class TransformerBlockFn(torch.autograd.Function):
             ctx.mop = mop
             ctx.fused_mlp = True
             return out if pack is not None else out.view(B, T, d)
-        h2, mu2, rs2 = K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
+        h2, mu2, rs2 = ln2_done or K.layernorm_fwd(x1, ln2w.detach(), _f(ln2b), amax=am[2:3] if fp8 else None)
         # pre holds GELU'(c_fc x) (bf16): the backward epilogue is then one multiply
         pre = torch.empty((M, w1.shape[0]), dtype=torch.bfloat16, device=x.device)
         if fp8:

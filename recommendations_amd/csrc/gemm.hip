@@ -1164,22 +1164,31 @@ __global__ __launch_bounds__(512, 1) void gemm_bt_k(GemmArgs g, int tiles_m, int
 constexpr int PP_BK = 64;
 constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k bf16)
 
-// LayerNorm-backward epilogue of the N = 256 dgrad (round 5, lthm_dgrad_layernorm_bwd): the
-// tile's 256 rows of dh = dy W are whole LayerNorm rows, so the block finishes the LayerNorm
-// backward itself (layernorm.hip ln_bwd_v4_k's arithmetic on the f32 dh) instead of writing dh
-// as bf16 for a separate pass to re-read.
+// LayerNorm epilogues of the N = 256 GEMMs (round 5): a 256 x 256 tile holds whole rows of a
+// d = 256 LayerNorm, so the block finishes the LayerNorm itself instead of writing the GEMM
+// output for a separate pass to re-read.
+//  * PP_LNB (lthm_dgrad_layernorm_bwd): dh = dy W stays f32 on chip, then layernorm.hip
+//    ln_bwd_v4_k's arithmetic: dx (+ residuals), its bf16 copy, per-tile dw / db partials;
+//  * PP_LNF (lthm_linear_layernorm_fwd): x1 = res1 + o W^T + bias is written (f32) and
+//    ln_fwd_v4_k's arithmetic (two-pass statistics, the same lane layout) gives the bf16
+//    LayerNorm output and the row statistics.
+constexpr int PP_PLAIN = 0, PP_LNB = 1, PP_LNF = 2;
 struct LnbArgs {
-  const float* x;      // LayerNorm input [M, 256] f32
+  const float* x;      // LNB: LayerNorm input [M, 256] f32
   const float* w;      // LayerNorm weight [256]
-  const float* mean;   // [M]
-  const float* rstd;   // [M]
-  const float* res1;   // [M, 256] f32 or null
-  const float* res2;   // [M, 256] f32 or null
-  float* dx;           // [M, 256] f32
-  bf16_t* dxb;         // [M, 256] bf16 copy or null
-  float* dw_part;      // [tiles, 256] per-tile weight-gradient partials
-  float* db_part;      // [tiles, 256]
-  int res1_twice;      // the f32 dx carries res1 once more than the bf16 copy
+  const float* mean;   // LNB: [M] (read)
+  const float* rstd;   // LNB: [M] (read)
+  const float* res1;   // [M, 256] f32 or null (LNF: the residual added before the LayerNorm)
+  const float* res2;   // LNB: [M, 256] f32 or null
+  float* dx;           // LNB: [M, 256] f32;  LNF: x1 [M, 256] f32
+  bf16_t* dxb;         // LNB: [M, 256] bf16 copy or null;  LNF: the LayerNorm output [M, 256] bf16
+  float* dw_part;      // LNB: [tiles, 256] per-tile weight-gradient partials
+  float* db_part;      // LNB: [tiles, 256]
+  int res1_twice;      // LNB: the f32 dx carries res1 once more than the bf16 copy
+  const float* b;      // LNF: LayerNorm bias [256] or null
+  const float* bias;   // LNF: the linear layer's bias [256] or null
+  float* mean_out;     // LNF: [M]
+  float* rstd_out;     // LNF: [M]
 };
 
 
@@ -1190,7 +1199,7 @@ struct LnbArgs {
 // SPREAD: the next K-tile's four half images are issued one per quadrant phase (2 DMAs each)
 // instead of all eight DMAs behind the barrier (bf16: C4 forms 4-6 % faster; the fp8 form ran
 // 3x slower so, and raising the MFMA phases' wave priority lost 5-7 %, profiles/r04ab/)
-template <bool F8, bool SPREAD = false, bool LNB = false>
+template <bool F8, bool SPREAD = false, int EPX = PP_PLAIN>
 __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int tiles_n, LnbArgs L = LnbArgs{}) {
   __shared__ __attribute__((aligned(16))) unsigned char sh[2 * 4 * PP_HALF];  // [buf][A0, A1, B0, B1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1313,7 +1322,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if constexpr (LNB) {
+  if constexpr (EPX != PP_PLAIN) {
     // 128 rows x 256 f32 per half (rows 64 hb .. of both row waves), column c of row t at
     // c ^ (((t >> 2) & 3) << 4): the accumulator stores (16 consecutive columns x 4 row groups
     // per instruction) hit 64 distinct banks, the row reads stay 16-B contiguous
@@ -1336,54 +1345,107 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      // wave w: staged rows 16 w .. 16 w + 15, four rows' loads in flight at a time
+      if constexpr (EPX == PP_LNF) {
+        float lb[4] = {0.f, 0.f, 0.f, 0.f}, bb[4] = {0.f, 0.f, 0.f, 0.f};
+        if (L.b) load_vec<float, 16>(L.b + c, lb);
+        if (L.bias) load_vec<float, 16>(L.bias + c, bb);
 #pragma unroll 1
-      for (int q0 = 0; q0 < 16; q0 += 4) {
-        float xv[4][4], r1[4][4], r2[4][4], mu[4], rs[4];
-        int64_t grow[4];
+        for (int q0 = 0; q0 < 16; q0 += 4) {
+          float r1[4][4];
+          int64_t grow[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int t = wave * 16 + q0 + u;
-          grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
-          const bool ok = grow[u] < g.M;
-          const int64_t gr = ok ? grow[u] : 0;
+          for (int u = 0; u < 4; ++u) {
+            const int t = wave * 16 + q0 + u;
+            grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
+            const int64_t gr = grow[u] < g.M ? grow[u] : 0;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { r1[u][e] = 0.f; r2[u][e] = 0.f; }
-          load_vec<float, 16>(L.x + gr * 256 + c, xv[u]);
-          if (L.res1) load_vec<float, 16>(L.res1 + gr * 256 + c, r1[u]);
-          if (L.res2) load_vec<float, 16>(L.res2 + gr * 256 + c, r2[u]);
-          mu[u] = L.mean[gr];
-          rs[u] = L.rstd[gr];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int t = wave * 16 + q0 + u;
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
-          const float d[4] = {d4.x, d4.y, d4.z, d4.w};
-          float gg[4], xh[4], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            xh[e] = (xv[u][e] - mu[u]) * rs[u];
-            gg[e] = d[e] * wg[e];
-            s1 += gg[e];
-            s2 += gg[e] * xh[e];
+            for (int e = 0; e < 4; ++e) r1[u][e] = 0.f;
+            if (L.res1) load_vec<float, 16>(L.res1 + gr * 256 + c, r1[u]);
           }
-          s1 = wave_sum(s1) / 256.f;
-          s2 = wave_sum(s2) / 256.f;
-          if (grow[u] < g.M) {
-            float o[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = wave * 16 + q0 + u;
+            const f32x4 a4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
+            float v[4] = {a4.x + bb[0], a4.y + bb[1], a4.z + bb[2], a4.w + bb[3]};
+            float sm = 0.f;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              dwa[e] += d[e] * xh[e];
-              dba[e] += d[e];
-              o[e] = rs[u] * (gg[e] - s1 - xh[e] * s2) + r1[u][e] + r2[u][e];
+              v[e] += r1[u][e];
+              sm += v[e];
             }
-            if (L.dxb) store_vec<bf16_t, 4>(L.dxb + grow[u] * 256 + c, o);
-            if (L.res1_twice) {
+            sm = wave_sum(sm);
+            const float mu = sm / 256.f;
+            float qq = 0.f;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] += r1[u][e];
+            for (int e = 0; e < 4; ++e) {
+              const float dd = v[e] - mu;
+              qq += dd * dd;
             }
-            store_vec<float, 4>(L.dx + grow[u] * 256 + c, o);
+            qq = wave_sum(qq);
+            const float rs = 1.f / sqrtf(qq / 256.f + 1e-5f);
+            if (grow[u] < g.M) {
+              store_vec<float, 4>(L.dx + grow[u] * 256 + c, v);
+              float o[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = (v[e] - mu) * rs * wg[e] + lb[e];
+              store_vec<bf16_t, 4>(L.dxb + grow[u] * 256 + c, o);
+              if (lane == 0) {
+                L.mean_out[grow[u]] = mu;
+                L.rstd_out[grow[u]] = rs;
+              }
+            }
+          }
+        }
+      } else {
+        // wave w: staged rows 16 w .. 16 w + 15, four rows' loads in flight at a time
+  #pragma unroll 1
+        for (int q0 = 0; q0 < 16; q0 += 4) {
+          float xv[4][4], r1[4][4], r2[4][4], mu[4], rs[4];
+          int64_t grow[4];
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = wave * 16 + q0 + u;
+            grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
+            const bool ok = grow[u] < g.M;
+            const int64_t gr = ok ? grow[u] : 0;
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) { r1[u][e] = 0.f; r2[u][e] = 0.f; }
+            load_vec<float, 16>(L.x + gr * 256 + c, xv[u]);
+            if (L.res1) load_vec<float, 16>(L.res1 + gr * 256 + c, r1[u]);
+            if (L.res2) load_vec<float, 16>(L.res2 + gr * 256 + c, r2[u]);
+            mu[u] = L.mean[gr];
+            rs[u] = L.rstd[gr];
+          }
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = wave * 16 + q0 + u;
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
+            const float d[4] = {d4.x, d4.y, d4.z, d4.w};
+            float gg[4], xh[4], s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              xh[e] = (xv[u][e] - mu[u]) * rs[u];
+              gg[e] = d[e] * wg[e];
+              s1 += gg[e];
+              s2 += gg[e] * xh[e];
+            }
+            s1 = wave_sum(s1) / 256.f;
+            s2 = wave_sum(s2) / 256.f;
+            if (grow[u] < g.M) {
+              float o[4];
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                dwa[e] += d[e] * xh[e];
+                dba[e] += d[e];
+                o[e] = rs[u] * (gg[e] - s1 - xh[e] * s2) + r1[u][e] + r2[u][e];
+              }
+              if (L.dxb) store_vec<bf16_t, 4>(L.dxb + grow[u] * 256 + c, o);
+              if (L.res1_twice) {
+  #pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] += r1[u][e];
+              }
+              store_vec<float, 4>(L.dx + grow[u] * 256 + c, o);
+            }
           }
         }
       }
@@ -1391,6 +1453,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+    if constexpr (EPX == PP_LNF) return;
     // per-tile weight-gradient partials: the 8 waves' column sums in a fixed order
     const int tile = lid / tiles_n;
 #pragma unroll
@@ -1525,7 +1588,32 @@ extern "C" int lthm_dgrad_layernorm_bwd(const void* dy, const void* wt, int64_t 
   g.fast_ok = true;
   const int tm = lthm_dgrad_layernorm_bwd_tiles(M);
   LnbArgs L{x, w, mean, rstd, res1, res2, dx, (bf16_t*)dx_bf16, partials, partials + (int64_t)tm * 256, flags & 1};
-  hipLaunchKernelGGL((gemm_pp_k<false, false, true>), dim3(tm), dim3(512), 0, (hipStream_t)stream, g, tm, 1, L);
+  hipLaunchKernelGGL((gemm_pp_k<false, false, PP_LNB>), dim3(tm), dim3(512), 0, (hipStream_t)stream, g, tm, 1, L);
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_linear_layernorm_fwd(const void* x, const void* w, const float* bias, const float* res1, int64_t M,
+                                         int32_t D, int64_t K, const float* ln_w, const float* ln_b, float* x1,
+                                         void* h, float* mean, float* rstd, void* stream) {
+  LTHM_REQUIRE(D == 256 && M >= 0 && K > 0 && K % PP_BK == 0);
+  LTHM_REQUIRE(x && w && ln_w && x1 && h && mean && rstd);
+  auto al16 = [](const void* p) { return ((uintptr_t)p % 16) == 0; };
+  LTHM_REQUIRE(al16(x) && al16(w) && al16(ln_w) && al16(x1) && ((uintptr_t)h % 8) == 0 && (!bias || al16(bias)) &&
+               (!ln_b || al16(ln_b)) && (!res1 || al16(res1)));
+  if (M == 0) return 0;
+  GemmArgs g{};
+  g.A = (const bf16_t*)x; g.B = (const bf16_t*)w; g.C = nullptr;
+  g.M = M; g.N = 256; g.K = K;
+  g.lda = K; g.ldb = K; g.ldc = 256;
+  g.alpha = 1.f;
+  g.act = LTHM_ACT_NONE;
+  g.fast_ok = true;
+  const int tm = (int)((M + 255) / 256);
+  LnbArgs L{};
+  L.w = ln_w; L.b = ln_b; L.bias = bias; L.res1 = res1;
+  L.dx = x1; L.dxb = (bf16_t*)h; L.mean_out = mean; L.rstd_out = rstd;
+  hipLaunchKernelGGL((gemm_pp_k<false, false, PP_LNF>), dim3(tm), dim3(512), 0, (hipStream_t)stream, g, tm, 1, L);
   LTHM_CHECK_LAUNCH();
   return 0;
 }

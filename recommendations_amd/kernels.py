@@ -739,6 +739,40 @@ def dgrad_layernorm_bwd(dy2d, w_bf16, x2d, w, mean, rstd, res1=None, res2=None, 
 
 # LTHM_LN_DGRAD=0: the dgrad GEMM writes dh (bf16) and the LayerNorm backward runs as its own pass
 _LN_DGRAD = os.environ.get("LTHM_LN_DGRAD", "1") != "0"
+# LTHM_LN_LINEAR=0: the c_proj GEMM writes x1 and ln_2's forward runs as its own pass
+_LN_LINEAR = os.environ.get("LTHM_LN_LINEAR", "1") != "0"
+
+
+def linear_layernorm_fwd_ok(x2d, w_bf16) -> bool:
+    """Shapes lthm_linear_layernorm_fwd takes: output width 256, K a multiple of 64, aligned."""
+    M, Kd = x2d.shape
+    return (_LN_LINEAR and tuple(w_bf16.shape) == (256, Kd) and Kd % 64 == 0 and x2d.dtype == torch.bfloat16
+            and w_bf16.dtype == torch.bfloat16 and x2d.is_contiguous() and w_bf16.is_contiguous()
+            and x2d.data_ptr() % 16 == 0 and w_bf16.data_ptr() % 16 == 0)
+
+
+def linear_layernorm_fwd(x2d, w_bf16, bias, res1, ln_w, ln_b):
+    """x1 = res1 + x W^T + bias (f32) and LayerNorm(x1) in one kernel (lthm_linear_layernorm_fwd)
+    -> (x1 f32 [M, 256], h bf16 [M, 256], mean, rstd)."""
+    require_gpu(x2d, w_bf16)
+    _check(linear_layernorm_fwd_ok(x2d, w_bf16), "linear_layernorm_fwd: unsupported shapes")
+    M, Kd = x2d.shape
+    for t, n, nm in ((bias, 256, "bias"), (ln_w, 256, "ln weight"), (ln_b, 256, "ln bias"), (res1, M * 256, "res1")):
+        _check(t is None or (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
+                             and t.numel() == n), f"linear_layernorm_fwd: {nm} must be contiguous aligned f32 [{n}]")
+    _check(ln_w is not None, "linear_layernorm_fwd: ln weight")
+    dev = x2d.device
+    x1 = torch.empty((M, 256), dtype=torch.float32, device=dev)
+    h = torch.empty((M, 256), dtype=torch.bfloat16, device=dev)
+    mean = torch.empty(M, dtype=torch.float32, device=dev)
+    rstd = torch.empty(M, dtype=torch.float32, device=dev)
+    # compulsory HBM bytes: x read, the residual read, x1 (f32) and h (bf16) written, the statistics
+    nb = float(M * Kd * 2 + M * 256 * ((4 if res1 is not None else 0) + 4 + 2) + 8 * M)
+    call("lthm_linear_layernorm_fwd", ptr(x2d), ptr(w_bf16), ptr(bias), ptr(res1), M, 256, Kd, ptr(ln_w), ptr(ln_b),
+         ptr(x1), ptr(h), ptr(mean), ptr(rstd), stream(),
+         _key=(_GEMM_TAG[-1] + ":linear_ln") if _GEMM_TAG else "linear_ln", _work=2.0 * M * Kd * 256, _unit="flop",
+         _bytes=nb)
+    return x1, h, mean, rstd
 
 
 def layernorm_bwd(dy2d, x2d, w, mean, rstd, res1=None, res2=None, want_bf16=True, need_bias=True, res1_twice=False):

@@ -617,3 +617,40 @@ def test_dgrad_layernorm_bwd_vs_fp64(dev, M, N, res, twice):
                                     res1_twice=twice)
     check("dx vs unfused", relerr(dx, ux), 4e-3)
     check("dw vs unfused", relerr(dw, uw), 4e-3)
+
+
+@pytest.mark.parametrize("M,Kd,bias,res", [(2048, 256, True, True), (1000, 256, False, True), (7, 64, True, False),
+                                           (33001, 512, True, True)])
+def test_linear_layernorm_fwd_vs_fp64(dev, M, Kd, bias, res):
+    """lthm_linear_layernorm_fwd (the block's c_proj + residual, then ln_2: commons/transformers/
+    layers.py:264, :371, :142-149) against fp64 on the same bf16 operands: x1 1e-6 relative
+    Frobenius (f32 accumulation), h 4e-3 (bf16 output), mean / rstd 1e-5; and against the
+    unfused pair (persistent GEMM with the residual epilogue, then lthm_layernorm_fwd)."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(M + Kd)
+    x = bf(torch.randn(M, Kd, generator=g))
+    W = bf(torch.randn(256, Kd, generator=g) / math.sqrt(Kd))
+    b = torch.randn(256, generator=g) if bias else None
+    r = torch.randn(M, 256, generator=g) * 3 + 1 if res else None
+    lw = torch.randn(256, generator=g) * 0.3 + 1
+    lb = torch.randn(256, generator=g) * 0.1
+    d = lambda t: None if t is None else t.to(dev)
+    assert K.linear_layernorm_fwd_ok(d(x), d(W))
+    x1, h, mu, rs = K.linear_layernorm_fwd(d(x), d(W), d(b), d(r), d(lw), d(lb))
+    torch.cuda.synchronize()
+    want = x.double() @ W.double().T
+    if b is not None:
+        want = want + b.double()
+    if r is not None:
+        want = want + r.double()
+    m64 = want.mean(1)
+    r64 = 1.0 / torch.sqrt(want.var(1, unbiased=False) + 1e-5)
+    h64 = (want - m64[:, None]) * r64[:, None] * lw.double() + lb.double()
+    check("x1", relerr(x1, want), 1e-6)
+    check("h", relerr(h.float(), h64), 4e-3)
+    check("mean", relerr(mu, m64), 1e-5)
+    check("rstd", relerr(rs, r64), 1e-5)
+    ux = K.linear_fwd(d(x), d(W), d(b), res1=d(r), out_dtype=torch.float32)
+    uh, um, ur = K.layernorm_fwd(ux, d(lw), d(lb))
+    check("x1 vs unfused", relerr(x1, ux), 1e-6)
+    check("h vs unfused", relerr(h.float(), uh.float()), 4e-3)

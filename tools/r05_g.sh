@@ -1,5 +1,5 @@
 # Round-5 GPU pass g: K = 1 table backward with first-touch stores (C4) and the dgrad GEMM fused
-# with the LayerNorm backward (C2): tests, then A/B benches (LTHM_KSHIFT_FIRST, LTHM_LN_DGRAD)
+# with the LayerNorm backward and c_proj with ln_2's forward (C2): tests, then A/B benches (LTHM_KSHIFT_FIRST, LTHM_LN_DGRAD, LTHM_LN_LINEAR)
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r05g
 export PARITY_LOG=gpurun_out/r05g/parity.json
@@ -12,7 +12,7 @@ for v in 1 0 1 0; do
   LTHM_KSHIFT_FIRST=$v timeout -k 10 300 python bench.py --config c4 --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/r05g/c4_$v.log 2>&1 || { tail -20 gpurun_out/r05g/c4_$v.log; exit 1; }
   summ gpurun_out/r05g/c4_$v.log FIRST=$v kshift,adam
 done
-for v in 1 0 1 0; do
-  LTHM_LN_DGRAD=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-hbm-gather --steps 10 --warmup 3 > gpurun_out/r05g/c2_$v.log 2>&1 || { tail -20 gpurun_out/r05g/c2_$v.log; exit 1; }
-  summ gpurun_out/r05g/c2_$v.log LNDG=$v layernorm,dgrad_ln,gemm_k
+for v in 11 00 10 01 11 00; do
+  LTHM_LN_DGRAD=${v:0:1} LTHM_LN_LINEAR=${v:1:1} timeout -k 10 300 python bench.py --no-cpu-baseline --no-hbm-gather --steps 10 --warmup 3 > gpurun_out/r05g/c2_$v.log 2>&1 || { tail -20 gpurun_out/r05g/c2_$v.log; exit 1; }
+  summ gpurun_out/r05g/c2_$v.log LN=$v layernorm,dgrad_ln,linear_ln,gemm_k
 done
