@@ -777,6 +777,12 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_mfma_k(AttnArgs a) {
 // ((u >> 1) & 3): the row-fragment reads (16 lanes, 16 rows, one chunk) and the
 // transposed reads (4 rows x 4 chunks per 32 lanes) are both conflict-free.
 constexpr int E_BWD32 = 64;
+// cost-ladder builds of attn_bwd32_k (tools/build_variant.sh ... -DLTHM_ABW_X=n; timing only,
+// wrong results): 1 skips the units (staging, delta, bias copies, partial stores only), 2 skips
+// the staging loads (units on stale LDS), 3 skips the units' gradient stores
+#ifndef LTHM_ABW_X
+#define LTHM_ABW_X 0
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
@@ -873,7 +879,7 @@ __device__ __forceinline__ bf16x8v tr_at(const unsigned char* lo, const unsigned
 __device__ __forceinline__ void store_accT32(const f32x16& x, float scale, bf16_t* __restrict__ base, int64_t ts,
                                              int r0, int nd, int T, int lane, const int* map = nullptr) {
   const int r = r0 + (lane & 31), hh = lane >> 5;
-  if (r >= T) return;
+  if (LTHM_ABW_X == 3 || r >= T) return;
   const int64_t rr = map ? (int64_t)map[r] : (int64_t)r;
   if (rr < 0) return;
   bf16_t* row = base + rr * ts + 32 * nd + 4 * hh;
@@ -1300,11 +1306,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_W
   const bf16_t* og = a.o + b * a.o_bs + h * a.o_hs;
   const bf16_t* dog = a.dout + b * a.o_bs + h * a.o_hs;
   const float* lse_g = a.lse + ((int64_t)b * a.H + h) * T;
+  if (LTHM_ABW_X != 2) {
   stage_img32(IK, kg, a.k_ts, T, Ti, wave, lane, NW);
   stage_img32(IQ, qg, a.q_ts, T, Ti, wave, lane, NW);
   stage_img32(IO, dog, a.o_ts, T, Ti, wave, lane, NW);
   stage_img32(IV, vg, a.v_ts, T, Ti, wave, lane, NW);
-  {  // delta[q] = dO[q] . O[q]: four threads per row, every load in flight before the first use
+  }
+  if (LTHM_ABW_X != 2) {  // delta[q] = dO[q] . O[q]: four threads per row, every load in flight before the first use
     constexpr int RPI = 16 * NW, NIT = (256 + RPI - 1) / RPI;  // rows per iteration, iterations for Tk <= 256
     u32x4 du[NIT][2], ou[NIT][2];
 #pragma unroll
@@ -1348,7 +1356,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_W
     __syncthreads();
   }
   const Frag32Off fo = frag32_off(lane);
-  const uint32_t mine = lpt_units<NW>(nt, a.causal, wave, tail);
+  const uint32_t mine = LTHM_ABW_X == 1 ? 0u : lpt_units<NW>(nt, a.causal, wave, tail);
   // longest first: the rows unit of tile c - 1 and the columns unit of tile nt - c cost alike
   for (int c = nt; c >= 1; --c) {
     if (mine & (1u << (c - 1))) bwd32_rows(a, m, fo, b, h, c - 1, lane, Tu);
