@@ -1209,7 +1209,7 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
 // (a thread per key; dot products over the swizzled image rows), stored to tp / tds and as
 // the bias gradient's diagonal q* - k (written once each, before any unit adds to it)
 __device__ __forceinline__ void bwd32_tail_pass(const Bwd32Smem& m, float* tp, float* tds, float* dbias, int T, int tid,
-                                                int nth) {
+                                                int nth, bool accum = false) {
   const float c2 = rsqrtf((float)E_BWD32) * 1.4426950408889634f;
   const int qs = T - 1, sq = a32_swz(qs);
   const float lq = m.lse[qs], dl = m.dlt[qs];
@@ -1227,7 +1227,8 @@ __device__ __forceinline__ void bwd32_tail_pass(const Bwd32Smem& m, float* tp, f
     const float ds = p * (dp - dl);
     tp[k] = p;
     tds[k] = ds;
-    dbias[qs - k + T] = ds;
+    if (accum) dbias[qs - k + T] += ds;  // the persistent kernel sums the diagonals over its batch entries
+    else dbias[qs - k + T] = ds;
   }
 }
 
@@ -1371,6 +1372,118 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(BWD32_W
 
 static size_t bwd32_lds(int T, bool tail) {
   return (size_t)bwd32_fbytes(T, tail) + (size_t)(4 * bwd32_timg(T) + bwd32_slack(T, tail ? T - 1 : T)) * 128;
+}
+
+// Persistent form of attn_bwd32_k (round 5): one workgroup per CU walks the batch entries of one
+// head, b = slot, slot + S, ... (S workgroups per head), with TWO image sets: while the units of
+// entry b run on one set, the LDS-DMA of entry b + S fills the other, so the K / Q / dO / V
+// staging (the non-persistent kernel waits on it at every workgroup start) overlaps the MFMA
+// work.  The next entry's O rows and LSE ride in registers (one wave per SIMD: the whole
+// register file); delta = dO . O is formed from the landed dO image.  The head's bias copies
+// are staged once, and the bias gradient accumulates over the workgroup's entries in LDS: one
+// partial per (slot, head) instead of one per batch entry.
+__host__ __device__ __forceinline__ int bwd32p_set_bytes(int T, bool tail) {
+  return (4 * bwd32_timg(T) + bwd32_slack(T, tail ? T - 1 : T)) * 128;
+}
+static size_t bwd32p_lds(int T, bool tail) { return (size_t)bwd32_fbytes(T, tail) + 2 * (size_t)bwd32p_set_bytes(T, tail); }
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd32p_k(AttnArgs a, int B,
+                                                                                                  int S) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr int NIT = (256 + 16 * NW - 1) / (16 * NW);  // delta rows per thread (Tk <= 256)
+  const int T = a.T, Tk = (T + 31) & ~31, ne = bias_ne(T), Ti = bwd32_timg(T);
+  const bool tail = a.tail != 0;
+  const int Tu = tail ? T - 1 : T, nt = (Tu + 31) >> 5;
+  float* bfw = reinterpret_cast<float*>(smem);
+  float* brv = bfw + 2 * ne;
+  float* lse_s = brv + 2 * ne;
+  float* dlt_s = lse_s + Tk;
+  float* dbias = dlt_s + Tk;
+  float* tp = dbias + ((2 * T + 1 + 3) & ~3);
+  float* tds = tp + ((T + 3) & ~3);
+  const int setb = bwd32p_set_bytes(T, tail);
+  unsigned char* img0 = smem + bwd32_fbytes(T, tail);
+  const int g = blockIdx.x, h = g % a.H, slot = g / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the head's bias copies, the bias-gradient sums, both sets' zero slack
+  for (int c = 0; c < 2; ++c)
+    for (int y = tid; y < ne; y += 64 * NW) {
+      const int xf = y + c - BPAD, xr = ne - 1 - (y + c) - BPAD;
+      bfw[c * ne + y] = (a.table && xf >= 0 && xf <= 2 * T) ? a.table[(int64_t)xf * a.H + h] * L2E : 0.f;
+      brv[c * ne + y] = (a.table && xr >= 0 && xr <= 2 * T) ? a.table[(int64_t)xr * a.H + h] * L2E : 0.f;
+    }
+  for (int i = tid; i <= 2 * T; i += 64 * NW) dbias[i] = 0.f;
+  for (int st = 0; st < 2; ++st)
+    for (int i = tid; i < bwd32_slack(T, Tu) * 32; i += 64 * NW)
+      reinterpret_cast<float*>(img0 + st * setb + 4 * Ti * 128)[i] = 0.f;
+  // entry b's images into set st, its O rows and LSE into registers
+  u32x4 ou[NIT][2];
+  float lq = 0.f;
+  auto fetch = [&](int bb, int st) {
+    unsigned char* IK = img0 + st * setb;
+    stage_img32(IK, a.k + bb * a.k_bs + h * a.k_hs, a.k_ts, T, Ti, wave, lane, NW);
+    stage_img32(IK + Ti * 128, a.q + bb * a.q_bs + h * a.q_hs, a.q_ts, T, Ti, wave, lane, NW);
+    stage_img32(IK + 2 * Ti * 128, a.dout + bb * a.o_bs + h * a.o_hs, a.o_ts, T, Ti, wave, lane, NW);
+    stage_img32(IK + 3 * Ti * 128, a.v + bb * a.v_bs + h * a.v_hs, a.v_ts, T, Ti, wave, lane, NW);
+    const bf16_t* og = a.o + bb * a.o_bs + h * a.o_hs;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid >> 2) + 16 * NW * it, c = (tid & 3) * 16;
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+        ou[it][x] = r < T ? *reinterpret_cast<const u32x4*>(og + (int64_t)r * a.o_ts + c + 8 * x) : u32x4{0u, 0u, 0u, 0u};
+    }
+    lq = tid < T ? a.lse[((int64_t)bb * a.H + h) * T + tid] : 0.f;
+  };
+  const Frag32Off fo = frag32_off(lane);
+  const uint32_t mine = LTHM_ABW_X == 1 ? 0u : lpt_units<NW>(nt, a.causal, wave, tail);
+  if (slot < B) fetch(slot, 0);
+  int st = 0;
+  for (int b = slot; b < B; b += S, st ^= 1) {
+    wait_vm<0>();
+    __syncthreads();  // entry b landed; every wave is done with the previous entry (set st ^ 1, floats)
+    unsigned char* IK = img0 + st * setb;
+    unsigned char* IQ = IK + Ti * 128;
+    unsigned char* IO = IQ + Ti * 128;
+    unsigned char* IV = IO + Ti * 128;
+    {  // delta[q] = dO[q] . O[q] from the dO image and the O rows in registers; the LSE
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int r = (tid >> 2) + 16 * NW * it, c = (tid & 3) * 16;
+        const int rr = r < Ti ? r : 0;
+        float d = 0.f;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          const int ch = (c >> 3) + x;
+          const bf16x8v dv = frag_at(IO + rr * 128 + ((ch ^ a32_swz(rr)) << 4));
+          d += bf8_dot(dv, __builtin_bit_cast(bf16x8v, ou[it][x]));
+        }
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        if ((tid & 3) == 0 && r < Tk) dlt_s[r] = r < T ? d : 0.f;
+      }
+      if (tid < Tk) lse_s[tid] = tid < T ? lq * L2E : 0.f;
+    }
+    if (b + S < B) fetch(b + S, st ^ 1);  // the other set's last readers passed the barrier above
+    __syncthreads();
+    const Bwd32Smem m{IK, IQ, IO, IV, bfw, brv, lse_s, dlt_s, dbias, ne, tail ? tp : nullptr, tail ? tds : nullptr};
+    if (tail) {
+      bwd32_tail_pass(m, tp, tds, dbias, T, tid, 64 * NW, true);
+      __syncthreads();
+    }
+    const int bh = b;  // (b, h) of this entry
+    for (int c = nt; c >= 1; --c) {
+      if (mine & (1u << (c - 1))) bwd32_rows(a, m, fo, bh, h, c - 1, lane, Tu);
+      if (mine & (1u << (2 * nt - c))) bwd32_cols(a, m, fo, bh, h, nt - c, lane, Tu);
+    }
+    if (mine & (1u << (2 * nt))) bwd32_tail_unit(a, m, bh, h, lane);
+  }
+  if (a.dtable_part && slot < B) {
+    __syncthreads();
+    for (int i = tid; i <= 2 * T; i += 64 * NW) a.dtable_part[((int64_t)slot * (2 * T + 1) + i) * a.H + h] = dbias[i];
+  }
 }
 
 // ===========================================================================
@@ -1783,14 +1896,35 @@ static size_t bwd_mfma_lds(int T, int E) {
   return (size_t)2 * Tk * E * 2 + (size_t)(2 * T + 2) * 8 + (size_t)2 * Tk * 4 + (size_t)4 * 16 * SCR_LD * 4;
 }
 
+static int attn_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 template <int E>
 static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   static const bool old_bwd = getenv("LTHM_ATTN_BWD_OLD") && atoi(getenv("LTHM_ATTN_BWD_OLD"));  // A/B switch
   // LTHM_ATTN_TAIL=0: the last query of T' = 32 n + 1 in tiles like the others (A/B switch)
   static const bool no_tail = getenv("LTHM_ATTN_TAIL") && getenv("LTHM_ATTN_TAIL")[0] == '0';
+  // LTHM_ATTN_BWD_P=0: one workgroup per (b, h) instead of the persistent double-buffered kernel
+  static const bool no_pers = getenv("LTHM_ATTN_BWD_P") && getenv("LTHM_ATTN_BWD_P")[0] == '0';
   if (E == 64 && bwd && !old_bwd) {
     AttnArgs t = a;
     t.tail = !no_tail && bwd32_tail_mode(a.T, a.causal);
+    const int cus = attn_cu_count();
+    int S = std::min(B, std::max(1, cus / a.H));  // workgroups per head
+    if (!no_pers && bwd32p_lds(a.T, t.tail) <= 160 * 1024 && B >= 2 * S && S >= 1) {
+      hipLaunchKernelGGL(attn_bwd32p_k<4>, dim3(S * a.H), dim3(256), bwd32p_lds(a.T, t.tail), s, t, B, S);
+      LTHM_CHECK_LAUNCH();
+      // partials past the S per head were never written
+      return attn_zero_parts(a, S, attn_parts(B, a.T), s);
+    }
     hipLaunchKernelGGL(attn_bwd32_k<BWD32_NW>, dim3(B * a.H), dim3(64 * BWD32_NW), bwd32_lds(a.T, t.tail), s, t);
     LTHM_CHECK_LAUNCH();
     return 0;

@@ -207,7 +207,10 @@ def test_layernorm_golden(dev):
                                             (2, 47, 3, 32, True), (2, 225, 2, 64, True), (3, 97, 1, 64, False),
                                             # windowed long-sequence path (T' > 256; C5 has T' = 513)
                                             (2, 513, 2, 64, True), (3, 300, 1, 64, False), (17, 257, 1, 32, True),
-                                            (1, 400, 2, 128, True), (20, 520, 1, 64, True)])
+                                            (1, 400, 2, 128, True), (20, 520, 1, 64, True),
+                                            # the persistent double-buffered E = 64 backward (B >= 2 x the
+                                            # workgroups per head): tail mode, uneven entries per slot
+                                            (300, 129, 4, 64, True), (520, 65, 1, 64, False), (600, 100, 2, 64, True)])
 def test_attention_vs_oracle(dev, B, T, H, E, causal):
     from recommendations_amd import kernels as K
     g = torch.Generator().manual_seed(B * T + H)
