@@ -95,7 +95,8 @@ int lthm_kshift_bwd_dense(const int64_t* ids, int64_t n, int32_t F, const void* 
                           int32_t mode, float* dW, void* stream);
 
 /* Same, plus the touched-row list for the sparse row-wise optimizers: the first
- * add to a row sets flags[row] (int32 [F*P], caller keeps it zeroed) and appends
+ * add to a row sets flags[row] (int32 [F*P], caller keeps it zeroed; lthm_sparse_adamw /
+ * lthm_sparse_adagrad re-zero the entries of the rows they update, or none with flags = NULL) and appends
  * the row to list (int64 [>= n*F*K]) at atomic index *count (int64, zeroed). */
 int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void* dY,
                            int32_t dy_dtype, const void* out, int32_t out_dtype,
@@ -103,11 +104,13 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
                            float* dW, int32_t* flags, int64_t* list, int64_t* count, void* stream);
 /* The K = 1, plain-output case of lthm_kshift_bwd_sparse (FlatEmbedding / table-batched flat
  * lookups, the C4 ranker: commons/layers.py:56-61's nn.Embedding backward) with the rows of
- * first touch STORED: the item whose flag exchange returned 0 writes its row of dW (no prior
- * contents needed: rows are stored, not accumulated), every other item of a touched row is
- * added afterwards with f32 atomics.  dup_ws: int64 [>= n * F + 1] workspace.  Same dW / flags /
- * list / count result as lthm_kshift_bwd_sparse with K = 1, mode LTHM_KSHIFT_SCALE, up to the
- * f32 summation order of duplicated rows. */
+ * first touch STORED: the item that sets the row's bit writes its row of dW (no prior contents
+ * needed: rows are stored, not accumulated), every other item of a touched row is added
+ * afterwards with f32 atomics.  flags here is a BITMAP: bit (row & 31) of 32-bit word row >> 5,
+ * [>= ceil(F * P / 32)] words, kept zeroed by the caller (the row-wise optimizer clears it whole
+ * after its step).  dup_ws: int64 [>= n * F + 1] workspace.  Same dW / list / count result as
+ * lthm_kshift_bwd_sparse with K = 1, mode LTHM_KSHIFT_SCALE, up to the f32 summation order of
+ * duplicated rows. */
 int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
                                  int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list, int64_t* count,
                                  int64_t* dup_ws, int64_t dup_cap, void* stream);

@@ -28,6 +28,7 @@ class _SparseRowsMixin:
         self._shadow_version = -1
         self._shadow_src = (0, None)  # (data_ptr, device) of the master the shadow was cast from
         self.sparse_grad = self.sparse_flags = self.sparse_rows = self.sparse_count = None
+        self.sparse_flag_bits = False
         self.sparse_pending = 0
         self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
 
@@ -35,7 +36,11 @@ class _SparseRowsMixin:
         w = self.weight
         if self.sparse_grad is None or self.sparse_grad.device != w.device:
             self.sparse_grad = K.zeros(w.shape, torch.float32, w.device)
-            self.sparse_flags = torch.zeros(w.shape[0], dtype=torch.int32, device=w.device)
+            # K = 1 tables: a touched-row bitmap (F * P bits; the first-touch backward), else an
+            # int32 flag per row
+            self.sparse_flag_bits = K.kshift_first_touch_ok(self._num_shifts, self._mode, w.shape[1])
+            nflag = (w.shape[0] + 31) // 32 if self.sparse_flag_bits else w.shape[0]
+            self.sparse_flags = torch.zeros(nflag, dtype=torch.int32, device=w.device)
             self.sparse_count = torch.zeros(1, dtype=torch.int64, device=w.device)
             self.sparse_rows = torch.empty(0, dtype=torch.int64, device=w.device)
         need = min(self.sparse_pending + max_new_rows, w.shape[0])
@@ -191,7 +196,7 @@ def _kshift_bwd_local(mod, ids, gy, out, norms):
     mod._ensure_sparse_state(ids.numel() * mod._num_shifts)
     K.kshift_bwd_sparse(ids, gy, out, norms, mod._num_embeddings, mod._num_shifts, mod._mode, mod._F,
                         mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,
-                        pending=mod.sparse_pending)
+                        pending=mod.sparse_pending, flag_bits=mod.sparse_flag_bits)
     mod.sparse_pending += ids.numel() * mod._num_shifts
 
 

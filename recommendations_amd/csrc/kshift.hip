@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_k(const int64_t* __restrict
 template <typename TY>
 __global__ __launch_bounds__(256) void kshift_bwd_k1_first_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
                                                              const TY* __restrict__ dY, int64_t P, int D,
-                                                             float* __restrict__ dW, int32_t* __restrict__ flags,
+                                                             float* __restrict__ dW, uint32_t* __restrict__ bits,
                                                              int64_t* __restrict__ list,
                                                              unsigned long long* __restrict__ count,
                                                              int64_t* __restrict__ dups,
@@ -593,7 +593,10 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_first_k(const int64_t* __re
       const bool ok = item < c1;
       const int64_t row = ok ? ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], 0, P) : 0;
       int prev = 1;
-      if (ok && d == 0) prev = atomicExch(flags + row, 1);
+      if (ok && d == 0) {  // the row's bit of the touched-row bitmap (F * P bits: an Infinity-Cache-sized array)
+        const uint32_t bit = 1u << (row & 31);
+        prev = (atomicOr(bits + (row >> 5), bit) & bit) ? 1 : 0;
+      }
       prev = __shfl(prev, il * D, 64);  // the item's first lane decided for its D lanes
       if (ok) {
         const float g = Elem<TY>::ld(dY + item * D + d);
@@ -642,7 +645,7 @@ static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY
   if (K == 1 && mode != LTHM_KSHIFT_NORMALIZE && D <= 64 && 64 % D == 0 && flags && dups && ndup) {
     LTHM_REQUIRE(hipMemsetAsync(ndup, 0, sizeof(unsigned long long), s) == hipSuccess);
     hipLaunchKernelGGL((kshift_bwd_k1_first_k<TY>), dim3(grid_for(n_items, K1_CHUNK, 256 * 8)), dim3(256), 0, s, ids,
-                       n_items, F, (const TY*)dY, P, D, dW, flags, list, count, dups, ndup);
+                       n_items, F, (const TY*)dY, P, D, dW, reinterpret_cast<uint32_t*>(flags), list, count, dups, ndup);
     LTHM_CHECK_LAUNCH();
     hipLaunchKernelGGL((kshift_bwd_k1_dup_k<TY>), dim3(1024), dim3(256), 0, s, ids, F, (const TY*)dY, P, D, dW,
                        (const int64_t*)dups, (const unsigned long long*)ndup);

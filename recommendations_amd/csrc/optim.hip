@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
     }
-    if (d0 == 0) flags[r] = 0;
+    if (flags && d0 == 0) flags[r] = 0;
   }
 }
 
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void sparse_opt_v4_k(const int64_t* __restrict
     if (shadow) st4bf(shadow + i, pi);
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
     st4f(g + i, z);
-    if (d0 == 0) flags[r] = 0;
+    if (flags && d0 == 0) flags[r] = 0;
     r = rn;
   }
 }
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restric
       if (shadow) shadow[i] = f2bf(pi);
       g[i] = 0.f;
     }
-    if (d0 == 0) flags[r] = 0;
+    if (flags && d0 == 0) flags[r] = 0;
   }
 }
 

@@ -936,20 +936,31 @@ _KSHIFT_FIRST = os.environ.get("LTHM_KSHIFT_FIRST", "1") != "0"
 _dup_ws = {}
 
 
-def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0):
+def kshift_first_touch_ok(K, mode, D) -> bool:
+    """The K = 1 table backward with first-touch stores and a touched-row bitmap
+    (lthm_kshift_bwd_sparse_first) serves this table shape (LTHM_KSHIFT_FIRST=0: never)."""
+    return _KSHIFT_FIRST and K == 1 and mode != KSHIFT_NORMALIZE and D <= 64 and 64 % D == 0
+
+
+def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0, flag_bits=False):
     """Accumulate into dense dW and append the touched rows (see include/lthm.h).
     Table-batched layout: dW and flags cover all F*P rows; rows_list must hold
-    every row that can still be appended (<= F*P, <= pending + ids*K)."""
+    every row that can still be appended (<= F*P, <= pending + ids*K).  flag_bits: flags is
+    the touched-row bitmap of the first-touch K = 1 backward (int32 words, >= ceil(F*P / 32))."""
     require_gpu(ids, gy, out, norms, dW, flags, rows_list, count)
     D = dW.shape[1]
     _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0], gy=gy, out=out, norms=norms)
     _check(dW.dtype == torch.float32, "dW must be float32")
-    _check(flags.dtype == torch.int32 and flags.numel() >= F * P, "flags must be int32 with >= F*P entries")
+    nflag = (F * P + 31) // 32 if flag_bits else F * P
+    _check(flags.dtype == torch.int32 and flags.numel() >= nflag, f"flags must be int32 with >= {nflag} entries")
+    _check(not flag_bits or kshift_first_touch_ok(K, mode, D), "a touched-row bitmap needs the K = 1 first-touch path")
     cap = min(F * P, pending + ids.numel() * K)
     _check(rows_list.dtype == torch.int64 and rows_list.numel() >= cap, f"rows_list must be int64 with >= {cap} entries")
     _check(count.dtype == torch.int64 and count.numel() >= 1, "count must be an int64 scalar buffer")
     n = ids.numel() // F
-    if _KSHIFT_FIRST and K == 1 and mode != KSHIFT_NORMALIZE and D <= 64 and 64 % D == 0 and ids.numel():
+    if flag_bits:
+        if not ids.numel():
+            return
         # first-touch rows stored, repeats added afterwards (lthm_kshift_bwd_sparse_first)
         ws = _dup_ws.get(ids.device)
         if ws is None or ws.numel() < ids.numel() + 1:
@@ -1014,7 +1025,7 @@ def adagrad_(p, g, s, lr, lr_decay, eps, wd, step, zero_grad=False):
 def _check_sparse_rows(rows, max_rows, p, flags, *states):
     _check(p.dim() == 2 and max_rows <= p.shape[0], "sparse update: p must be [R, D] and max_rows <= R")
     _need(rows, max_rows, "rows")
-    _need(flags, p.shape[0], "flags")
+    _need(flags, p.shape[0], "flags")  # (flags None: the caller clears its touched-row bitmap itself)
     for t in states:
         _need(t, p.numel(), "state")
 

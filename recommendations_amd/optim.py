@@ -109,6 +109,15 @@ class FusedAdagrad(torch.optim.Optimizer):
         return loss
 
 
+def _clear_touched(m, bits):
+    """After a row-wise step: the touched-row list is consumed; a touched-row bitmap (K = 1
+    tables, F * P / 8 bytes) is cleared whole, int32 flags were re-zeroed per row by the kernel."""
+    if bits:
+        m.sparse_flags.zero_()
+    m.sparse_count.zero_()
+    m.sparse_pending = 0
+
+
 class SparseRowAdamW:
     """Row-wise AdamW over TableBatchedKShiftEmbedding modules (sparse=True)."""
 
@@ -129,11 +138,11 @@ class SparseRowAdamW:
                 st = self.state[id(m)] = (K.zeros(m.weight.shape, torch.float32, m.weight.device),
                                           K.zeros(m.weight.shape, torch.float32, m.weight.device))
             shadow = m.shadow_current()
+            bits = getattr(m, "sparse_flag_bits", False)
             K.sparse_adamw_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
-                            m.sparse_grad, st[0], st[1], m.sparse_flags, self.lr, self.betas, self.eps,
-                            self.weight_decay, self.step_count, shadow=shadow)
-            m.sparse_count.zero_()
-            m.sparse_pending = 0
+                            m.sparse_grad, st[0], st[1], None if bits else m.sparse_flags, self.lr, self.betas,
+                            self.eps, self.weight_decay, self.step_count, shadow=shadow)
+            _clear_touched(m, bits)
 
     def zero_grad(self, set_to_none: bool = True):
         pass  # the row-wise step consumes and re-zeroes exactly the rows it updates
@@ -154,8 +163,8 @@ class SparseRowAdagrad(SparseRowAdamW):
             if st is None:
                 st = self.state[id(m)] = K.zeros(m.weight.shape, torch.float32, m.weight.device)
             shadow = m.shadow_current()
+            bits = getattr(m, "sparse_flag_bits", False)
             K.sparse_adagrad_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
-                              m.sparse_grad, st, m.sparse_flags, self.lr, self.lr_decay, self.eps, self.step_count,
-                              shadow=shadow)
-            m.sparse_count.zero_()
-            m.sparse_pending = 0
+                              m.sparse_grad, st, None if bits else m.sparse_flags, self.lr, self.lr_decay, self.eps,
+                              self.step_count, shadow=shadow)
+            _clear_touched(m, bits)

@@ -196,7 +196,8 @@ def test_kshift_sparse_touched_rows(dev, P, D, Kk, F, n):
                                         (64, 32, 2, 1, torch.bfloat16), (300, 64, 4, 9000, torch.float32)])
 def test_kshift_sparse_k1_accumulates(dev, first, P, D, F, n, dt):
     """K = 1 table backward (commons/layers.py:56-61's nn.Embedding backward over the C4
-    ranker's tables): lthm_kshift_bwd_sparse_first (first touch stored, repeats added) and the
+    ranker's tables): lthm_kshift_bwd_sparse_first (first touch stored, repeats added, a
+    touched-row bitmap) and the
     all-atomic lthm_kshift_bwd_sparse give the fp64 per-row sums, the touched rows once in the
     list, across two backward calls (the second over rows already flagged, gradient
     accumulation).  f32 sums in a different order: 1e-5 of the row's |dY| mass."""
@@ -206,7 +207,8 @@ def test_kshift_sparse_k1_accumulates(dev, first, P, D, F, n, dt):
     try:
         g = np.random.default_rng(P + n + D)
         dW = torch.zeros((F * P, D), dtype=torch.float32, device=dev)
-        flags = torch.zeros(F * P, dtype=torch.int32, device=dev)
+        # first: the touched-row bitmap (bit r & 31 of word r >> 5); else an int32 flag per row
+        flags = torch.zeros((F * P + 31) // 32 if first else F * P, dtype=torch.int32, device=dev)
         lst = torch.zeros(F * P, dtype=torch.int64, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
         want = np.zeros((F * P, D))
@@ -217,7 +219,7 @@ def test_kshift_sparse_k1_accumulates(dev, first, P, D, F, n, dt):
             ids[: n // 5] = ids[n // 5]  # a hot row per feature
             dy = torch.randn((n, F, D), dtype=torch.float32).to(dt)
             K.kshift_bwd_sparse(torch.from_numpy(ids).to(dev), dy.to(dev), None, None, P, 1, 0, F, dW, flags, lst, cnt,
-                                pending=pending)
+                                pending=pending, flag_bits=first)
             pending += n * F
             rows = kshift_rows(ids.reshape(-1), P, 1).reshape(-1) + np.tile(np.arange(F) * P, n)
             d64 = dy.double().numpy().reshape(-1, D)
@@ -230,6 +232,8 @@ def test_kshift_sparse_k1_accumulates(dev, first, P, D, F, n, dt):
         c = int(cnt.item())
         np.testing.assert_array_equal(np.sort(lst[:c].cpu().numpy()), touched)
         fl = flags.cpu().numpy()
+        if first:
+            fl = np.unpackbits(fl.view(np.uint8), bitorder="little")[: F * P]
         assert fl[touched].all() and fl.sum() == len(touched)
     finally:
         K._KSHIFT_FIRST = old
