@@ -582,29 +582,52 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_first_k(const int64_t* __re
   __shared__ int s_nnew, s_ndup;
   __shared__ unsigned long long s_base, s_dbase;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ipw = 64 / D;  // items per wave instruction
-  const int il = lane / D, d = lane - il * D;
+  // copy phase: VEC columns per lane (16-B f32 stores where D % 4 == 0), LPI lanes per item
+  const int VEC = (D % 4 == 0) ? 4 : 1, LPI = D / VEC, ipw = 64 / LPI;
+  const int il = lane / LPI, c = (lane - il * LPI) * VEC;
+  const uint64_t lt = (1ull << lane) - 1ull;  // lanes below this one
   for (int64_t c0 = (int64_t)blockIdx.x * K1_CHUNK; c0 < n_items; c0 += (int64_t)gridDim.x * K1_CHUNK) {
     if (tid == 0) s_nnew = s_ndup = 0;
     __syncthreads();
     const int64_t c1 = min(n_items, c0 + K1_CHUNK);
-    for (int64_t b = c0 + (int64_t)wave * ipw; b < c1; b += 4 * ipw) {
-      const int64_t item = b + il;
+    for (int64_t base = c0 + (int64_t)wave * 64; base < c1; base += 256) {
+      // 64 items per wave, one per lane: the 64 bitmap atomics of the wave in flight together
+      // (per item, serially, the atomic's round trip bounded the kernel)
+      const int64_t item = base + lane;
       const bool ok = item < c1;
       const int64_t row = ok ? ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], 0, P) : 0;
       int prev = 1;
-      if (ok && d == 0) {  // the row's bit of the touched-row bitmap (F * P bits: an Infinity-Cache-sized array)
+      if (ok) {  // the row's bit of the touched-row bitmap (F * P bits: an Infinity-Cache-sized array)
         const uint32_t bit = 1u << (row & 31);
         prev = (atomicOr(bits + (row >> 5), bit) & bit) ? 1 : 0;
       }
-      prev = __shfl(prev, il * D, 64);  // the item's first lane decided for its D lanes
-      if (ok) {
-        const float g = Elem<TY>::ld(dY + item * D + d);
-        if (prev == 0) {
-          dW[row * D + d] = g;  // first touch: the row's gradient IS this item's
-          if (d == 0) s_new[atomicAdd(&s_nnew, 1)] = row;
-        } else if (d == 0) {
-          s_dup[atomicAdd(&s_ndup, 1)] = item;
+      const bool isnew = ok && prev == 0, isdup = ok && prev != 0;
+      const uint64_t mnew = __ballot(isnew), mdup = __ballot(isdup);
+      int bn = 0, bd = 0;
+      if (lane == 0) {
+        bn = atomicAdd(&s_nnew, (int)__popcll(mnew));
+        bd = atomicAdd(&s_ndup, (int)__popcll(mdup));
+      }
+      bn = __shfl(bn, 0, 64);
+      bd = __shfl(bd, 0, 64);
+      if (isnew) s_new[bn + __popcll(mnew & lt)] = row;
+      if (isdup) s_dup[bd + __popcll(mdup & lt)] = item;
+      // first touches: the row's gradient IS this item's (plain stores; repeats: kshift_bwd_k1_dup_k)
+      const uint32_t rlo = (uint32_t)row, rhi = (uint32_t)((uint64_t)row >> 32);
+#pragma unroll 4
+      for (int s0 = 0; s0 < 64; s0 += ipw) {
+        const int src = s0 + il;
+        const int64_t r = (int64_t)(((uint64_t)(uint32_t)__shfl((int)rhi, src, 64) << 32) | (uint32_t)__shfl((int)rlo, src, 64));
+        const int pv = __shfl(prev, src, 64);
+        const int64_t it = base + src;
+        if (it < c1 && pv == 0) {
+          if (VEC == 4) {
+            float g[4];
+            load_vec<TY, 4 * (int)sizeof(TY)>(dY + it * D + c, g);
+            *reinterpret_cast<f32x4*>(dW + r * D + c) = f32x4{g[0], g[1], g[2], g[3]};
+          } else {
+            dW[r * D + c] = Elem<TY>::ld(dY + it * D + c);
+          }
         }
       }
     }
