@@ -158,46 +158,33 @@ __global__ __launch_bounds__(256) void sparse_opt_v4_k(const int64_t* __restrict
   const int L = D >> 2, rpw = 64 / L;
   const int sub = lane / L, d0 = (lane - sub * L) * 4;
   const int64_t stride = (int64_t)gridDim.x * 4 * rpw;
-  // U rows per lane group in flight: every array's row loads of U rows issued before the first
-  // update (random 128-B rows: the loads' round trip, not the bytes, bounded one row at a time)
-  constexpr int U = 4;
-  for (int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + sub; k0 < cnt; k0 += U * stride) {
-    int64_t r[U];
-    float gi[U][4], pi[U][4], mi[U][4], vi[U][4];
+  int64_t k = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + sub;
+  int64_t r = k < cnt ? rows[k] : 0;
+  for (; k < cnt; k += stride) {
+    const int64_t kn = k + stride;
+    const int64_t rn = kn < cnt ? rows[kn] : 0;  // the next row index in flight
+    const int64_t i = r * D + d0;
+    float gi[4], pi[4], mi[4];
+    ld4f(g + i, gi);
+    ld4f(p + i, pi);
+    ld4f(m + i, mi);  // ADAM: first moment; Adagrad: the state sum
+    if constexpr (ADAM) {
+      float vi[4];
+      ld4f(v + i, vi);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t k = k0 + u * stride;
-      r[u] = k < cnt ? rows[k] : -1;
+      for (int e = 0; e < 4; ++e) pi[e] = adamw_elem(pi[e], gi[e], mi[e], vi[e], lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+      st4f(v + i, vi);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pi[e] = adagrad_elem(pi[e], gi[e], mi[e], lr, eps);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (r[u] < 0) continue;
-      const int64_t i = r[u] * D + d0;
-      ld4f(g + i, gi[u]);
-      ld4f(p + i, pi[u]);
-      ld4f(m + i, mi[u]);  // ADAM: first moment; Adagrad: the state sum
-      if constexpr (ADAM) ld4f(v + i, vi[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (r[u] < 0) continue;
-      const int64_t i = r[u] * D + d0;
-      if constexpr (ADAM) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          pi[u][e] = adamw_elem(pi[u][e], gi[u][e], mi[u][e], vi[u][e], lr, b1, b2, eps, wd, bc1, bc2_sqrt);
-        st4f(v + i, vi[u]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pi[u][e] = adagrad_elem(pi[u][e], gi[u][e], mi[u][e], lr, eps);
-      }
-      st4f(m + i, mi[u]);
-      st4f(p + i, pi[u]);
-      if (shadow) st4bf(shadow + i, pi[u]);
-      const float z[4] = {0.f, 0.f, 0.f, 0.f};
-      st4f(g + i, z);
-      if (flags && d0 == 0) flags[r[u]] = 0;
-    }
+    st4f(m + i, mi);
+    st4f(p + i, pi);
+    if (shadow) st4bf(shadow + i, pi);
+    const float z[4] = {0.f, 0.f, 0.f, 0.f};
+    st4f(g + i, z);
+    if (flags && d0 == 0) flags[r] = 0;
+    r = rn;
   }
 }
 
