@@ -879,16 +879,34 @@ __device__ __forceinline__ bf16x8v tr_at(const unsigned char* lo, const unsigned
 __device__ __forceinline__ void store_accT32(const f32x16& x, float scale, bf16_t* __restrict__ base, int64_t ts,
                                              int r0, int nd, int T, int lane, const int* map = nullptr) {
   const int r = r0 + (lane & 31), hh = lane >> 5;
-  if (LTHM_ABW_X == 3 || r >= T) return;
-  const int64_t rr = map ? (int64_t)map[r] : (int64_t)r;
-  if (rr < 0) return;
-  bf16_t* row = base + rr * ts + 32 * nd + 4 * hh;
+  if (LTHM_ABW_X == 3) return;
+  // every lane takes part in the lane-half exchange below; the store is per lane
+  const int64_t rr = r < T ? (map ? (int64_t)map[r] : (int64_t)r) : -1;
+  // register 4 g + j holds e = 32 nd + 8 g + 4 hh + j.  Packed to bf16 pairs, then the lane halves
+  // trade groups (v_permlane32_swap: the upper half of the first operand with the lower half of
+  // the second): lane (t, hh) ends with e = 32 nd + 16 hh .. + 15, two 16-B stores per lane
+  // instead of four 8-B ones (the stores touch half as many lines per instruction)
+  uint32_t w[4][2];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const uint2 w = {pk_bf16_rne(x[4 * g] * scale, x[4 * g + 1] * scale),
-                     pk_bf16_rne(x[4 * g + 2] * scale, x[4 * g + 3] * scale)};
-    *reinterpret_cast<uint2*>(row + 8 * g) = w;
+    w[g][0] = pk_bf16_rne(x[4 * g] * scale, x[4 * g + 1] * scale);
+    w[g][1] = pk_bf16_rne(x[4 * g + 2] * scale, x[4 * g + 3] * scale);
   }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(w[g][q], w[g + 2][q], false, false);
+      w[g][q] = sw[0];
+      w[g + 2][q] = sw[1];
+    }
+  if (r >= T || rr < 0) return;
+  bf16_t* row = base + rr * ts + 32 * nd + 16 * hh;
+  // hh = 0: w[g] = e 8g .. 8g + 3 (kept), w[g + 2] = e 8g + 4 .. 8g + 7 (from the upper half);
+  // hh = 1: w[g] = e 16 + 8g .. + 3 (from the lower half), w[g + 2] = e 16 + 8g + 4 .. (kept)
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    *reinterpret_cast<uint4*>(row + 8 * g) = uint4{w[g][0], w[g][1], w[g + 2][0], w[g + 2][1]};
 }
 
 // the wave's units over the NW waves, longest first: unit u < nt is the rows unit of query
@@ -1184,8 +1202,8 @@ __device__ __forceinline__ void bwd32_cols(const AttnArgs& a, const Bwd32Smem& m
   }
   if (pkd) {
     // a chain key's gradient is one sequence's share of the chain row's: to the chain buffer
-    // (summed over the sequences afterwards), the others to their packed row
-    if (k >= T) return;
+    // (summed over the sequences afterwards), the others to their packed row (keys k >= T:
+    // store_accT32 stores nothing, but every lane takes part in its lane exchange)
     const bool ch = rk < a.chain;
     bf16_t* dkg = ch ? a.dk_chain + ((int64_t)b * a.chain + k) * a.chain_ts + h * a.k_hs : a.dk + rk * a.k_ts + h * a.k_hs;
     bf16_t* dvg = ch ? a.dv_chain + ((int64_t)b * a.chain + k) * a.chain_ts + h * a.v_hs : a.dv + rk * a.v_ts + h * a.v_hs;
@@ -1912,8 +1930,11 @@ static int attn_launch_mfma(const AttnArgs& a, int B, bool bwd, hipStream_t s) {
   static const bool old_bwd = getenv("LTHM_ATTN_BWD_OLD") && atoi(getenv("LTHM_ATTN_BWD_OLD"));  // A/B switch
   // LTHM_ATTN_TAIL=0: the last query of T' = 32 n + 1 in tiles like the others (A/B switch)
   static const bool no_tail = getenv("LTHM_ATTN_TAIL") && getenv("LTHM_ATTN_TAIL")[0] == '0';
-  // LTHM_ATTN_BWD_P=0: one workgroup per (b, h) instead of the persistent double-buffered kernel
-  static const bool no_pers = getenv("LTHM_ATTN_BWD_P") && getenv("LTHM_ATTN_BWD_P")[0] == '0';
+  // LTHM_ATTN_BWD_P=1: the persistent double-buffered kernel instead of one workgroup per (b, h).
+  // Off by default: at one wave per SIMD its units' dependency chains are exposed (C2 1.23 ms
+  // against 0.91; with the loads removed it still takes 1.23, the per-(b, h) kernel 0.60:
+  // profiles/r05h_ladder.log)
+  static const bool no_pers = !(getenv("LTHM_ATTN_BWD_P") && getenv("LTHM_ATTN_BWD_P")[0] == '1');
   if (E == 64 && bwd && !old_bwd) {
     AttnArgs t = a;
     t.tail = !no_tail && bwd32_tail_mode(a.T, a.causal);
