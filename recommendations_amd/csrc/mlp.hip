@@ -315,6 +315,11 @@ __device__ __forceinline__ void mlp_load_ln(const MlpArgs& a, const float* lw, c
 // beside the partner's S MFMAs and its output MFMAs beside the partner's GELU
 // (MI355X_MICROARCH.md, two waves per SIMD, item 9).  The ring then prefetches one chunk ahead
 // (chunk j - 1 stays readable during step j); without STAG it prefetches two.
+// cost-ladder builds of mlp_fwd_k (tools/build_variant.sh ... -DLTHM_MLPF_X=n; timing only, wrong
+// results): 1 no DMA waits, 2 no GELU (the bias add only), 3 no per-chunk barrier, 4 no S MFMAs
+#ifndef LTHM_MLPF_X
+#define LTHM_MLPF_X 0
+#endif
 template <int D, int NW, bool STAG>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   constexpr int NS = 3, DIST = STAG ? 1 : 2;
@@ -354,6 +359,10 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     // LDS reads one step ahead of their MFMA; the compiler fences keep the unrolled loops
     // from hoisting every read (register pressure: 2 waves per SIMD)
     f32x16 S = f32x16{};
+    if (LTHM_MLPF_X == 4) {
+      S[0] = (float)mlp_row_frag<D>(w1, lane, 0)[0];
+      return S;
+    }
     bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -371,7 +380,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     for (int m = 0; m < 4; ++m) {
       const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hv[4 * m + e] = gelu_tanh(S[4 * m + e] + bb[e]);
+      for (int e = 0; e < 4; ++e) hv[4 * m + e] = LTHM_MLPF_X == 2 ? S[4 * m + e] + bb[e] : gelu_tanh(S[4 * m + e] + bb[e]);
     }
     const bf16x8m hf0 = mlp_pack(hv), hf1 = mlp_pack(hv + 8);
     bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
@@ -401,9 +410,11 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     for (int j = 0; j < NC; ++j, ++g) {
       // retire chunk g; at prefetch distance 2 chunk g + 1 stays in flight (a tile's first step
       // drains: the x / residual / output accesses were issued behind the DMAs)
-      if (DIST == 1 || j == 0) wait_vm<0>();
-      else wait_vm<DPC>();
-      __syncthreads();  // chunk g landed everywhere; every wave is done with chunk g + DIST - NS
+      if (LTHM_MLPF_X != 1) {
+        if (DIST == 1 || j == 0) wait_vm<0>();
+        else wait_vm<DPC>();
+      }
+      if (LTHM_MLPF_X != 3) __syncthreads();  // chunk g landed everywhere; every wave is done with chunk g + DIST - NS
       asm volatile("" ::: "memory");
       {
         // chunk g + DIST: of this tile, or the next tile's (same weights, chunk index wraps)
