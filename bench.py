@@ -93,7 +93,7 @@ def pmc_traffic(key, calls_per_step):
     return tot / (calls_per_step * PMC_STEPS)
 
 
-def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=10):
+def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=50):
     """SURVEY §8(d) embedding roofline: KShift gather + pool forward on a table far past
     the 256 MiB Infinity Cache (P x D bf16 = 4.1 GB), algorithmic bytes per lookup
     8 + K*D*2 + D*2 (bf16 out) over the HIP-event time of the kernel, for two id sets:
@@ -107,21 +107,27 @@ def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=10):
     g = torch.Generator(device=dev).manual_seed(7)
     W = torch.randn((P, D), device=dev, generator=g).to(torch.bfloat16)
     per = 8 + K * D * 2 + D * 2
-    res = {"kernel": "kshift_fwd_k", "table": f"P={P} D={D} bf16 ({P * D * 2 / 1e9:.2f} GB)", "K": K,
+    res = {"kernel": "kshift_fwd_reg_k", "table": f"P={P} D={D} bf16 ({P * D * 2 / 1e9:.2f} GB)", "K": K,
            "lookups": n, "bytes_per_lookup": per, "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     for name, lo in (("spread_ids", 0), ("reference_ids", -(2 ** 63))):
         ids = torch.randint(lo, 2 ** 63 - 1, (n,), device=dev, generator=g, dtype=torch.int64)
-        out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
+        for _ in range(3):
             out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
-        e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / iters
+        # every launch between its own pair of events (the launches are back to back on the
+        # stream): the median launch is the reported rate, the mean beside it
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+        evs[0].record()
+        for i in range(iters):
+            out = K_.kshift(ids, W, P, K, K_.KSHIFT_SCALE)
+            evs[i + 1].record()
+        torch.cuda.synchronize()
+        per_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(iters))
+        ms = per_ms[iters // 2]
+        mean_ms = sum(per_ms) / iters
         gbs = n * per / (ms / 1000.0) / 1e9
-        res[name] = {"avg_launch_ms": round(ms, 4), "achieved": round(gbs, 1)}
+        res[name] = {"median_launch_ms": round(ms, 4), "mean_launch_ms": round(mean_ms, 4), "launches": iters,
+                     "achieved": round(gbs, 1)}
         if name == "spread_ids":
             res[name]["frac"] = round(gbs / HBM_PEAK_GBS, 4)
         else:  # about half the row reads hit the one cached row P-1: algorithmic bytes exceed HBM's
@@ -130,15 +136,21 @@ def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=10):
         del out
     del W
     res["achieved"], res["frac"] = res["spread_ids"]["achieved"], res["spread_ids"]["frac"]
-    try:  # HBM bytes per launch from the committed counter passes (tools/pmc_gather.sh)
-        with open(os.path.join(ROOT, "profiles", "r02_gather_pmc.json")) as f:
-            pmc = json.load(f)
-        for name in ("spread_ids", "reference_ids"):
-            res[name]["traffic"] = pmc[name]["hbm_bytes"]
-        res["traffic"] = pmc["spread_ids"]["hbm_bytes"]
-    except (OSError, KeyError, ValueError):
-        res["traffic"] = None
-    res["traffic_source"] = "profiles/r02_gather_pmc.json (tools/pmc_gather.sh: rocprofv3 --pmc over tools/gather_bench.py)"
+    # HBM bytes per launch from the committed counter passes (tools/pmc_gather.sh): this round's
+    # kernel when its summary is present, else round 2's
+    res["traffic"] = None
+    for src in ("r06_gather_pmc.json", "r02_gather_pmc.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", src)) as f:
+                pmc = json.load(f)
+            for name in ("spread_ids", "reference_ids"):
+                res[name]["traffic"] = pmc[name]["hbm_bytes"]
+            res["traffic"] = pmc["spread_ids"]["hbm_bytes"]
+            res["traffic_source"] = (f"profiles/{src} (tools/pmc_gather.sh: rocprofv3 --pmc over tools/gather_bench.py;"
+                                     f" kernel {pmc.get('kernel')})")
+            break
+        except (OSError, KeyError, ValueError):
+            continue
     return res
 
 
@@ -547,6 +559,40 @@ def main():
                                            "frac_roofline: per form max(flop / MFMA peak, compulsory HBM bytes / "
                                            "HBM peak) summed, over the time taken (K = 528k-row weight gradients "
                                            "sit below the ridge point)"}
+
+            def split(pred, note):
+                sub = {k: v for k, v in enc.items() if pred(k)}
+                if not sub:
+                    return None
+                ts = sum(v["ms"] for v in sub.values()) / 1000.0
+                pk_s = sum(v["work"] / ((FP8_PEAK_TFLOPS if "fp8" in k else BF16_PEAK_TFLOPS) * 1e12)
+                           for k, v in sub.items())
+                o = {"achieved": round(sum(v["work"] for v in sub.values()) / ts / 1e12, 1), "unit": "TFLOP/s",
+                     "frac": round(pk_s / ts, 4), "ms_per_step": round(1000 * ts / PROF_STEPS, 3),
+                     "flop_per_step": round(sum(v["work"] for v in sub.values()) / PROF_STEPS / 1e12, 3),
+                     "forms": sorted(sub), "note": note}
+                nbytes = sum(v.get("bytes", 0.0) for v in sub.values())
+                if nbytes:
+                    o["declared_bytes_per_step"] = round(nbytes / PROF_STEPS)
+                return o
+            # the MFMA fraction of the plain GEMM kernels alone, and the fused
+            # forms beside it (their LayerNorm / GELU work and bytes are inside their time)
+            plain = lambda k: k.split(":")[-1].startswith("gemm")  # noqa: E731
+            subs = {"gemm_only": split(plain, "plain GEMM kernels (gemm_ps_k / gemm_wg_k / gemm_pp_k forms with "
+                                               "bias / activation epilogues only): forward, dgrad and weight "
+                                               "gradients of c_attn and c_proj, and every form the fused MLP "
+                                               "does not cover"),
+                    "fused_mlp": split(lambda k: k.split(":")[-1].startswith("mlp"),
+                                       "mlp_fwd (c_fc -> GELU -> c_proj, hidden on chip) and mlp_bwd (hidden "
+                                       "recomputed, G / dP written): their flops are the GEMMs', their time "
+                                       "includes the GELU / GELU' work"),
+                    "layernorm_fused": split(lambda k: k.split(":")[-1] in ("dgrad_ln", "linear_ln"),
+                                             "GEMMs whose 256-column tiles finish a LayerNorm (c_fc / c_attn dgrad "
+                                             "+ ln backward, c_proj + ln_2 forward): flops are the GEMMs', the "
+                                             "LayerNorm's HBM bytes are declared_bytes_per_step")}
+            for kk, vv in subs.items():
+                if vv is not None:
+                    res["encoder_gemm"][kk] = vv
         live = timer.summary()
         dom = max((k for k in live if single_kernel_key(k)), key=lambda k: live[k]["ms"])
         s = live[dom]
@@ -587,7 +633,7 @@ def main():
                            "avg_launch_ms": round(s["ms"] / s["calls"], 4), **both}
         if "kshift_fwd_k" in summ:
             g = summ["kshift_fwd_k"]
-            res["embedding_gather_c2"] = {"kernel": "kshift_fwd_k", "bound": "hbm",
+            res["embedding_gather_c2"] = {"kernel": "kshift_fwd_reg_k", "bound": "hbm",
                                           "note": "C2 tables (64 MB item, 32 x 64 MB cat) are Infinity-Cache resident",
                                           "achieved": round(g["work"] / (g["ms"] / 1000) / 1e9, 1),
                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",

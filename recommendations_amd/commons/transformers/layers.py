@@ -153,7 +153,7 @@ class TransformerBlockFn(torch.autograd.Function):
         if pr > 0.0:
             x1 = K.dropout(lin(o, wp_b, _f(bp), out_dtype=torch.float32, amax_in=am[1:2] if fp8 else None), pr,
                            seed + 1, res1=x2)
-        elif not fp8 and not _MLP_LN and K.linear_layernorm_fwd_ok(o, wp_b):
+        elif not fp8 and not _MLP_LN and K.linear_layernorm_fwd_ok(o, wp_b, _f(bp), x2, ln2w.detach(), _f(ln2b)):
             # c_proj + residual, then ln_2, in one kernel (its 256-row tiles hold whole rows)
             x1, h2f, mu2f, rs2f = K.linear_layernorm_fwd(o, wp_b, _f(bp), x2, ln2w.detach(), _f(ln2b))
             ln2_done = (h2f, mu2f, rs2f)

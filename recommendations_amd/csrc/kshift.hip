@@ -118,6 +118,88 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
   }
 }
 
+// Register-row form of kshift_fwd_k (round 6) for 16-B lane vectors and K = KT in {4, 8, 16}:
+// the LPR lanes of an item's group compute its K rows (lane gl: shifts c = gl + LPR j) and every
+// lane reads them across the group (ds_bpermute), so no LDS staging and no workgroup barrier sit
+// between two items, and the K row loads of an item issue back to back, held as raw 16-B vectors
+// (4 registers each) until the in-order sum.  Waves walk the items independently (grid-stride over
+// wave iterations of 64 / LPR items); the next iteration's id load is issued before this
+// iteration's row loads retire.  Same arithmetic as kshift_fwd_k: f32 sum in the order
+// c = 0 .. K - 1, then / sqrt(K) or / max(|v|, 1e-12).
+template <typename TW, typename TO, int KT, int LPR>
+__global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_reg_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
+                                                           const TW* __restrict__ W, int64_t P, int D, int mode,
+                                                           float scale, TO* __restrict__ out,
+                                                           float* __restrict__ norms) {
+  constexpr int NE = 16 / (int)sizeof(TW);  // elements per lane
+  constexpr int IPW = 64 / LPR;             // items per wave iteration
+  constexpr int KJ = (KT + LPR - 1) / LPR;  // rows computed per lane
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (LPR - 1), gb = lane & ~(LPR - 1), gi = lane / LPR;
+  const int64_t nwaves = (int64_t)gridDim.x * (KS_BLOCK / 64);
+  int64_t w = (int64_t)blockIdx.x * (KS_BLOCK / 64) + (threadIdx.x >> 6);
+  int64_t item = w * IPW + gi;
+  int64_t id = item < n_items ? ids[item] : 0;
+  const TW* colp = W + (size_t)gl * NE;
+  for (; w * IPW < n_items; w += nwaves) {  // wave-uniform
+    const bool valid = item < n_items;
+    const int64_t rbase = (valid && F > 1) ? (int64_t)(item % F) * P : 0;
+    uint32_t rlo[KJ], rhi[KJ];
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) {
+      const int c = gl + LPR * j;
+      const int64_t r = (valid && c < KT) ? rbase + kshift_row(id, c, P) : 0;
+      rlo[j] = (uint32_t)r;
+      rhi[j] = (uint32_t)((uint64_t)r >> 32);
+    }
+    const int64_t nitem = item + nwaves * IPW;
+    const int64_t nid = nitem < n_items ? ids[nitem] : 0;  // in flight behind this item's rows
+    u32x4 raw[KT];
+#pragma unroll
+    for (int c = 0; c < KT; ++c) {
+      const int src = gb + (c % LPR);
+      const uint64_t r = ((uint64_t)(uint32_t)__shfl((int)rhi[c / LPR], src, 64) << 32) |
+                         (uint32_t)__shfl((int)rlo[c / LPR], src, 64);
+      raw[c] = *reinterpret_cast<const u32x4*>(colp + (int64_t)r * D);
+    }
+    float acc[NE];
+#pragma unroll
+    for (int c = 0; c < KT; ++c) {
+      float v[NE];
+      if constexpr (sizeof(TW) == 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __uint_as_float(raw[c][e]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[2 * i] = __uint_as_float(raw[c][i] << 16);
+          v[2 * i + 1] = __uint_as_float(raw[c][i] & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = c == 0 ? v[e] : acc[e] + v[e];
+    }
+    if (mode == LTHM_KSHIFT_NORMALIZE) {
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) ss += acc[e] * acc[e];
+#pragma unroll
+      for (int o = LPR >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float nrm = sqrtf(ss);
+      const float den = fmaxf(nrm, 1e-12f);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / den;
+      if (valid && norms != nullptr && gl == 0) norms[item] = nrm;
+    } else if (mode == LTHM_KSHIFT_SCALE) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[e] = acc[e] / scale;
+    }
+    if (valid) store_vec<TO, NE>(out + item * D + (size_t)gl * NE, acc);
+    item = nitem;
+    id = nid;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Backward: LDS-staged dedup + wave-segmented reduction + one f32 add per
 // unique row per workgroup.
@@ -504,6 +586,35 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
     LTHM_CHECK_LAUNCH();
     return 0;
   }
+  // register-row gather: 16-B lane vectors, K 4 / 8 / 16, 4 .. 32 lanes per row (LTHM_KSHIFT_REG=0: off)
+  static const bool reg_off = getenv("LTHM_KSHIFT_REG") && getenv("LTHM_KSHIFT_REG")[0] == '0';
+  if (!reg_off && xrows == nullptr && vb == 16 && (K == 16 || K == 8 || K == 4) && l2 >= 2 && l2 <= 5) {
+    const int lpr = 1 << l2;
+    // waves: enough iterations per wave to amortise the first id load, capped at 32 blocks per CU
+    const int64_t iters = (n_items + (64 / lpr) - 1) / (64 / lpr);
+    const int gr = grid_for(iters, 4 * 2, 256 * 32);
+#define KSR_LAUNCH(KT_, LPR_)                                                                                       \
+  hipLaunchKernelGGL((kshift_fwd_reg_k<TW, TO, KT_, LPR_>), dim3(gr), dim3(KS_BLOCK), 0, s, ids, n_items, F,     \
+                     (const TW*)W, P, D, mode, scale, (TO*)out, norms)
+#define KSR_LPR(KT_)            \
+  switch (lpr) {                \
+    case 4: KSR_LAUNCH(KT_, 4); break;   \
+    case 8: KSR_LAUNCH(KT_, 8); break;   \
+    case 16: KSR_LAUNCH(KT_, 16); break; \
+    default: KSR_LAUNCH(KT_, 32); break; \
+  }
+    if (K == 16) {
+      KSR_LPR(16)
+    } else if (K == 8) {
+      KSR_LPR(8)
+    } else {
+      KSR_LPR(4)
+    }
+#undef KSR_LPR
+#undef KSR_LAUNCH
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   if (vb == 16)
     hipLaunchKernelGGL((kshift_fwd_k<TW, TO, 16>), dim3(grid), dim3(KS_BLOCK), 0, s, ids, n_items, F,
                        (const TW*)W, P, D, K, mode, scale, (TO*)out, norms, l2, xrows);
@@ -793,6 +904,9 @@ int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const
   LTHM_REQUIRE(dW && flags && list && count && dup_ws && (dy_dtype == LTHM_F32 || dy_dtype == LTHM_BF16));
   const int64_t items = n * (int64_t)F;
   LTHM_REQUIRE(dup_cap >= items + 1);
+  // the first-touch rows are copied as f32x4 stores from 4-element dY vectors
+  const int esz = dy_dtype == LTHM_F32 ? 4 : 2;
+  LTHM_REQUIRE(D % 4 != 0 || (((uintptr_t)dW % 16) == 0 && ((uintptr_t)dY % (4 * esz)) == 0));
   if (items == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   unsigned long long* ndup = (unsigned long long*)dup_ws;  // dup_ws[0]: the count, then the items

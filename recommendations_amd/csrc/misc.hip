@@ -127,23 +127,25 @@ __device__ __forceinline__ void logq_step(float& b, float& a, float idx, float a
   a = idx;
 }
 
+// one thread per (token, module) pair: the modules' probe chains (returning CAS round trips)
+// run side by side instead of one after another per token (round 6: 7 modules on C2)
 __global__ __launch_bounds__(256) void logq_insert_k(LogqArgs p) {
-  const int64_t n = p.B * p.T;
+  const int64_t n = p.B * p.T * p.n_mod;
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t bb = i / p.T, t = i % p.T;
+    const int64_t tok = i / p.n_mod;
+    const int m = (int)(i - tok * p.n_mod);
+    const int64_t bb = tok / p.T, t = tok - bb * p.T;
     if (p.mask && p.mask[bb * p.mask_stride + t]) continue;
     const int64_t id = p.ids[bb * p.ids_stride + t];
     const int mb = (int)(bb / p.mbs);
-    for (int m = 0; m < p.n_mod; ++m) {
-      const uint32_t key = (uint32_t)((int64_t)m * p.nb + logq_bucket(id, p.offs[m], p.nb));
-      uint32_t s = logq_slot0(key, p.cap_mask);
-      while (true) {
-        const uint32_t old = atomicCAS(p.keys + s, LQ_EMPTY, key);
-        if (old == LQ_EMPTY || old == key) break;
-        s = (s + 1) & p.cap_mask;
-      }
-      atomicOr(p.bits + (int64_t)s * p.n_w + (mb >> 5), 1u << (mb & 31));
+    const uint32_t key = (uint32_t)((int64_t)m * p.nb + logq_bucket(id, p.offs[m], p.nb));
+    uint32_t s = logq_slot0(key, p.cap_mask);
+    while (true) {
+      const uint32_t old = atomicCAS(p.keys + s, LQ_EMPTY, key);
+      if (old == LQ_EMPTY || old == key) break;
+      s = (s + 1) & p.cap_mask;
     }
+    atomicOr(p.bits + (int64_t)s * p.n_w + (mb >> 5), 1u << (mb & 31));
   }
 }
 
@@ -384,7 +386,7 @@ extern "C" int lthm_logq_stream(const int64_t* ids, int64_t ids_stride, const ui
     p.cap_mask = (uint32_t)(cap - 1);
     if (hipMemsetAsync(p.keys, 0xFF, cap * 4, s) != hipSuccess) return (int)hipGetLastError();
     if (hipMemsetAsync(p.bits, 0, cap * 4 * (int64_t)p.n_w, s) != hipSuccess) return (int)hipGetLastError();
-    hipLaunchKernelGGL(logq_insert_k, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(logq_insert_k, dim3(grid_for(n * n_modules, 256, 256 * 64)), dim3(256), 0, s, p);
     LTHM_CHECK_LAUNCH();
     hipLaunchKernelGGL(logq_apply_k, dim3(grid_for(cap, 256, 256 * 32)), dim3(256), 0, s, p);
     LTHM_CHECK_LAUNCH();

@@ -445,6 +445,125 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- forward, two workgroups per CU
+// mlp_fwd_k's chunk loop at 4 waves (128-row tiles) with everything that kept a second workgroup
+// off the CU removed, so that two independent workgroups share each CU and one's tile edges (the
+// x / residual loads, the output stores, the first chunk's drain) run beside the other's MFMAs:
+//  * the accumulator starts as b2 + res1 (+ res2), loaded straight into the C layout when the tile
+//    starts (register i of tile t: row 4 h + (i & 3) + 8 (i >> 2), column 32 t + r32; each
+//    half-wave reads one 128-B row piece), and leaves from the C layout the same way, so the tile
+//    end is stores only, no LDS strip and no load after a store;
+//  * W1 / W2T chunks on a 2-slot ring (prefetch distance 1): 64 KiB of images + 5 KiB of biases.
+// Two workgroups of 4 waves are 2 waves per SIMD (256 registers each, as the 8-wave form).
+template <int D, int NRES>
+__global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
+  constexpr int NW = 4, NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [slot][W1_j, W2T_j]
+  extern __shared__ float b1s[];                                         // [HID] b1, [D] b2
+  float* b2s = b1s + a.HID;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  for (int i = tid; i < D; i += NTH) b2s[i] = a.b2 ? a.b2[i] : 0.f;
+  retire_loads();
+  const int64_t ntile_wg = (re - rs + TR - 1) / TR;
+  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
+  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  __syncthreads();  // b1s / b2s
+  int g = 0;
+  int64_t tix = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR, ++tix) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform: a wave past the tile's rows only streams weights
+    bf16x8m xf[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    f32x16 acc[NT];
+    // register i of tile t holds wave row (i & 3) + 8 (i >> 2) + 4 h; rows past `last` (the wave's
+    // last row in range) read row `last` and are never stored
+    const int last = active ? (int)min((int64_t)32, lim - rb) - 1 : 0;
+    if (active) {
+      const float* r1 = a.res1 + rb * D;
+      const float* r2 = a.res2 + rb * D;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float bb = b2s[32 * t + r32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int o = min((i & 3) + 8 * (i >> 2) + 4 * h, last) * D + 32 * t + r32;
+          float v = bb;
+          if constexpr (NRES >= 1) v += r1[o];
+          if constexpr (NRES >= 2) v += r2[o];
+          acc[t][i] = v;
+        }
+      }
+    }
+    for (int j = 0; j < NC; ++j, ++g) {
+      wait_vm<0>();     // chunk g landed (a tile's first step also drains its x / residual loads)
+      __syncthreads();  // ... everywhere; every wave is done with chunk g - 1's slot
+      asm volatile("" ::: "memory");
+      if (j + 1 < NC || tix + 1 < ntile_wg) {
+        const int jn = j + 1 < NC ? j + 1 : 0;
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      }
+      if (!active) continue;
+      const unsigned char* w1 = img[g & 1][0];
+      const unsigned char* w2 = img[g & 1][1];
+      // S^T = W1_j . x^T (LDS row reads one step ahead of their MFMA)
+      f32x16 S = f32x16{};
+      {
+        bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const bf16x8m fn = mlp_row_frag<D>(w1, lane, k + 1 < KS ? k + 1 : k);
+          S = mfma32(fa, xf[k], S);
+          fa = fn;
+          asm volatile("" ::: "memory");
+        }
+      }
+      // H = bf16(GELU(S + b1_j)), Y += H . W2T_j
+      float hv[16];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[4 * m + e] = gelu_tanh(S[4 * m + e] + bb[e]);
+      }
+      const bf16x8m hf0 = mlp_pack(hv), hf1 = mlp_pack(hv + 8);
+      bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int tn = t + 1 < NT ? t + 1 : t;
+        const bf16x8m n0 = mlp_tr_frag<D>(w2, lane, 0, tn), n1 = mlp_tr_frag<D>(w2, lane, 1, tn);
+        acc[t] = mfma32(hf0, b0, acc[t]);
+        acc[t] = mfma32(hf1, b1, acc[t]);
+        b0 = n0;
+        b1 = n1;
+        asm volatile("" ::: "memory");
+      }
+    }
+    if (active) {
+      float* o = a.out + rb * D;
+      if (last == 31) {  // wave-uniform: a full 32-row wave tile
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[((i & 3) + 8 * (i >> 2) + 4 * h) * D + 32 * t + r32] = acc[t][i];
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (rr <= last) o[rr * D + 32 * t + r32] = acc[t][i];
+          }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- forward, software-pipelined
 // One wave per SIMD (4 waves, 512 registers each), the chunk stream software-pipelined inside
 // the wave so that the MFMAs and the GELU VALU of different chunks issue side by side: phase k
@@ -970,6 +1089,103 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
   }
 }
 
+// mlp_bwdp_k at 4 waves with two workgroups per CU (round 6, as mlp_fwd2_k): 2-slot W1 / W2T ring
+// (64 KiB), one 2-KiB strip per wave that g and then dp pass through, b1 in dynamic LDS: 76 KiB
+// per workgroup, so a second workgroup's chunk loop runs beside one's tile edges and store bursts.
+template <int D>
+__global__ __launch_bounds__(256, 2) void mlp_bwdp2_k(MlpBwdArgs a) {
+  constexpr int NW = 4, NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, TR = 32 * NW;
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][2][IMG];  // [stage][W1_j, W2T_j]
+  __shared__ __attribute__((aligned(16))) bf16_t stb_all[NW][32 * 32];   // g, then dp, of the chunk
+  extern __shared__ float b1s[];                                          // [HID]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int NC = a.HID / 32;
+  const int64_t rs = a.M * blockIdx.x / gridDim.x, re = a.M * (blockIdx.x + 1) / gridDim.x;
+  if (rs >= re) return;  // uniform
+  for (int i = tid; i < a.HID; i += NTH) b1s[i] = a.b1 ? a.b1[i] : 0.f;
+  bf16_t* stb = stb_all[wave];
+  retire_loads();
+  mlp_dma32<D, NTH>(img[0][0], a.W1, tid);
+  mlp_dma32<D, NTH>(img[0][1], a.W2T, tid);
+  __syncthreads();  // b1s
+  int g = 0;
+  for (int64_t t0 = rs; t0 < re; t0 += TR) {
+    const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
+    const bool active = rb < lim;  // wave-uniform
+    bf16x8m xf[KS], df[KS];
+    mlp_load_x<D, KS>(a.X, rb + r32, rb + r32 < lim, h, xf);
+    mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
+    const bool more_tiles = t0 + TR < re;
+    for (int j = 0; j < NC; ++j, ++g) {
+      wait_vm<0>();
+      __syncthreads();  // chunk j landed everywhere; every wave is done with chunk j - 1's stage
+      asm volatile("" ::: "memory");
+      if (j + 1 < NC || more_tiles) {
+        const int jn = j + 1 < NC ? j + 1 : 0;
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][0], a.W1 + (int64_t)jn * 32 * D, tid);
+        mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
+      }
+      if (!active) continue;
+      const unsigned char* w1 = img[g & 1][0];
+      const unsigned char* w2 = img[g & 1][1];
+      f32x16 S = f32x16{}, dH = f32x16{};
+      bf16x8m fa = mlp_row_frag<D>(w1, lane, 0), fb = mlp_row_frag<D>(w2, lane, 0);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int kn = k + 1 < KS ? k + 1 : k;
+        const bf16x8m na = mlp_row_frag<D>(w1, lane, kn), nb = mlp_row_frag<D>(w2, lane, kn);
+        S = mfma32(fa, xf[k], S);
+        dH = mfma32(fb, df[k], dH);
+        fa = na;
+        fb = nb;
+        asm volatile("" ::: "memory");
+      }
+      uint2 dpk[4];  // dp of the chunk, packed, until g has left the strip
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+        float gv[4], dv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float gd;
+          gv[e] = gelu_tanh_and_grad(S[4 * m + e] + bb[e], gd);
+          dv[e] = dH[4 * m + e] * gd;
+        }
+        *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) =
+            uint2{pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3])};
+        dpk[m] = uint2{pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3])};
+      }
+      // [32 tokens][32 units] bf16 out of the strip as 16-B row pieces: lane -> row l / 4 (+ 16), piece l % 4
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        bf16_t* dst = pass == 0 ? a.G : a.dP;
+        u32x4 v[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
+          v[q] = *reinterpret_cast<const u32x4*>(stb + rl * 32 + (pc ^ (8 * ((rl >> 2) & 3))));
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        if (pass == 0) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) *reinterpret_cast<uint2*>(stb + r32 * 32 + 8 * (m ^ ((r32 >> 2) & 3)) + 4 * h) = dpk[m];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
+          const int64_t row = rb + rl;
+          if (row < lim) *reinterpret_cast<u32x4*>(dst + row * a.HID + 32 * j + pc) = v[q];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 // ---------------------------------------------------------------- weight gradients (recompute)
 // dW1 = dpre^T x, dW2^T = g^T dy, db1 = colsum dpre with g / dpre recomputed per token tile and
 // never written: the loop order is the transpose of the kernels above.  A wave OWNS 32 hidden
@@ -1289,6 +1505,23 @@ static int mlp_fwd_launch(MlpArgs a, int D, void* stream) {
     LTHM_CHECK_LAUNCH();
     return 0;
   }
+  // two 4-wave workgroups per CU (mlp_fwd2_k; LTHM_MLP_FWD2=0: the 8-wave form), no ln_2 prologue
+  static const bool fwd2 = !(getenv("LTHM_MLP_FWD2") && getenv("LTHM_MLP_FWD2")[0] == '0');
+  if (fwd2 && !a.ln_w) {
+    a.ntiles = (int)((M + 127) / 128);
+    const int g2 = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count() * 2);
+    const size_t dyn2 = (size_t)(HID + D) * 4;
+    if (!a.res1 && a.res2) std::swap(a.res1, a.res2);
+    const int nres = a.res2 ? 2 : a.res1 ? 1 : 0;
+#define LTHM_MLPF2(D_)                                                                                     \
+    if (nres == 2) hipLaunchKernelGGL((mlp_fwd2_k<D_, 2>), dim3(g2), dim3(256), dyn2, s, a);               \
+    else if (nres == 1) hipLaunchKernelGGL((mlp_fwd2_k<D_, 1>), dim3(g2), dim3(256), dyn2, s, a);          \
+    else hipLaunchKernelGGL((mlp_fwd2_k<D_, 0>), dim3(g2), dim3(256), dyn2, s, a);
+    if (D == 256) { LTHM_MLPF2(256) } else { LTHM_MLPF2(128) }
+#undef LTHM_MLPF2
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   // LTHM_MLP_STAG=1: the 8-wave form with the half-chunk lag of waves 4-7 (A/B)
   static const bool stag = getenv("LTHM_MLP_STAG") && getenv("LTHM_MLP_STAG")[0] == '1';
 #define LTHM_MLPF(D_, NW_)                                                                                 \
@@ -1422,6 +1655,16 @@ extern "C" int lthm_mlp_bwd_hidden(const void* X, const void* dY, int64_t M, int
   a.b1 = b1; a.G = (bf16_t*)G; a.dP = (bf16_t*)dP;
   a.M = M; a.HID = HID;
   hipStream_t s = (hipStream_t)stream;
+  // two 4-wave workgroups per CU (mlp_bwdp2_k; LTHM_MLP_BWDP2=0: the 8-wave form)
+  static const bool p2 = !(getenv("LTHM_MLP_BWDP2") && getenv("LTHM_MLP_BWDP2")[0] == '0');
+  if (p2) {
+    const int64_t nt2 = (M + 127) / 128;
+    const int g2 = (int)std::min<int64_t>(nt2, (int64_t)mlp_cu_count() * 2);
+    if (D == 256) hipLaunchKernelGGL((mlp_bwdp2_k<256>), dim3(g2), dim3(256), (size_t)HID * 4, s, a);
+    else hipLaunchKernelGGL((mlp_bwdp2_k<128>), dim3(g2), dim3(256), (size_t)HID * 4, s, a);
+    LTHM_CHECK_LAUNCH();
+    return 0;
+  }
   constexpr int NW = 8;
   const int64_t ntiles = (M + 32 * NW - 1) / (32 * NW);
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)mlp_cu_count());

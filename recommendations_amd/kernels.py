@@ -9,6 +9,7 @@ from __future__ import annotations
 import math
 from typing import Any, Dict, Optional
 
+import collections
 import os
 
 import torch
@@ -472,6 +473,25 @@ def linear_fwd(x2d, w_bf16, bias=None, act=ACT_NONE, aux_out=None, res1=None, re
 
 
 _DGRAD_WT = os.environ.get("LTHM_DGRAD_WT", "1") == "1"
+# W^T copies of the bf16 weight operands, reused by every dgrad of one backward (the c_attn and
+# c_fc dgrads of a block run twice when the LayerNorm backward is fused into them, and the same
+# copy serves recomputed blocks): keyed by the operand object, valid while its version holds
+_WT_CACHE = collections.OrderedDict()
+_WT_CACHE_MAX = 64
+
+
+def weight_t(w_bf16: torch.Tensor) -> torch.Tensor:
+    """w_bf16.t().contiguous(), cached per operand tensor (bounded LRU; entries hold the operand,
+    so its id cannot be reused while cached, and a torch in-place write bumps its version)."""
+    ent = _WT_CACHE.get(id(w_bf16))
+    if ent is not None and ent[0] is w_bf16 and ent[1] == w_bf16._version:
+        _WT_CACHE.move_to_end(id(w_bf16))
+        return ent[2]
+    wt = w_bf16.t().contiguous()
+    _WT_CACHE[id(w_bf16)] = (w_bf16, w_bf16._version, wt)
+    while len(_WT_CACHE) > _WT_CACHE_MAX:
+        _WT_CACHE.popitem(last=False)
+    return wt
 
 
 def linear_dgrad(dy2d, w_bf16, act_grad=ACT_NONE, aux=None, out_dtype=torch.bfloat16, res1=None):
@@ -482,7 +502,7 @@ def linear_dgrad(dy2d, w_bf16, act_grad=ACT_NONE, aux=None, out_dtype=torch.bflo
     M, N = dy2d.shape
     K_ = w_bf16.shape[1]
     if _DGRAD_WT:
-        wt = w_bf16.t().contiguous()
+        wt = weight_t(w_bf16)
         return gemm(dy2d, wt, M, K_, N, act=act_grad, aux=aux, out_dtype=out_dtype, res1=res1)
     return gemm(dy2d, w_bf16, M, K_, N, a_kcontig=True, b_kcontig=False, ldb=K_, act=act_grad, aux=aux,
                 out_dtype=out_dtype, res1=res1)
@@ -720,7 +740,7 @@ def dgrad_layernorm_bwd(dy2d, w_bf16, x2d, w, mean, rstd, res1=None, res2=None, 
     _need(mean, M, "mean")
     _need(rstd, M, "rstd")
     _check(not res1_twice or res1 is not None, "dgrad_layernorm_bwd(res1_twice) needs res1")
-    wt = w_bf16.t().contiguous()
+    wt = weight_t(w_bf16)
     tiles = int(load().lthm_dgrad_layernorm_bwd_tiles(M))
     part = torch.empty((2, tiles, D), dtype=torch.float32, device=x2d.device)
     dx = torch.empty((M, D), dtype=torch.float32, device=x2d.device)
@@ -743,19 +763,34 @@ _LN_DGRAD = os.environ.get("LTHM_LN_DGRAD", "1") != "0"
 _LN_LINEAR = os.environ.get("LTHM_LN_LINEAR", "1") != "0"
 
 
-def linear_layernorm_fwd_ok(x2d, w_bf16) -> bool:
-    """Shapes lthm_linear_layernorm_fwd takes: output width 256, K a multiple of 64, aligned."""
+def _ln_epi_operands_ok(M, bias, res1, ln_w, ln_b):
+    """The epilogue operands of lthm_linear_layernorm_fwd: contiguous 16-B aligned f32 of the
+    right size (bias / ln_b may be absent, ln_w may not)."""
+    if ln_w is None:
+        return False
+    for t, n in ((bias, 256), (ln_w, 256), (ln_b, 256), (res1, M * 256)):
+        if t is not None and not (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
+                                  and t.numel() == n):
+            return False
+    return True
+
+
+def linear_layernorm_fwd_ok(x2d, w_bf16, bias=None, res1=None, ln_w=None, ln_b=None, check_epi=True) -> bool:
+    """Shapes lthm_linear_layernorm_fwd takes: output width 256, K a multiple of 64, aligned, and
+    (check_epi) f32 epilogue operands it can read directly -- a caller whose residual or LayerNorm
+    parameters fail this drops to the unfused GEMM + LayerNorm path instead of raising."""
     M, Kd = x2d.shape
     return (_LN_LINEAR and tuple(w_bf16.shape) == (256, Kd) and Kd % 64 == 0 and x2d.dtype == torch.bfloat16
             and w_bf16.dtype == torch.bfloat16 and x2d.is_contiguous() and w_bf16.is_contiguous()
-            and x2d.data_ptr() % 16 == 0 and w_bf16.data_ptr() % 16 == 0)
+            and x2d.data_ptr() % 16 == 0 and w_bf16.data_ptr() % 16 == 0
+            and (not check_epi or _ln_epi_operands_ok(M, bias, res1, ln_w, ln_b)))
 
 
 def linear_layernorm_fwd(x2d, w_bf16, bias, res1, ln_w, ln_b):
     """x1 = res1 + x W^T + bias (f32) and LayerNorm(x1) in one kernel (lthm_linear_layernorm_fwd)
     -> (x1 f32 [M, 256], h bf16 [M, 256], mean, rstd)."""
     require_gpu(x2d, w_bf16)
-    _check(linear_layernorm_fwd_ok(x2d, w_bf16), "linear_layernorm_fwd: unsupported shapes")
+    _check(linear_layernorm_fwd_ok(x2d, w_bf16, check_epi=False), "linear_layernorm_fwd: unsupported shapes")
     M, Kd = x2d.shape
     for t, n, nm in ((bias, 256, "bias"), (ln_w, 256, "ln weight"), (ln_b, 256, "ln bias"), (res1, M * 256, "res1")):
         _check(t is None or (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
@@ -933,6 +968,8 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=
 # ----------------------------------------------------------------- sparse KShift backward
 # LTHM_KSHIFT_FIRST=0 keeps the all-atomic K = 1 table backward (A/B switch)
 _KSHIFT_FIRST = os.environ.get("LTHM_KSHIFT_FIRST", "1") != "0"
+# duplicate-list workspaces of the first-touch backward, one per (device, stream): word 0 is the
+# kernel's duplicate counter, so two tables' backwards on different streams must not share one
 _dup_ws = {}
 
 
@@ -962,10 +999,11 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
         if not ids.numel():
             return
         # first-touch rows stored, repeats added afterwards (lthm_kshift_bwd_sparse_first)
-        ws = _dup_ws.get(ids.device)
+        key = (ids.device, torch.cuda.current_stream(ids.device).cuda_stream)
+        ws = _dup_ws.get(key)
         if ws is None or ws.numel() < ids.numel() + 1:
             ws = torch.empty(ids.numel() + 1, dtype=torch.int64, device=ids.device)
-            _dup_ws[ids.device] = ws
+            _dup_ws[key] = ws
         call("lthm_kshift_bwd_sparse_first", ptr(ids), n, F, ptr(gy), dcode(gy), P, D, ptr(dW), ptr(flags),
              ptr(rows_list), ptr(count), ptr(ws), ws.numel(), stream())
         return

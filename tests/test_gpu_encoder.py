@@ -638,7 +638,10 @@ def test_linear_layernorm_fwd_vs_fp64(dev, M, Kd, bias, res):
     lw = torch.randn(256, generator=g) * 0.3 + 1
     lb = torch.randn(256, generator=g) * 0.1
     d = lambda t: None if t is None else t.to(dev)
-    assert K.linear_layernorm_fwd_ok(d(x), d(W))
+    assert K.linear_layernorm_fwd_ok(d(x), d(W), d(b), d(r), d(lw), d(lb))
+    # an operand the epilogue cannot read directly sends the caller to the unfused path
+    assert not K.linear_layernorm_fwd_ok(d(x), d(W), d(b), d(torch.randn(M, 256).to(torch.bfloat16)), d(lw), d(lb))
+    assert not K.linear_layernorm_fwd_ok(d(x), d(W), d(b), d(r), None, d(lb))
     x1, h, mu, rs = K.linear_layernorm_fwd(d(x), d(W), d(b), d(r), d(lw), d(lb))
     torch.cuda.synchronize()
     want = x.double() @ W.double().T

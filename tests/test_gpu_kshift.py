@@ -76,6 +76,34 @@ def test_kshift_vs_oracle_sizes(dev, P, D, Kk, F, wdt):
         np.testing.assert_allclose(dW[f * P:(f + 1) * P], e, rtol=1e-4, atol=2e-6 * np.abs(e).max() + 1e-5)
 
 
+@pytest.mark.parametrize("P,D,Kk,F,wdt", [(1_000_003, 32, 16, 1, torch.bfloat16), (200_000, 128, 16, 1, torch.bfloat16),
+                                          (60_000, 256, 16, 1, torch.bfloat16), (80_000, 64, 8, 3, torch.bfloat16),
+                                          (90_000, 16, 4, 1, torch.float32), (50_001, 64, 16, 2, torch.float32)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_kshift_register_rows_vs_oracle(dev, P, D, Kk, F, wdt, mode):
+    """The register-row gather (kshift_fwd_reg_k: 16-B lane vectors, 4 .. 32 lanes per row,
+    K 4 / 8 / 16) in every output mode, ragged last wave iteration (n not a multiple of the
+    items per iteration), bf16 and f32 outputs: bit-exact to the C oracle in scale / none mode
+    (same in-order f32 sum), 1e-6 after the L2 normalisation."""
+    from recommendations_amd import kernels as K
+    g = torch.Generator().manual_seed(P + D + mode)
+    n = 20011 // F
+    ids = torch.randint(-(2 ** 63), 2 ** 63 - 1, (n, F), generator=g, dtype=torch.int64)
+    ids[::5] = torch.randint(0, 2 ** 62, (len(ids[::5]), F), generator=g, dtype=torch.int64)  # non-negative too
+    ids[::7] = 0
+    W = torch.randn(F * P, D, generator=g).to(wdt)
+    Wf = W.float().numpy()
+    exp = np.stack([ref.kshift_fwd_c(ids[:, f].numpy(), Wf[f * P:(f + 1) * P], Kk, mode) for f in range(F)], 1)
+    out = K.kshift(ids.to(dev), W.to(dev), P, Kk, mode, F=F, out_dtype=torch.float32).cpu().numpy()
+    if mode == 1:
+        np.testing.assert_allclose(out, exp, rtol=1e-6, atol=1e-7)
+    else:
+        np.testing.assert_array_equal(out, exp)
+    ob = K.kshift(ids.to(dev), W.to(dev), P, Kk, mode, F=F, out_dtype=torch.bfloat16).float().cpu()
+    if mode != 1:
+        np.testing.assert_array_equal(ob.numpy(), torch.from_numpy(exp).to(torch.bfloat16).float().numpy())
+
+
 def test_empty_and_errors(dev):
     from recommendations_amd import kernels as K
     W = torch.randn(10, 8, device=dev)

@@ -81,6 +81,7 @@ def main():
             return K.mlp_bwd_dx(x, dy, w1, b1, w2t), K.mlp_wgrad(x, dy, w1, b1, w2t)
         for name, fn, parts in (("bwd_chain_r4", chain4, None),
                                 ("bwd_chain_r5", chain5, None),
+                                ("bwd_hidden", lambda: K.mlp_bwd(x, dy, w1, b1, w2t, want_dx=False), 2.0),
                                 ("bwd_dx", lambda: K.mlp_bwd_dx(x, dy, w1, b1, w2t), 3.0),
                                 ("bwd_wgrad", lambda: K.mlp_wgrad(x, dy, w1, b1, w2t), 4.0)):
             if only and name not in only:
