@@ -31,7 +31,7 @@ FP8_PEAK_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md 
 # Kernel-timer key (one C-ABI call) -> the gfx950 kernels that call launches, as
 # named in the rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/*_pmc_summary.json).
 # the newest committed counter passes over the default (C2) bench
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_summary.json") for r in (5, 4, 3))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_summary.json") for r in (6, 5, 4, 3))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03_pmc_summary.json"))
 PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call key launches
     "cl_fr32_k": ["cl_fr32_k", "cl_fr32v_k"],
@@ -50,8 +50,9 @@ PMC_KERNELS = {  # kernel-name prefixes (rocprofv3 short names) each C-ABI call 
     "cve_tab_bwd_k": ["cve_tab_bwd_k<", "seg_tab_reduce_k"],
     "lthm_product_tower_fwd": ["ptower_"],
     # the fused MLP calls (tagged enc:mlp_*): each is ONE kernel of one shape
-    "mlp_fwd": ["mlp_fwd_k<"],
-    "mlp_bwd": ["mlp_bwdp_k<", "mlp_bwd_k<", "mlp_bwdx_k<"],
+    "mlp_fwd": ["mlp_fwd_k<", "mlp_fwd2_k<"],
+    "mlp_bwd": ["mlp_bwdp_k<", "mlp_bwdp2_k<", "mlp_bwd_k<", "mlp_bwdx_k<"],
+    "kshift_fwd_k": ["kshift_fwd_k<", "kshift_fwd_reg_k<", "kshift_fwd_k1_k<"],
     "mlp_wgrad": ["mlp_wgrad_k<"],
 }
 PMC_STEPS = 3  # tools/pmc_passes.sh profiles `bench.py --steps 2 --warmup 1 --no-kernel-timing`
@@ -63,12 +64,19 @@ PMC_STEPS = 3  # tools/pmc_passes.sh profiles `bench.py --steps 2 --warmup 1 --n
 # (one launch per layer, every layer the same M x d x 4d), so they compete.
 MULTI_KERNEL_KEYS = {"cl_fwd_k", "cl_bwd_k", "lthm_product_tower_fwd", "cve_tab_bwd_k", "attn_bwd_k"}
 SINGLE_KERNEL_TAGGED = ("mlp_fwd", "mlp_bwd", "mlp_wgrad")
+# the attention backward is ONE kernel (attn_bwd32_k, one workgroup per (b, h)) at T' <= 256 (C2,
+# C3, C1); past that it is the rows / columns pair plus the delta pass.  Set from the config.
+ATTN_BWD_SINGLE = [False]
 
 
 def single_kernel_key(k: str) -> bool:
     if k.startswith("enc:"):
         return k.split(":")[-1] in SINGLE_KERNEL_TAGGED
+    if k == "attn_bwd_k" and ATTN_BWD_SINGLE[0]:
+        return True
     return not (k in MULTI_KERNEL_KEYS or k.startswith("gemm_k<") or k == "gemm_fp8")
+
+
 PROF_STEPS = 2  # untimed per-kernel profiling steps between warm-up and the timed region
 
 
@@ -375,6 +383,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cfgd = dict(CONFIGS[args.config], name=args.config.upper())
+    ATTN_BWD_SINGLE[0] = cfgd.get("T") is not None and cfgd["T"] + 1 <= 256
     if args.batch:
         cfgd["B"] = args.batch
     cfgd["ckpt"] = bool(args.checkpointing)

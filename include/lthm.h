@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 40 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 41 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -710,6 +710,17 @@ int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int64_t max_row
 int lthm_sparse_adagrad(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
                         float* g, float* state_sum, int32_t* flags, float lr, float lr_decay, float eps,
                         int64_t step, void* bf16_shadow, void* stream);
+/* lthm_sparse_adamw / lthm_sparse_adagrad with keep_grad = 1: the consumed gradient rows are NOT
+ * re-zeroed -- for tables whose next backward overwrites a row at its first touch
+ * (lthm_kshift_bwd_sparse_first with a touched-row bitmap the caller clears after the step), so the
+ * zero store is dead traffic; keep_grad = 0 is the plain entry point.  Round 6 (ABI 41). */
+int lthm_sparse_adamw_ex(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                         float* g, float* m, float* v, int32_t* flags, float lr, float beta1, float beta2,
+                         float eps, float weight_decay, int64_t step, void* bf16_shadow, int32_t keep_grad,
+                         void* stream);
+int lthm_sparse_adagrad_ex(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                           float* g, float* state_sum, int32_t* flags, float lr, float lr_decay, float eps,
+                           int64_t step, void* bf16_shadow, int32_t keep_grad, void* stream);
 /* *out_accum += sum(x^2) */
 int lthm_sumsq(const void* x, int32_t dtype, int64_t n, float* out_accum, void* stream);
 /* max_norm <= 0: y = x / (sqrt(*sumsq) + add_eps)   (cap_gradients, commons/functional.py:23)

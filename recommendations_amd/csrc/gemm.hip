@@ -1173,6 +1173,13 @@ constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k 
 //    ln_fwd_v4_k's arithmetic (two-pass statistics, the same lane layout) gives the bf16
 //    LayerNorm output and the row statistics.
 constexpr int PP_PLAIN = 0, PP_LNB = 1, PP_LNF = 2;
+// rows per wave whose LayerNorm-epilogue loads (x / residuals) are in flight together: the
+// epilogue is a chain of HBM round trips, 16 rows per wave and half in 16 / PP_EPR of them
+// (round 6: 8, was 4; LTHM_PP_EPR=4 rebuilds the old form)
+#ifndef LTHM_PP_EPR
+#define LTHM_PP_EPR 8
+#endif
+constexpr int PP_EPR = LTHM_PP_EPR;
 struct LnbArgs {
   const float* x;      // LNB: LayerNorm input [M, 256] f32
   const float* w;      // LayerNorm weight [256]
@@ -1350,11 +1357,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
         if (L.b) load_vec<float, 16>(L.b + c, lb);
         if (L.bias) load_vec<float, 16>(L.bias + c, bb);
 #pragma unroll 1
-        for (int q0 = 0; q0 < 16; q0 += 4) {
-          float r1[4][4];
-          int64_t grow[4];
+        for (int q0 = 0; q0 < 16; q0 += PP_EPR) {
+          float r1[PP_EPR][4];
+          int64_t grow[PP_EPR];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < PP_EPR; ++u) {
             const int t = wave * 16 + q0 + u;
             grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
             const int64_t gr = grow[u] < g.M ? grow[u] : 0;
@@ -1363,7 +1370,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
             if (L.res1) load_vec<float, 16>(L.res1 + gr * 256 + c, r1[u]);
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < PP_EPR; ++u) {
             const int t = wave * 16 + q0 + u;
             const f32x4 a4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
             float v[4] = {a4.x + bb[0], a4.y + bb[1], a4.z + bb[2], a4.w + bb[3]};
@@ -1397,13 +1404,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
           }
         }
       } else {
-        // wave w: staged rows 16 w .. 16 w + 15, four rows' loads in flight at a time
+        // wave w: staged rows 16 w .. 16 w + 15, PP_EPR rows' loads in flight at a time
   #pragma unroll 1
-        for (int q0 = 0; q0 < 16; q0 += 4) {
-          float xv[4][4], r1[4][4], r2[4][4], mu[4], rs[4];
-          int64_t grow[4];
+        for (int q0 = 0; q0 < 16; q0 += PP_EPR) {
+          float xv[PP_EPR][4], r1[PP_EPR][4], r2[PP_EPR][4], mu[PP_EPR], rs[PP_EPR];
+          int64_t grow[PP_EPR];
   #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < PP_EPR; ++u) {
             const int t = wave * 16 + q0 + u;
             grow[u] = m0 + (t >> 6) * 128 + hb * 64 + (t & 63);
             const bool ok = grow[u] < g.M;
@@ -1417,7 +1424,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_k(GemmArgs g, int tiles_m, int
             rs[u] = L.rstd[gr];
           }
   #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < PP_EPR; ++u) {
             const int t = wave * 16 + q0 + u;
             const f32x4 d4 = *reinterpret_cast<const f32x4*>(T + t * 256 + (c ^ (((t >> 2) & 3) << 4)));
             const float d[4] = {d4.x, d4.y, d4.z, d4.w};

@@ -455,6 +455,9 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
 //    end is stores only, no LDS strip and no load after a store;
 //  * W1 / W2T chunks on a 2-slot ring (prefetch distance 1): 64 KiB of images + 5 KiB of biases.
 // Two workgroups of 4 waves are 2 waves per SIMD (256 registers each, as the 8-wave form).
+#ifndef LTHM_MLPF2_PF
+#define LTHM_MLPF2_PF 1
+#endif
 template <int D, int NRES>
 __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
   constexpr int NW = 4, NTH = 64 * NW, IMG = 32 * D * 2, KS = D / 16, NT = D / 32, TR = 32 * NW;
@@ -483,9 +486,8 @@ __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
     // register i of tile t holds wave row (i & 3) + 8 (i >> 2) + 4 h; rows past `last` (the wave's
     // last row in range) read row `last` and are never stored
     const int last = active ? (int)min((int64_t)32, lim - rb) - 1 : 0;
-    if (active) {
+    if (active) {  // acc = b2 + res1 (res2 joins in the epilogue, where the registers are free)
       const float* r1 = a.res1 + rb * D;
-      const float* r2 = a.res2 + rb * D;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const float bb = b2s[32 * t + r32];
@@ -494,7 +496,6 @@ __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
           const int o = min((i & 3) + 8 * (i >> 2) + 4 * h, last) * D + 32 * t + r32;
           float v = bb;
           if constexpr (NRES >= 1) v += r1[o];
-          if constexpr (NRES >= 2) v += r2[o];
           acc[t][i] = v;
         }
       }
@@ -511,9 +512,19 @@ __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
       if (!active) continue;
       const unsigned char* w1 = img[g & 1][0];
       const unsigned char* w2 = img[g & 1][1];
-      // S^T = W1_j . x^T (LDS row reads one step ahead of their MFMA)
+      // S^T = W1_j . x^T (LDS row reads LTHM_MLPF2_PF steps ahead of their MFMA)
       f32x16 S = f32x16{};
-      {
+      if (LTHM_MLPF2_PF >= 2) {
+        bf16x8m fa = mlp_row_frag<D>(w1, lane, 0), fb = mlp_row_frag<D>(w1, lane, 1);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const bf16x8m fn = mlp_row_frag<D>(w1, lane, k + 2 < KS ? k + 2 : KS - 1);
+          S = mfma32(fa, xf[k], S);
+          fa = fb;
+          fb = fn;
+          asm volatile("" ::: "memory");
+        }
+      } else {
         bf16x8m fa = mlp_row_frag<D>(w1, lane, 0);
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
@@ -546,6 +557,23 @@ __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
     }
     if (active) {
       float* o = a.out + rb * D;
+      if constexpr (NRES >= 2) {  // + res2, two column tiles' loads in flight at a time
+        const float* r2 = a.res2 + rb * D;
+#pragma unroll
+        for (int t = 0; t < NT; t += 2) {
+          float rv[2][16];
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              rv[u][i] = r2[min((i & 3) + 8 * (i >> 2) + 4 * h, last) * D + 32 * (t + u) + r32];
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[t + u][i] += rv[u][i];
+          asm volatile("" ::: "memory");
+        }
+      }
       if (last == 31) {  // wave-uniform: a full 32-row wave tile
 #pragma unroll
         for (int t = 0; t < NT; ++t)

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
                                                       int64_t max_rows, int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                       float* __restrict__ v, int32_t* __restrict__ flags, float lr, float b1,
                                                       float b2, float eps, float wd, float bc1, float bc2_sqrt,
-                                                      bf16_t* __restrict__ shadow) {
+                                                      bf16_t* __restrict__ shadow, int zero_grad) {
   const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
   // D <= 64 dividing 64: 64 / D rows per wave (all lanes busy); else one row per wave
   const int lane = threadIdx.x & 63;
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void sparse_adamw_k(const int64_t* __restrict_
       v[i] = vi;
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
-      g[i] = 0.f;
+      if (zero_grad) g[i] = 0.f;
     }
     if (flags && d0 == 0) flags[r] = 0;
   }
@@ -146,7 +146,9 @@ __device__ __forceinline__ void st4bf(bf16_t* p, const float (&v)[4]) {
   *reinterpret_cast<u32x2*>(p) = w;
 }
 
-template <bool ADAM>
+// ZG: re-zero each consumed gradient row (off when the next backward overwrites a row's first
+// touch: the K = 1 first-touch tables, lthm_sparse_*_ex keep_grad)
+template <bool ADAM, bool ZG>
 __global__ __launch_bounds__(256) void sparse_opt_v4_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
                                                        int64_t max_rows, int D, float* __restrict__ p,
                                                        float* __restrict__ g, float* __restrict__ m,
@@ -181,8 +183,10 @@ __global__ __launch_bounds__(256) void sparse_opt_v4_k(const int64_t* __restrict
     st4f(m + i, mi);
     st4f(p + i, pi);
     if (shadow) st4bf(shadow + i, pi);
-    const float z[4] = {0.f, 0.f, 0.f, 0.f};
-    st4f(g + i, z);
+    if constexpr (ZG) {
+      const float z[4] = {0.f, 0.f, 0.f, 0.f};
+      st4f(g + i, z);
+    }
     if (flags && d0 == 0) flags[r] = 0;
     r = rn;
   }
@@ -198,7 +202,7 @@ static bool sparse_v4_ok(int D, const void* a, const void* b, const void* c, con
 __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restrict__ rows, const int64_t* __restrict__ count,
                                                         int64_t max_rows, int D, float* __restrict__ p, float* __restrict__ g, float* __restrict__ s,
                                                         int32_t* __restrict__ flags, float clr, float eps,
-                                                        bf16_t* __restrict__ shadow) {
+                                                        bf16_t* __restrict__ shadow, int zero_grad) {
   const int64_t cnt = min(*count, max_rows);  // never past the row-list capacity
   const int lane = threadIdx.x & 63;
   const int rpw = (D <= 64 && 64 % D == 0) ? 64 / D : 1;
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(256) void sparse_adagrad_k(const int64_t* __restric
       s[i] = si;
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
-      g[i] = 0.f;
+      if (zero_grad) g[i] = 0.f;
     }
     if (flags && d0 == 0) flags[r] = 0;
   }
@@ -300,21 +304,57 @@ extern "C" int lthm_adagrad(float* p, float* g, float* state_sum, int64_t n, flo
   return 0;
 }
 
-extern "C" int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p, float* g,
-                                 float* m, float* v, int32_t* flags, float lr, float beta1, float beta2, float eps,
-                                 float weight_decay, int64_t step, void* bf16_shadow, void* stream) {
+extern "C" int lthm_sparse_adamw_ex(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                                    float* g, float* m, float* v, int32_t* flags, float lr, float beta1, float beta2,
+                                    float eps, float weight_decay, int64_t step, void* bf16_shadow, int32_t keep_grad,
+                                    void* stream) {
   LTHM_REQUIRE(D > 0 && step >= 1 && max_rows >= 0);
   if (max_rows == 0) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
   if (sparse_v4_ok(D, p, g, m, v, bf16_shadow)) {
     const int rpw = 256 / D;
-    hipLaunchKernelGGL(sparse_opt_v4_k<true>, dim3(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16)), dim3(256), 0,
-                       (hipStream_t)stream, rows, count, max_rows, D, p, g, m, v, flags, lr, beta1, beta2, eps,
-                       weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+    const dim3 grid(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16));
+    if (keep_grad)
+      hipLaunchKernelGGL((sparse_opt_v4_k<true, false>), grid, dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
+                         p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+    else
+      hipLaunchKernelGGL((sparse_opt_v4_k<true, true>), grid, dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
+                         p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
   } else {
     hipLaunchKernelGGL(sparse_adamw_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count, max_rows, D,
-                       p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow);
+                       p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), (bf16_t*)bf16_shadow,
+                       keep_grad ? 0 : 1);
+  }
+  LTHM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p, float* g,
+                                 float* m, float* v, int32_t* flags, float lr, float beta1, float beta2, float eps,
+                                 float weight_decay, int64_t step, void* bf16_shadow, void* stream) {
+  return lthm_sparse_adamw_ex(rows, count, max_rows, D, p, g, m, v, flags, lr, beta1, beta2, eps, weight_decay, step,
+                              bf16_shadow, 0, stream);
+}
+
+extern "C" int lthm_sparse_adagrad_ex(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
+                                      float* g, float* state_sum, int32_t* flags, float lr, float lr_decay, float eps,
+                                      int64_t step, void* bf16_shadow, int32_t keep_grad, void* stream) {
+  LTHM_REQUIRE(D > 0 && step >= 1 && max_rows >= 0);
+  if (max_rows == 0) return 0;
+  const float clr = lr / (1.f + (float)(step - 1) * lr_decay);
+  if (sparse_v4_ok(D, p, g, state_sum, nullptr, bf16_shadow)) {
+    const int rpw = 256 / D;
+    const dim3 grid(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16));
+    if (keep_grad)
+      hipLaunchKernelGGL((sparse_opt_v4_k<false, false>), grid, dim3(256), 0, (hipStream_t)stream, rows, count, max_rows,
+                         D, p, g, state_sum, nullptr, flags, clr, 0.f, 0.f, eps, 0.f, 1.f, 1.f, (bf16_t*)bf16_shadow);
+    else
+      hipLaunchKernelGGL((sparse_opt_v4_k<false, true>), grid, dim3(256), 0, (hipStream_t)stream, rows, count, max_rows,
+                         D, p, g, state_sum, nullptr, flags, clr, 0.f, 0.f, eps, 0.f, 1.f, 1.f, (bf16_t*)bf16_shadow);
+  } else {
+    hipLaunchKernelGGL(sparse_adagrad_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count,
+                       max_rows, D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow, keep_grad ? 0 : 1);
   }
   LTHM_CHECK_LAUNCH();
   return 0;
@@ -323,20 +363,8 @@ extern "C" int lthm_sparse_adamw(const int64_t* rows, const int64_t* count, int6
 extern "C" int lthm_sparse_adagrad(const int64_t* rows, const int64_t* count, int64_t max_rows, int32_t D, float* p,
                                    float* g, float* state_sum, int32_t* flags, float lr, float lr_decay, float eps,
                                    int64_t step, void* bf16_shadow, void* stream) {
-  LTHM_REQUIRE(D > 0 && step >= 1 && max_rows >= 0);
-  if (max_rows == 0) return 0;
-  const float clr = lr / (1.f + (float)(step - 1) * lr_decay);
-  if (sparse_v4_ok(D, p, g, state_sum, nullptr, bf16_shadow)) {
-    const int rpw = 256 / D;
-    hipLaunchKernelGGL(sparse_opt_v4_k<false>, dim3(grid_for((max_rows + rpw - 1) / rpw, 4, 256 * 16)), dim3(256), 0,
-                       (hipStream_t)stream, rows, count, max_rows, D, p, g, state_sum, nullptr, flags, clr, 0.f, 0.f,
-                       eps, 0.f, 1.f, 1.f, (bf16_t*)bf16_shadow);
-  } else {
-    hipLaunchKernelGGL(sparse_adagrad_k, dim3(grid_for(max_rows, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, rows, count,
-                       max_rows, D, p, g, state_sum, flags, clr, eps, (bf16_t*)bf16_shadow);
-  }
-  LTHM_CHECK_LAUNCH();
-  return 0;
+  return lthm_sparse_adagrad_ex(rows, count, max_rows, D, p, g, state_sum, flags, lr, lr_decay, eps, step, bf16_shadow,
+                                0, stream);
 }
 
 extern "C" int lthm_sumsq(const void* x, int32_t dtype, int64_t n, float* out_accum, void* stream) {

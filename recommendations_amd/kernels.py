@@ -915,8 +915,9 @@ def attn_fwd_qkv(qkv, B, T, H, E, table=None, causal=True, mask=None, pack=None)
     k = qkv[:, C:]
     v = qkv[:, 2 * C:]
     d = _attn_desc(q, k, v, B, T, H, E, out, lse, table, causal, 3 * C, 3 * C, E, mask, pack=pack)
+    # compulsory HBM bytes: q / k / v read, out written (bf16 rows), lse written
     call("lthm_attn_fwd", ctypes.addressof(d), stream(), _key="attn_fwd_k", _work=4.0 * B * H * T * T * E,
-         _unit="flop")
+         _unit="flop", _bytes=float(4 * qkv.shape[0] * C * 2 + B * H * T * 4))
     return out, lse
 
 
@@ -955,8 +956,9 @@ def attn_bwd_qkv(qkv, out, dout, lse, B, T, H, E, table=None, causal=True, mask=
         chain = torch.empty((B * (pack.P + 1), 2 * C), dtype=torch.bfloat16, device=qkv.device)
         d.dk_chain, d.dv_chain, d.chain_ts, d.chain_rows = ptr(chain), ptr(chain[:, C:]), 2 * C, pack.P + 1
     d.dtable_part, d.delta = ptr(part), ptr(delta)
+    # compulsory HBM bytes: q / k / v, out and dout read, dq / dk / dv written (bf16 rows), lse read
     call("lthm_attn_bwd", ctypes.addressof(d), stream(), _key="attn_bwd_k", _work=10.0 * B * H * T * T * E,
-         _unit="flop")
+         _unit="flop", _bytes=float(8 * qkv.shape[0] * C * 2 + B * H * T * 4))
     if chain is not None:
         pack.chain_sum(chain, 2 * C, pack.P + 1, dqkv[:, C:])
     dtab = None
@@ -1079,23 +1081,26 @@ def _touched_work(count, max_rows, per_row):
     return lambda: float(min(int(snap.item()), max_rows)) * per_row
 
 
-def sparse_adamw_(rows, count, max_rows, p, g, m, v, flags, lr, betas, eps, wd, step, shadow=None):
+def sparse_adamw_(rows, count, max_rows, p, g, m, v, flags, lr, betas, eps, wd, step, shadow=None, keep_grad=False):
+    """Row-wise AdamW over the touched rows (lthm_sparse_adamw_ex).  keep_grad: the gradient rows
+    are not re-zeroed (first-touch tables: the next backward overwrites them)."""
     _check_sparse_rows(rows, max_rows, p, flags, g, m, v, shadow)
     D = p.shape[1]
-    # per touched row: its index, p / g / m / v read, p / m / v written, g zeroed, the touched flag,
-    # the bf16 shadow row
-    per_row = 8 + 4 + 8 * 4 * D + (2 * D if shadow is not None else 0)
-    call("lthm_sparse_adamw", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(m), ptr(v),
-         ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), stream(), _key="lthm_sparse_adamw",
-         _work=_touched_work(count, max_rows, per_row), _unit="byte")
+    # per touched row: its index, p / g / m / v read, p / m / v written, g zeroed (unless kept), the
+    # touched flag, the bf16 shadow row
+    per_row = 8 + 4 + (7 if keep_grad else 8) * 4 * D + (2 * D if shadow is not None else 0)
+    call("lthm_sparse_adamw_ex", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(m), ptr(v),
+         ptr(flags), lr, betas[0], betas[1], eps, wd, step, ptr(shadow), int(keep_grad), stream(),
+         _key="lthm_sparse_adamw", _work=_touched_work(count, max_rows, per_row), _unit="byte")
 
 
-def sparse_adagrad_(rows, count, max_rows, p, g, s, flags, lr, lr_decay, eps, step, shadow=None):
+def sparse_adagrad_(rows, count, max_rows, p, g, s, flags, lr, lr_decay, eps, step, shadow=None, keep_grad=False):
     _check_sparse_rows(rows, max_rows, p, flags, g, s, shadow)
     D = p.shape[1]
-    per_row = 8 + 4 + 6 * 4 * D + (2 * D if shadow is not None else 0)  # p / g / s read, p / s written, g zeroed
-    call("lthm_sparse_adagrad", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(s), ptr(flags),
-         lr, lr_decay, eps, step, ptr(shadow), stream(), _key="lthm_sparse_adagrad",
+    # p / g / s read, p / s written, g zeroed (unless kept)
+    per_row = 8 + 4 + (5 if keep_grad else 6) * 4 * D + (2 * D if shadow is not None else 0)
+    call("lthm_sparse_adagrad_ex", ptr(rows), ptr(count), max_rows, D, ptr(p), ptr(g), ptr(s), ptr(flags),
+         lr, lr_decay, eps, step, ptr(shadow), int(keep_grad), stream(), _key="lthm_sparse_adagrad",
          _work=_touched_work(count, max_rows, per_row), _unit="byte")
 
 

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Iterable
 
+import os
+
 import torch
 
 from . import kernels as K
@@ -109,6 +111,11 @@ class FusedAdagrad(torch.optim.Optimizer):
         return loss
 
 
+# LTHM_SPARSE_KEEP_GRAD=0: the bitmap tables' row-wise step re-zeroes the gradient rows as the
+# int32-flag tables' does (A/B of lthm_sparse_*_ex keep_grad)
+_KEEP_GRAD = os.environ.get("LTHM_SPARSE_KEEP_GRAD", "1") != "0"
+
+
 def _clear_touched(m, bits):
     """After a row-wise step: the touched-row list is consumed; a touched-row bitmap (K = 1
     tables, F * P / 8 bytes) is cleared whole, int32 flags were re-zeroed per row by the kernel."""
@@ -139,9 +146,10 @@ class SparseRowAdamW:
                                           K.zeros(m.weight.shape, torch.float32, m.weight.device))
             shadow = m.shadow_current()
             bits = getattr(m, "sparse_flag_bits", False)
+            # a bitmap table's next backward stores each row at its first touch: no re-zeroing
             K.sparse_adamw_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
                             m.sparse_grad, st[0], st[1], None if bits else m.sparse_flags, self.lr, self.betas,
-                            self.eps, self.weight_decay, self.step_count, shadow=shadow)
+                            self.eps, self.weight_decay, self.step_count, shadow=shadow, keep_grad=bits and _KEEP_GRAD)
             _clear_touched(m, bits)
 
     def zero_grad(self, set_to_none: bool = True):
@@ -166,5 +174,5 @@ class SparseRowAdagrad(SparseRowAdamW):
             bits = getattr(m, "sparse_flag_bits", False)
             K.sparse_adagrad_(m.sparse_rows, m.sparse_count, min(m.sparse_pending, m.weight.shape[0]), m.weight.data,
                               m.sparse_grad, st, None if bits else m.sparse_flags, self.lr, self.lr_decay, self.eps,
-                              self.step_count, shadow=shadow)
+                              self.step_count, shadow=shadow, keep_grad=bits and _KEEP_GRAD)
             _clear_touched(m, bits)

@@ -197,3 +197,35 @@ def test_sparse_row_optimizers_16b_form(dev, D, adam):
     torch.testing.assert_close(m1[rows], me, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(p1[rows], pe, rtol=1e-5, atol=1e-6)
     assert torch.equal(s1[rows], p1[rows].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("mis", [False, True])
+@pytest.mark.parametrize("adam", [True, False])
+def test_sparse_row_optimizers_keep_grad(dev, adam, mis):
+    """lthm_sparse_adamw_ex / lthm_sparse_adagrad_ex with keep_grad = 1 (the first-touch tables'
+    step, round 6): the same parameters, moments and shadow bit for bit as the re-zeroing step
+    (16-byte and per-element forms), and the gradient rows left as they were."""
+    from recommendations_amd import kernels as K
+    torch.manual_seed(7 + adam)
+    R, n, D = 4000, 1500, 32
+    rows = torch.randperm(R, device=dev)[:n].to(torch.int64)
+    count = torch.tensor([n], dtype=torch.int64, device=dev)
+    f = _misaligned if mis else (lambda t: t.clone())
+    p0, g0 = torch.randn(R, D, device=dev), torch.randn(R, D, device=dev)
+    m0, v0 = torch.rand(R, D, device=dev), torch.rand(R, D, device=dev) * 0.01
+    outs = []
+    for keep in (False, True):
+        p, g, m, v = f(p0), f(g0), f(m0), f(v0)
+        sh = torch.zeros(R, D, dtype=torch.bfloat16, device=dev)
+        if adam:
+            K.sparse_adamw_(rows, count, n, p, g, m, v, None, 1e-2, (0.9, 0.999), 1e-8, 0.01, 2, shadow=sh,
+                            keep_grad=keep)
+        else:
+            K.sparse_adagrad_(rows, count, n, p, g, m, None, 1e-2, 0.0, 1e-10, 2, shadow=sh, keep_grad=keep)
+        torch.cuda.synchronize()
+        outs.append((p, g, m, v, sh))
+    (p1, g1, m1, v1, s1), (p2, g2, m2, v2, s2) = outs
+    for a, b in ((p1, p2), (m1, m2), (v1, v2), (s1, s2)):
+        assert torch.equal(a, b)
+    assert int((g1[rows] != 0).sum()) == 0
+    assert torch.equal(g2, g0)

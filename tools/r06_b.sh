@@ -3,7 +3,7 @@
 # MLP forward (tests + A/B) and the row-wise AdamW layout probe
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r06b
-timeout -k 10 500 python -u -m pytest tests/test_gpu_kshift.py tests/test_gpu_encoder.py tests/test_gpu_mlp.py -x -q --timeout 300 --timeout-method thread -k "kshift or golden or linear_layernorm or flat or rows or mlp" > gpurun_out/r06b/tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kshift.py tests/test_gpu_encoder.py tests/test_gpu_mlp.py tests/test_gpu_optim.py -x -q --timeout 300 --timeout-method thread -k "kshift or golden or linear_layernorm or flat or rows or mlp or sparse" > gpurun_out/r06b/tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r06b/tests.log; [ $rc -eq 0 ] || { grep -E "^FAILED|^E " gpurun_out/r06b/tests.log | head -30; exit $rc; }
 timeout -k 10 300 python -u -m pytest tests/test_gpu_loss_golden.py -q -s --timeout 200 --timeout-method thread > gpurun_out/r06b/tests_loss.log 2>&1
 rc=$?; tail -2 gpurun_out/r06b/tests_loss.log; grep -E "NaN|^FAILED" gpurun_out/r06b/tests_loss.log | head; [ $rc -le 1 ] || exit $rc

@@ -56,3 +56,20 @@ if [ "${LADDER:-0}" = 1 ]; then
   unset LTHM_LIB_PATH
   cat $L
 fi
+if [ "${GATHER:-0}" = 1 ]; then
+  bash tools/pmc_gather.sh || exit 1
+  cp gpurun_out/pmc_gather/gather_pmc.json gpurun_out/${TAG}_gather_pmc.json
+  cat gpurun_out/pmc_gather/summary.txt | head -30
+fi
+if [ "${C4PROF:-0}" = 1 ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_c4prof -o run -- python3 bench.py --config c4 --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-gather --no-kernel-timing > gpurun_out/${TAG}_c4prof.log 2>&1 || exit 1
+  python3 tools/rocpd_stats.py $(find gpurun_out/${TAG}_c4prof -name "*.db" | head -1) 30 > gpurun_out/${TAG}_c4_kernel_stats.txt 2>&1
+  head -12 gpurun_out/${TAG}_c4_kernel_stats.txt
+  rm -rf gpurun_out/${TAG}_c4prof
+fi
+if [ "${C5PROF:-0}" = 1 ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_c5prof -o run -- python3 bench.py --config c5 --steps 3 --warmup 2 --no-cpu-baseline --no-hbm-gather --no-kernel-timing > gpurun_out/${TAG}_c5prof.log 2>&1 || exit 1
+  python3 tools/rocpd_stats.py $(find gpurun_out/${TAG}_c5prof -name "*.db" | head -1) 30 > gpurun_out/${TAG}_c5_kernel_stats.txt 2>&1
+  head -12 gpurun_out/${TAG}_c5_kernel_stats.txt
+  rm -rf gpurun_out/${TAG}_c5prof
+fi
