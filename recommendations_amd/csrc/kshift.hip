@@ -586,9 +586,9 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
     LTHM_CHECK_LAUNCH();
     return 0;
   }
-  // register-row gather: 16-B lane vectors, K 4 / 8 / 16, 4 .. 32 lanes per row (LTHM_KSHIFT_REG=0: off)
-  static const bool reg_off = getenv("LTHM_KSHIFT_REG") && getenv("LTHM_KSHIFT_REG")[0] == '0';
-  if (!reg_off && xrows == nullptr && vb == 16 && (K == 16 || K == 8 || K == 4) && l2 >= 2 && l2 <= 5) {
+  // register-row gather: 16-B lane vectors, K 4 / 8 / 16, 4 .. 32 lanes per row (LTHM_KSHIFT_REG=1: on)
+  static const bool reg_on = getenv("LTHM_KSHIFT_REG") && getenv("LTHM_KSHIFT_REG")[0] == '1';
+  if (reg_on && xrows == nullptr && vb == 16 && (K == 16 || K == 8 || K == 4) && l2 >= 2 && l2 <= 5) {
     const int lpr = 1 << l2;
     // waves: enough iterations per wave to amortise the first id load, capped at 32 blocks per CU
     const int64_t iters = (n_items + (64 / lpr) - 1) / (64 / lpr);

@@ -1533,8 +1533,8 @@ static int mlp_fwd_launch(MlpArgs a, int D, void* stream) {
     LTHM_CHECK_LAUNCH();
     return 0;
   }
-  // two 4-wave workgroups per CU (mlp_fwd2_k; LTHM_MLP_FWD2=0: the 8-wave form), no ln_2 prologue
-  static const bool fwd2 = !(getenv("LTHM_MLP_FWD2") && getenv("LTHM_MLP_FWD2")[0] == '0');
+  // two 4-wave workgroups per CU (mlp_fwd2_k; LTHM_MLP_FWD2=1: on), no ln_2 prologue
+  static const bool fwd2 = getenv("LTHM_MLP_FWD2") && getenv("LTHM_MLP_FWD2")[0] == '1';
   if (fwd2 && !a.ln_w) {
     a.ntiles = (int)((M + 127) / 128);
     const int g2 = std::min<int64_t>(a.ntiles, (int64_t)mlp_cu_count() * 2);
@@ -1683,8 +1683,8 @@ extern "C" int lthm_mlp_bwd_hidden(const void* X, const void* dY, int64_t M, int
   a.b1 = b1; a.G = (bf16_t*)G; a.dP = (bf16_t*)dP;
   a.M = M; a.HID = HID;
   hipStream_t s = (hipStream_t)stream;
-  // two 4-wave workgroups per CU (mlp_bwdp2_k; LTHM_MLP_BWDP2=0: the 8-wave form)
-  static const bool p2 = !(getenv("LTHM_MLP_BWDP2") && getenv("LTHM_MLP_BWDP2")[0] == '0');
+  // two 4-wave workgroups per CU (mlp_bwdp2_k; LTHM_MLP_BWDP2=1: on)
+  static const bool p2 = getenv("LTHM_MLP_BWDP2") && getenv("LTHM_MLP_BWDP2")[0] == '1';
   if (p2) {
     const int64_t nt2 = (M + 127) / 128;
     const int g2 = (int)std::min<int64_t>(nt2, (int64_t)mlp_cu_count() * 2);

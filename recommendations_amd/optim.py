@@ -111,9 +111,9 @@ class FusedAdagrad(torch.optim.Optimizer):
         return loss
 
 
-# LTHM_SPARSE_KEEP_GRAD=0: the bitmap tables' row-wise step re-zeroes the gradient rows as the
-# int32-flag tables' does (A/B of lthm_sparse_*_ex keep_grad)
-_KEEP_GRAD = os.environ.get("LTHM_SPARSE_KEEP_GRAD", "1") != "0"
+# LTHM_SPARSE_KEEP_GRAD=1: the bitmap tables' row-wise step leaves the gradient rows (the next
+# backward stores them at their first touch); 0 re-zeroes them as the int32-flag tables' step does
+_KEEP_GRAD = os.environ.get("LTHM_SPARSE_KEEP_GRAD", "0") == "1"
 
 
 def _clear_touched(m, bits):

@@ -15,13 +15,14 @@ print(sys.argv[2], j['ms_per_step'], 'mlp_fwd', f('enc:mlp_fwd'), 'mlp_bwd', f('
       'linear_ln', f('enc:linear_ln'), 'logq', f('logq_stream'), 'kshift_fwd', f('kshift_fwd_k'))
 PY
 }
+L8=LTHM_LIB_PATH=$GRAFT_REPO_ROOT/recommendations_amd/liblthm_hip_EPR8.so
 run base LTHM_X=1 || exit 1
-run nofwd2 LTHM_MLP_FWD2=0 || exit 1
-run nobwdp2 LTHM_MLP_BWDP2=0 || exit 1
-run epr4 LTHM_LIB_PATH=$GRAFT_REPO_ROOT/recommendations_amd/liblthm_hip_EPR4.so || exit 1
-run pf2 LTHM_LIB_PATH=$GRAFT_REPO_ROOT/recommendations_amd/liblthm_hip_PF2.so || exit 1
+run fwd2 LTHM_MLP_FWD2=1 || exit 1
+run bwdp2 LTHM_MLP_BWDP2=1 || exit 1
+run epr8 $L8 || exit 1
+run all LTHM_MLP_FWD2=1 LTHM_MLP_BWDP2=1 LTHM_KSHIFT_REG=1 $L8 || exit 1
 run base2 LTHM_X=1 || exit 1
-timeout -k 10 300 python bench.py --config c4 --steps 20 --warmup 5 --no-hbm-gather --no-cpu-baseline > gpurun_out/r06c/c4.log 2>&1 || { tail -20 gpurun_out/r06c/c4.log; exit 1; }
+LTHM_SPARSE_KEEP_GRAD=1 timeout -k 10 300 python bench.py --config c4 --steps 20 --warmup 5 --no-hbm-gather --no-cpu-baseline > gpurun_out/r06c/c4.log 2>&1 || { tail -20 gpurun_out/r06c/c4.log; exit 1; }
 tail -c 300 gpurun_out/r06c/c4.log; echo
 LTHM_SPARSE_KEEP_GRAD=0 timeout -k 10 300 python bench.py --config c4 --steps 20 --warmup 5 --no-hbm-gather --no-cpu-baseline > gpurun_out/r06c/c4_zg.log 2>&1 || { tail -20 gpurun_out/r06c/c4_zg.log; exit 1; }
 tail -c 300 gpurun_out/r06c/c4_zg.log; echo
