@@ -1175,9 +1175,10 @@ constexpr int PP_HALF = 128 * 128;  // bytes of one half image (128 rows x 64 k 
 constexpr int PP_PLAIN = 0, PP_LNB = 1, PP_LNF = 2;
 // rows per wave whose LayerNorm-epilogue loads (x / residuals) are in flight together: the
 // epilogue is a chain of HBM round trips, 16 rows per wave and half in 16 / PP_EPR of them
-// (round 6: -DLTHM_PP_EPR=8 builds the deeper form)
+// (round 6: 8, was 4: dgrad_ln 0.574 / 0.568 -> 0.565 ms per C2 call, profiles/r06c/; -DLTHM_PP_EPR=4
+// rebuilds the old form)
 #ifndef LTHM_PP_EPR
-#define LTHM_PP_EPR 4
+#define LTHM_PP_EPR 8
 #endif
 constexpr int PP_EPR = LTHM_PP_EPR;
 struct LnbArgs {
