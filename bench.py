@@ -184,7 +184,10 @@ def build(cfgd, dev):
     torch.manual_seed(1234)  # identical replicas on every rank
     if cfgd.get("kind") == "ranker":
         from recommendations_amd.models.ranker.config import ranker_config
-        cfg = ranker_config(n_dense=cfgd["n_dense"], n_cat=cfgd["n_cat"], cat_vocab=cfgd["cat_vocab"])
+        # LTHM_C4_GATHER_BF16=1: the K = 1 tables gather from a bf16 shadow the row-wise step keeps
+        # (the same bf16 outputs; round 5's default, A/B)
+        cfg = ranker_config(n_dense=cfgd["n_dense"], n_cat=cfgd["n_cat"], cat_vocab=cfgd["cat_vocab"],
+                            cat_gather_bf16=os.environ.get("LTHM_C4_GATHER_BF16", "0") == "1")
         with torch.device(dev):  # 64 x 1M x 32 tables drawn on the device
             model = cfg.get_builder().build()
         return cfg, model

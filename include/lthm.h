@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 41 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 42 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -65,6 +65,12 @@ int lthm_kshift_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtyp
 int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* W,
                           int32_t w_dtype, int64_t P, int32_t D, int32_t K, int32_t mode,
                           void* out, int32_t out_dtype, float* norms, void* stream);
+/* lthm_kshift_fwd_multi writing item (b, f)'s row at out + b * out_ld + f * D (elements): the F x D
+ * rows of a sample inside a wider row, e.g. the ranker's MLP input [dense | F tables], built without a
+ * concatenation pass (round 6, ABI 42).  out_ld > F * D needs K = 1. */
+int lthm_kshift_fwd_multi_ld(const int64_t* ids, int64_t n, int32_t F, const void* W, int32_t w_dtype, int64_t P,
+                             int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, int64_t out_ld,
+                             float* norms, void* stream);
 
 /* Item-embedding artifact forward (embedding_module_gen.py:32-41 ModelWrapper, consumed
  * at encoder.py:25-29 via torch.jit.load): out[i] = KShift_K(ids[i]; W [P, D], mode)
@@ -114,6 +120,11 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
 int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
                                  int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list, int64_t* count,
                                  int64_t* dup_ws, int64_t dup_cap, void* stream);
+/* lthm_kshift_bwd_sparse_first reading item (b, f)'s gradient row at dY + b * dy_ld + f * D
+ * (the gradient of the strided lthm_kshift_fwd_multi_ld output, in place in the wider row). */
+int lthm_kshift_bwd_sparse_first_ld(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                                    int64_t dy_ld, int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list,
+                                    int64_t* count, int64_t* dup_ws, int64_t dup_cap, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* GEMM: every nn.Linear on the path (commons/transformers/layers.py:240-241,   */

@@ -509,11 +509,19 @@ static int launch_item_artifact(const int64_t* ids, int64_t n, const void* W, in
 // flight before the first store (the general kernel holds one row load per lane between two
 // barriers).  Same per-item arithmetic (the row, /1 or L2-normalised), no LDS.
 constexpr int KS1_U = 8;
+// element offset of item (b, f) = item of a [B, F, D] output / gradient whose F x D row block has
+// leading dimension ld (ld = F D: contiguous; larger: the block sits inside a wider row, e.g. the
+// ranker's MLP input [dense | F D table rows], round 6)
+__device__ __forceinline__ int64_t k1_item_off(int64_t item, int F, int D, int64_t ld) {
+  if (ld == (int64_t)F * D) return item * D;
+  const int64_t b = item / F;
+  return b * ld + (item - b * F) * D;
+}
 template <typename TW, typename TO, int VB>
 __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k1_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
                                                           const TW* __restrict__ W, int64_t P, int D, int mode,
                                                           TO* __restrict__ out, float* __restrict__ norms,
-                                                          int LPR_LOG2) {
+                                                          int LPR_LOG2, int64_t out_ld) {
   constexpr int NE = VB / (int)sizeof(TW);
   const int LPR = 1 << LPR_LOG2;
   const int lane = threadIdx.x & 63;
@@ -552,14 +560,17 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k1_k(const int64_t* __res
 #pragma unroll
         for (int e = 0; e < NE; ++e) v[u][e] = v[u][e] / 1.f;
       }
-      if (rows[u] >= 0) store_vec<TO, NE>(out + (base + u) * D + (size_t)gl * NE, v[u]);
+      if (rows[u] >= 0) store_vec<TO, NE>(out + k1_item_off(base + u, F, D, out_ld) + (size_t)gl * NE, v[u]);
     }
   }
 }
 
 template <typename TW, typename TO>
 static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W, int64_t P, int D, int K,
-                      int mode, void* out, float* norms, hipStream_t s, const int64_t* xrows = nullptr) {
+                      int mode, void* out, float* norms, hipStream_t s, const int64_t* xrows = nullptr,
+                      int64_t out_ld = 0) {
+  if (out_ld == 0) out_ld = (int64_t)F * D;
+  const bool strided = out_ld != (int64_t)F * D;  // only the K = 1 kernel writes strided rows
   int l2 = 0;
   const int vb = pick_vb(D, (int)sizeof(TW), &l2);
   LTHM_REQUIRE(vb > 0);
@@ -570,17 +581,18 @@ static int launch_fwd(const int64_t* ids, int64_t n_items, int F, const void* W,
   const int grid = grid_for(n_items, ipb, 256 * 32);
   const float scale = (float)__builtin_sqrt((double)K);
   static const bool k1_off = getenv("LTHM_KSHIFT_K1") && getenv("LTHM_KSHIFT_K1")[0] == '0';  // A/B
+  LTHM_REQUIRE(!strided || (K == 1 && xrows == nullptr && !k1_off && out_ld >= (int64_t)F * D));
   if (K == 1 && xrows == nullptr && !k1_off) {
     const int g1 = grid_for(n_items, ipb * KS1_U, 256 * 32);
     if (vb == 16)
       hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 16>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
-                         P, D, mode, (TO*)out, norms, l2);
+                         P, D, mode, (TO*)out, norms, l2, out_ld);
     else if (vb == 8)
       hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 8>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
-                         P, D, mode, (TO*)out, norms, l2);
+                         P, D, mode, (TO*)out, norms, l2, out_ld);
     else if (vb == 4)
       hipLaunchKernelGGL((kshift_fwd_k1_k<TW, TO, 4>), dim3(g1), dim3(KS_BLOCK), 0, s, ids, n_items, F, (const TW*)W,
-                         P, D, mode, (TO*)out, norms, l2);
+                         P, D, mode, (TO*)out, norms, l2, out_ld);
     else
       return (int)hipErrorInvalidValue;
     LTHM_CHECK_LAUNCH();
@@ -687,7 +699,7 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_first_k(const int64_t* __re
                                                              int64_t* __restrict__ list,
                                                              unsigned long long* __restrict__ count,
                                                              int64_t* __restrict__ dups,
-                                                             unsigned long long* __restrict__ ndup) {
+                                                             unsigned long long* __restrict__ ndup, int64_t dy_ld) {
   __shared__ int64_t s_new[K1_CHUNK];
   __shared__ int64_t s_dup[K1_CHUNK];
   __shared__ int s_nnew, s_ndup;
@@ -734,10 +746,10 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_first_k(const int64_t* __re
         if (it < c1 && pv == 0) {
           if (VEC == 4) {
             float g[4];
-            load_vec<TY, 4 * (int)sizeof(TY)>(dY + it * D + c, g);
+            load_vec<TY, 4 * (int)sizeof(TY)>(dY + k1_item_off(it, F, D, dy_ld) + c, g);
             *reinterpret_cast<f32x4*>(dW + r * D + c) = f32x4{g[0], g[1], g[2], g[3]};
           } else {
-            dW[r * D + c] = Elem<TY>::ld(dY + it * D + c);
+            dW[r * D + c] = Elem<TY>::ld(dY + k1_item_off(it, F, D, dy_ld) + c);
           }
         }
       }
@@ -758,7 +770,7 @@ template <typename TY>
 __global__ __launch_bounds__(256) void kshift_bwd_k1_dup_k(const int64_t* __restrict__ ids, int F,
                                                            const TY* __restrict__ dY, int64_t P, int D,
                                                            float* __restrict__ dW, const int64_t* __restrict__ dups,
-                                                           const unsigned long long* __restrict__ ndup) {
+                                                           const unsigned long long* __restrict__ ndup, int64_t dy_ld) {
   const int64_t nd = (int64_t)*ndup;
   const int lane = threadIdx.x & 63;
   const int ipw = 64 / D, il = lane / D, d = lane - il * D;
@@ -766,7 +778,7 @@ __global__ __launch_bounds__(256) void kshift_bwd_k1_dup_k(const int64_t* __rest
     if (b + il < nd) {
       const int64_t item = dups[b + il];
       const int64_t row = ((F > 1) ? (int64_t)(item % F) * P : 0) + kshift_row(ids[item], 0, P);
-      atomicAdd(dW + row * D + d, Elem<TY>::ld(dY + item * D + d));
+      atomicAdd(dW + row * D + d, Elem<TY>::ld(dY + k1_item_off(item, F, D, dy_ld) + d));
     }
   }
 }
@@ -775,17 +787,20 @@ template <typename TY, typename TO>
 static int launch_bwd(const int64_t* ids, int64_t n_items, int F, const void* dY, const void* out,
                       const float* norms, int64_t P, int D, int K, int mode, float* dW, int32_t* flags,
                       int64_t* list, unsigned long long* count, hipStream_t s, int64_t* dups = nullptr,
-                      unsigned long long* ndup = nullptr) {
+                      unsigned long long* ndup = nullptr, int64_t dy_ld = 0) {
+  if (dy_ld == 0) dy_ld = (int64_t)F * D;
   if (K == 1 && mode != LTHM_KSHIFT_NORMALIZE && D <= 64 && 64 % D == 0 && flags && dups && ndup) {
     LTHM_REQUIRE(hipMemsetAsync(ndup, 0, sizeof(unsigned long long), s) == hipSuccess);
     hipLaunchKernelGGL((kshift_bwd_k1_first_k<TY>), dim3(grid_for(n_items, K1_CHUNK, 256 * 8)), dim3(256), 0, s, ids,
-                       n_items, F, (const TY*)dY, P, D, dW, reinterpret_cast<uint32_t*>(flags), list, count, dups, ndup);
+                       n_items, F, (const TY*)dY, P, D, dW, reinterpret_cast<uint32_t*>(flags), list, count, dups, ndup,
+                       dy_ld);
     LTHM_CHECK_LAUNCH();
     hipLaunchKernelGGL((kshift_bwd_k1_dup_k<TY>), dim3(1024), dim3(256), 0, s, ids, F, (const TY*)dY, P, D, dW,
-                       (const int64_t*)dups, (const unsigned long long*)ndup);
+                       (const int64_t*)dups, (const unsigned long long*)ndup, dy_ld);
     LTHM_CHECK_LAUNCH();
     return 0;
   }
+  LTHM_REQUIRE(dy_ld == (int64_t)F * D);  // strided gradients: the first-touch path only
   if (K == 1 && mode != LTHM_KSHIFT_NORMALIZE && D <= 64 && 64 % D == 0) {
     hipLaunchKernelGGL((kshift_bwd_k1_k<TY>), dim3(grid_for(n_items, K1_CHUNK, 256 * 8)), dim3(256), 0, s, ids,
                        n_items, F, (const TY*)dY, P, D, dW, flags, list, count);
@@ -831,19 +846,19 @@ int lthm_kshift_rows(const int64_t* ids, int64_t n, int64_t P, int32_t K, int64_
 
 static int kshift_fwd_impl(const int64_t* ids, int64_t n_items, int F, const void* W, int w_dtype, int64_t P,
                            int D, int K, int mode, void* out, int out_dtype, float* norms, void* stream,
-                           const int64_t* xrows = nullptr) {
+                           const int64_t* xrows = nullptr, int64_t out_ld = 0) {
   LTHM_REQUIRE(P > 0 && K > 0 && K <= 64 && D > 0 && n_items >= 0 && F >= 1);
   LTHM_REQUIRE(mode >= 0 && mode <= 2);
   if (n_items == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (w_dtype == LTHM_F32 && out_dtype == LTHM_F32)
-    return launch_fwd<float, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
+    return launch_fwd<float, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows, out_ld);
   if (w_dtype == LTHM_F32 && out_dtype == LTHM_BF16)
-    return launch_fwd<float, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
+    return launch_fwd<float, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows, out_ld);
   if (w_dtype == LTHM_BF16 && out_dtype == LTHM_F32)
-    return launch_fwd<bf16_t, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
+    return launch_fwd<bf16_t, float>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows, out_ld);
   if (w_dtype == LTHM_BF16 && out_dtype == LTHM_BF16)
-    return launch_fwd<bf16_t, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows);
+    return launch_fwd<bf16_t, bf16_t>(ids, n_items, F, W, P, D, K, mode, out, norms, s, xrows, out_ld);
   return (int)hipErrorInvalidValue;
 }
 
@@ -861,6 +876,14 @@ int lthm_kshift_fwd_multi(const int64_t* ids, int64_t n, int32_t F, const void* 
                           int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, float* norms,
                           void* stream) {
   return kshift_fwd_impl(ids, n * (int64_t)F, F, W, w_dtype, P, D, K, mode, out, out_dtype, norms, stream);
+}
+
+int lthm_kshift_fwd_multi_ld(const int64_t* ids, int64_t n, int32_t F, const void* W, int32_t w_dtype, int64_t P,
+                             int32_t D, int32_t K, int32_t mode, void* out, int32_t out_dtype, int64_t out_ld,
+                             float* norms, void* stream) {
+  LTHM_REQUIRE(out_ld >= (int64_t)F * D && (out_ld == (int64_t)F * D || K == 1));
+  return kshift_fwd_impl(ids, n * (int64_t)F, F, W, w_dtype, P, D, K, mode, out, out_dtype, norms, stream, nullptr,
+                         out_ld);
 }
 
 int lthm_gather_pool(const int64_t* rows, int64_t n, int32_t K, const void* W, int32_t w_dtype, int64_t R, int32_t D,
@@ -897,9 +920,21 @@ int lthm_kshift_bwd_sparse(const int64_t* ids, int64_t n, int32_t F, const void*
   return (int)hipErrorInvalidValue;
 }
 
+int lthm_kshift_bwd_sparse_first_ld(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                                    int64_t dy_ld, int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list,
+                                    int64_t* count, int64_t* dup_ws, int64_t dup_cap, void* stream);
+
 int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
                                  int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list, int64_t* count,
                                  int64_t* dup_ws, int64_t dup_cap, void* stream) {
+  return lthm_kshift_bwd_sparse_first_ld(ids, n, F, dY, dy_dtype, (int64_t)F * D, P, D, dW, flags, list, count,
+                                         dup_ws, dup_cap, stream);
+}
+
+int lthm_kshift_bwd_sparse_first_ld(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                                    int64_t dy_ld, int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list,
+                                    int64_t* count, int64_t* dup_ws, int64_t dup_cap, void* stream) {
+  LTHM_REQUIRE(dy_ld >= (int64_t)F * D && (dy_ld % 4 == 0 || D % 4 != 0));
   LTHM_REQUIRE(P > 0 && D > 0 && D <= 64 && 64 % D == 0 && n >= 0 && F >= 1);
   LTHM_REQUIRE(dW && flags && list && count && dup_ws && (dy_dtype == LTHM_F32 || dy_dtype == LTHM_BF16));
   const int64_t items = n * (int64_t)F;
@@ -912,9 +947,9 @@ int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const
   unsigned long long* ndup = (unsigned long long*)dup_ws;  // dup_ws[0]: the count, then the items
   if (dy_dtype == LTHM_F32)
     return launch_bwd<float, float>(ids, items, F, dY, nullptr, nullptr, P, D, 1, LTHM_KSHIFT_SCALE, dW, flags, list,
-                                    (unsigned long long*)count, s, dup_ws + 1, ndup);
+                                    (unsigned long long*)count, s, dup_ws + 1, ndup, dy_ld);
   return launch_bwd<bf16_t, float>(ids, items, F, dY, nullptr, nullptr, P, D, 1, LTHM_KSHIFT_SCALE, dW, flags, list,
-                                   (unsigned long long*)count, s, dup_ws + 1, ndup);
+                                   (unsigned long long*)count, s, dup_ws + 1, ndup, dy_ld);
 }
 
 int lthm_item_artifact_fwd(const int64_t* ids, int64_t n, const void* W, int32_t w_dtype, int64_t P, int32_t D,

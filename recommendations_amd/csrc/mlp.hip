@@ -320,6 +320,23 @@ __device__ __forceinline__ void mlp_load_ln(const MlpArgs& a, const float* lw, c
 #ifndef LTHM_MLPF_X
 #define LTHM_MLPF_X 0
 #endif
+// LTHM_MLPF_STAMP=1 (diagnostic build, tools/build_variant.sh): mlp_fwd_k sums per wave the
+// s_memtime cycles of each phase of the chunk loop (wait + barrier, DMA issue + S issue, S
+// completion, GELU + Y issue) and of the tile epilogues into g_mlpf_stamps, read back with
+// lthm_debug_mlpf_stamps.  Timing only (the stamps' lgkmcnt waits perturb the LDS prefetch).
+#ifndef LTHM_MLPF_STAMP
+#define LTHM_MLPF_STAMP 0
+#endif
+// LTHM_MLPF_TRPF=2: W2T fragments read before the GELU and two output tiles ahead (A/B build)
+#ifndef LTHM_MLPF_TRPF
+#define LTHM_MLPF_TRPF 0
+#endif
+#if LTHM_MLPF_STAMP
+__device__ unsigned long long g_mlpf_stamps[2048 * 8 * 8];
+#define MLPF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define MLPF_T(v)
+#endif
 template <int D, int NW, bool STAG>
 __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   constexpr int NS = 3, DIST = STAG ? 1 : 2;
@@ -345,6 +362,10 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     }
   float* stg = stg_all[wave];
   retire_loads();
+#if LTHM_MLPF_STAMP
+  MLPF_T(tk0);
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   const int64_t ntile_wg = (re - rs + TR - 1) / TR;
   // chunks 0 .. DIST - 1 of the stream (chunk c: index c % NC of tile c / NC)
 #pragma unroll
@@ -375,6 +396,38 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
   };
   // H = bf16(GELU(S + b1_j)), Y += H . W2T_j
   auto gelu_out = [&](const f32x16& S, int j, const unsigned char* w2, f32x16(&acc)[NT]) {
+    if (LTHM_MLPF_TRPF >= 2) {
+      // the first two output tiles' W2T fragments are read BEFORE the GELU (they land while its
+      // VALU runs), then two tiles ahead of their MFMAs: the phase-stamp build measured the
+      // GELU + Y block at 53 % of a chunk step with the reads one tile ahead (tools/mlp_stamp.py)
+      bf16x8m b0 = mlp_tr_frag<D>(w2, lane, 0, 0), b1 = mlp_tr_frag<D>(w2, lane, 1, 0);
+      bf16x8m c0 = mlp_tr_frag<D>(w2, lane, 0, 1), c1 = mlp_tr_frag<D>(w2, lane, 1, 1);
+      u32x4 hw0, hw1;  // H packed as it is formed (no 16-float staging)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
+        float hv4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv4[e] = LTHM_MLPF_X == 2 ? S[4 * m + e] + bb[e] : gelu_tanh(S[4 * m + e] + bb[e]);
+        const uint32_t p0 = pack_bf16x2(hv4[0], hv4[1]), p1 = pack_bf16x2(hv4[2], hv4[3]);
+        if (m < 2) { hw0[2 * m] = p0; hw0[2 * m + 1] = p1; }
+        else { hw1[2 * (m - 2)] = p0; hw1[2 * (m - 2) + 1] = p1; }
+      }
+      const bf16x8m hf0 = __builtin_bit_cast(bf16x8m, hw0), hf1 = __builtin_bit_cast(bf16x8m, hw1);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int tn = t + 2 < NT ? t + 2 : NT - 1;
+        const bf16x8m n0 = mlp_tr_frag<D>(w2, lane, 0, tn), n1 = mlp_tr_frag<D>(w2, lane, 1, tn);
+        acc[t] = mfma32(hf0, b0, acc[t]);
+        acc[t] = mfma32(hf1, b1, acc[t]);
+        b0 = c0;
+        b1 = c1;
+        c0 = n0;
+        c1 = n1;
+        asm volatile("" ::: "memory");
+      }
+      return;
+    }
     float hv[16];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -408,6 +461,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
     f32x16 S = f32x16{};  // lagging waves: chunk j - 1's S across the barrier
     for (int j = 0; j < NC; ++j, ++g) {
+      MLPF_T(ts0);
       // retire chunk g; at prefetch distance 2 chunk g + 1 stays in flight (a tile's first step
       // drains: the x / residual / output accesses were issued behind the DMAs)
       if (LTHM_MLPF_X != 1) {
@@ -431,18 +485,55 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_fwd_k(MlpArgs a) {
         if (j > 0) gelu_out(S, j - 1, img[(g + NS - 1) % NS][1], acc);
         S = s_phase(img[g % NS][0], xf);
       } else {
+#if LTHM_MLPF_STAMP
+        MLPF_T(ts1);
+        const f32x16 Sj = s_phase(img[g % NS][0], xf);
+        MLPF_T(ts2);
+        {
+          float dep = Sj[15] + Sj[0];  // in-order issue: the stamp below waits for the S chain
+          asm volatile("" : "+v"(dep));
+          asm volatile("" ::"v"(dep));
+        }
+        MLPF_T(ts3);
+        gelu_out(Sj, j, img[g % NS][1], acc);
+        MLPF_T(ts4);
+        if (tix > 0) {
+          st_acc[0] += ts1 - ts0;  // wait + barrier + DMA issue
+          st_acc[1] += ts2 - ts1;  // S issue (LDS row reads)
+          st_acc[2] += ts3 - ts2;  // S completion
+          st_acc[3] += ts4 - ts3;  // GELU + Y issue
+          st_acc[4] += 1;
+        }
+#else
         const f32x16 Sj = s_phase(img[g % NS][0], xf);
         gelu_out(Sj, j, img[g % NS][1], acc);
+#endif
         S = f32x16{};  // nothing carried: keeps the loop-carried S out of this path's live range
       }
     }
+#if LTHM_MLPF_STAMP
+    MLPF_T(te0);
+#endif
     if (active) {
       if (lag) gelu_out(S, NC - 1, img[(g + NS - 1) % NS][1], acc);  // chunk g - 1: slot kept until step g + 1
       if (a.res1 && a.res2) mlp_fwd_epi<D, NT, 2>(a, acc, b2s, stg, rb, lim, lane);
       else if (a.res1) mlp_fwd_epi<D, NT, 1>(a, acc, b2s, stg, rb, lim, lane);
       else mlp_fwd_epi<D, NT, 0>(a, acc, b2s, stg, rb, lim, lane);
     }
+#if LTHM_MLPF_STAMP
+    MLPF_T(te1);
+    if (tix > 0) {
+      st_acc[5] += te1 - te0;  // tile epilogue issue
+      st_acc[6] += 1;
+    }
+#endif
   }
+#if LTHM_MLPF_STAMP
+  MLPF_T(tk);
+  st_acc[7] = tk - tk0;
+  if (lane == 0 && blockIdx.x < 2048)
+    for (int k = 0; k < 8; ++k) g_mlpf_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st_acc[k];
+#endif
 }
 
 // ---------------------------------------------------------------- forward, two workgroups per CU
@@ -608,28 +699,49 @@ __global__ __launch_bounds__(256, 2) void mlp_fwd2_k(MlpArgs a) {
 // GELU(Sp + b1) into ho (after its products are issued); DO: Y += ho . W2T.  Step i pairs S
 // MFMA i with output MFMA i (tile i / 2, k-step i % 2) and GELU element i; the LDS fragments
 // are read one step ahead (compiler fences keep the unrolled steps from hoisting every read).
+// LTHM_MLPP_PF: LDS fragment reads this many steps ahead of their MFMA (1 or 2; one wave per
+// SIMD, so an LDS read the MFMA waits on idles the matrix pipe)
+#ifndef LTHM_MLPP_PF
+#define LTHM_MLPP_PF 2
+#endif
 template <int D, bool DS, bool DG, bool DO>
 __device__ __forceinline__ void mlp_pipe_phase(const unsigned char* w1, const unsigned char* w2, const float* bj,
                                                const bf16x8m (&xf)[D / 16], f32x16 (&acc)[D / 32], f32x16& Sp,
                                                bf16x8m& ho0, bf16x8m& ho1, int lane) {
   constexpr int KS = D / 16;
+  static_assert(16 % KS == 0, "GELU elements per step");
   f32x16 Sn = f32x16{};
   float hv[16];
-  bf16x8m fa = {}, fb = {};
-  if (DS) fa = mlp_row_frag<D>(w1, lane, 0);
-  if (DO) fb = mlp_tr_frag<D>(w2, lane, 0, 0);
+  bf16x8m fa[LTHM_MLPP_PF], fb[LTHM_MLPP_PF];
+#pragma unroll
+  for (int q = 0; q < LTHM_MLPP_PF; ++q) {
+    fa[q] = fb[q] = bf16x8m{};
+    if (DS) fa[q] = mlp_row_frag<D>(w1, lane, q < KS ? q : KS - 1);
+    if (DO) fb[q] = mlp_tr_frag<D>(w2, lane, (q < KS ? q : KS - 1) & 1, (q < KS ? q : KS - 1) >> 1);
+  }
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
-    bf16x8m na = fa, nb = fb;
-    if (i + 1 < KS) {
-      if (DS) na = mlp_row_frag<D>(w1, lane, i + 1);
-      if (DO) nb = mlp_tr_frag<D>(w2, lane, (i + 1) & 1, (i + 1) >> 1);
+    const int in = i + LTHM_MLPP_PF < KS ? i + LTHM_MLPP_PF : KS - 1;
+    bf16x8m na = fa[0], nb = fb[0];
+    if (DS) na = mlp_row_frag<D>(w1, lane, in);
+    if (DO) nb = mlp_tr_frag<D>(w2, lane, in & 1, in >> 1);
+    if (DS) Sn = mfma32(fa[0], xf[i], Sn);
+    if (DO) acc[i >> 1] = mfma32((i & 1) ? ho1 : ho0, fb[0], acc[i >> 1]);
+    // 16 / KS GELU elements per step (element e: unit 8 (e >> 2) + 4 h + (e & 3) of the chunk)
+    if (DG) {
+#pragma unroll
+      for (int ee = 0; ee < 16 / KS; ++ee) {
+        const int e = i * (16 / KS) + ee;
+        hv[e] = gelu_tanh(Sp[e] + bj[8 * (e >> 2) + (e & 3)]);
+      }
     }
-    if (DS) Sn = mfma32(fa, xf[i], Sn);
-    if (DO) acc[i >> 1] = mfma32((i & 1) ? ho1 : ho0, fb, acc[i >> 1]);
-    if (DG && i < 16) hv[i] = gelu_tanh(Sp[i] + bj[8 * (i >> 2) + (i & 3)]);
-    fa = na;
-    fb = nb;
+#pragma unroll
+    for (int q = 0; q + 1 < LTHM_MLPP_PF; ++q) {
+      fa[q] = fa[q + 1];
+      fb[q] = fb[q + 1];
+    }
+    fa[LTHM_MLPP_PF - 1] = na;
+    fb[LTHM_MLPP_PF - 1] = nb;
     asm volatile("" ::: "memory");
   }
   if (DG) {
@@ -1049,6 +1161,11 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
   // the previous step issued its 4 G / dP stores AFTER the DMA of this step's chunk: a full-tile
   // wave retires the DMA with vmcnt 4, leaving its stores in flight (vmcnt retires in order)
   bool st4 = false;
+#if LTHM_MLPF_STAMP
+  MLPF_T(tk0);
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t tix = 0;
+#endif
   for (int64_t t0 = rs; t0 < re; t0 += TR) {
     const int64_t lim = min(t0 + TR, re), rb = t0 + 32 * wave;
     const bool active = rb < lim;  // wave-uniform
@@ -1058,6 +1175,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
     mlp_load_x<D, KS>(a.dY, rb + r32, rb + r32 < lim, h, df);
     const bool more_tiles = t0 + TR < re;
     for (int j = 0; j < NC; ++j, ++g) {
+      MLPF_T(ts0);
       if (st4) wait_vm<4>();
       else wait_vm<0>();
       st4 = false;
@@ -1069,6 +1187,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
         mlp_dma32<D, NTH>(img[(g + 1) & 1][1], a.W2T + (int64_t)jn * 32 * D, tid);
       }
       if (!active) continue;
+      MLPF_T(ts1);
       const unsigned char* w1 = img[g & 1][0];
       const unsigned char* w2 = img[g & 1][1];
       f32x16 S = f32x16{}, dH = f32x16{};
@@ -1083,6 +1202,15 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
         fb = nb;
         asm volatile("" ::: "memory");
       }
+#if LTHM_MLPF_STAMP
+      MLPF_T(ts2);
+      {
+        float dep = S[15] + dH[15];  // in-order issue: the stamp below waits for both chains
+        asm volatile("" : "+v"(dep));
+        asm volatile("" ::"v"(dep));
+      }
+      MLPF_T(ts3);
+#endif
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + 32 * j + 8 * m + 4 * h);
@@ -1099,6 +1227,9 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
+#if LTHM_MLPF_STAMP
+      MLPF_T(ts4);
+#endif
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int rl = (lane >> 2) + 16 * q, pc = 8 * (lane & 3);
@@ -1113,8 +1244,28 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_bwdp_k(MlpBwdArgs a) {
       st4 = full;  // every lane stored: exactly 4 store instructions issued
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
+#if LTHM_MLPF_STAMP
+      MLPF_T(ts5);
+      if (tix > 0) {
+        st_acc[0] += ts1 - ts0;  // wait + barrier + DMA issue
+        st_acc[1] += ts2 - ts1;  // S / dH issue
+        st_acc[2] += ts3 - ts2;  // S / dH completion
+        st_acc[3] += ts4 - ts3;  // GELU' + strip writes
+        st_acc[4] += 1;
+        st_acc[5] += ts5 - ts4;  // strip reads + G / dP store issue
+      }
+#endif
     }
+#if LTHM_MLPF_STAMP
+    ++tix;
+#endif
   }
+#if LTHM_MLPF_STAMP
+  MLPF_T(tk);
+  st_acc[7] = tk - tk0;
+  if (lane == 0 && blockIdx.x < 2048)
+    for (int k = 0; k < 8; ++k) g_mlpf_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st_acc[k];
+#endif
 }
 
 // mlp_bwdp_k at 4 waves with two workgroups per CU (round 6, as mlp_fwd2_k): 2-slot W1 / W2T ring
@@ -1468,6 +1619,12 @@ static int mlp_fwd_waves() {
   }
   return nw;
 }
+
+#if LTHM_MLPF_STAMP
+extern "C" int lthm_debug_mlpf_stamps(unsigned long long* host, int64_t n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mlpf_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int lthm_mlp_supported(int32_t D, int32_t HID) {
   return (D == 128 || D == 256) && HID >= 32 && HID % 32 == 0 && HID <= 8192;

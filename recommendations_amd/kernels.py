@@ -981,14 +981,23 @@ def kshift_first_touch_ok(K, mode, D) -> bool:
     return _KSHIFT_FIRST and K == 1 and mode != KSHIFT_NORMALIZE and D <= 64 and 64 % D == 0
 
 
-def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0, flag_bits=False):
+def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, count, pending=0, flag_bits=False,
+                      dy_ld=None):
     """Accumulate into dense dW and append the touched rows (see include/lthm.h).
     Table-batched layout: dW and flags cover all F*P rows; rows_list must hold
     every row that can still be appended (<= F*P, <= pending + ids*K).  flag_bits: flags is
     the touched-row bitmap of the first-touch K = 1 backward (int32 words, >= ceil(F*P / 32))."""
     require_gpu(ids, gy, out, norms, dW, flags, rows_list, count)
     D = dW.shape[1]
-    _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0], gy=gy, out=out, norms=norms)
+    if dy_ld is None:
+        _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0], gy=gy, out=out, norms=norms)
+    else:
+        # gy: a [B, F * D] view with row stride dy_ld inside a wider gradient row (the first-touch
+        # K = 1 path reads it in place: lthm_kshift_bwd_sparse_first_ld)
+        _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0])
+        _check(flag_bits and gy.dim() == 2 and gy.shape == (ids.numel() // F, F * D) and gy.stride(1) == 1
+               and gy.stride(0) == dy_ld and gy.data_ptr() % 16 == 0 and dy_ld % 4 == 0,
+               "kshift_bwd_sparse(dy_ld): a [B, F*D] row-strided view, first-touch tables only")
     _check(dW.dtype == torch.float32, "dW must be float32")
     nflag = (F * P + 31) // 32 if flag_bits else F * P
     _check(flags.dtype == torch.int32 and flags.numel() >= nflag, f"flags must be int32 with >= {nflag} entries")
@@ -1006,6 +1015,10 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
         if ws is None or ws.numel() < ids.numel() + 1:
             ws = torch.empty(ids.numel() + 1, dtype=torch.int64, device=ids.device)
             _dup_ws[key] = ws
+        if dy_ld is not None:
+            call("lthm_kshift_bwd_sparse_first_ld", ptr(ids), n, F, ptr(gy), dcode(gy), dy_ld, P, D, ptr(dW),
+                 ptr(flags), ptr(rows_list), ptr(count), ptr(ws), ws.numel(), stream())
+            return
         call("lthm_kshift_bwd_sparse_first", ptr(ids), n, F, ptr(gy), dcode(gy), P, D, ptr(dW), ptr(flags),
              ptr(rows_list), ptr(count), ptr(ws), ws.numel(), stream())
         return
@@ -1219,7 +1232,7 @@ class MLPChainFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, x2, acts, out_f32, *wb):
+    def forward(ctx, x, x2, acts, out_f32, dx_f32, *wb):
         """x2 (optional, [.., K2]): concatenated after x's features as the first GEMM's operand
         (the ranker's [dense | categorical] input, built once in bf16, the GEMM operand dtype,
         instead of as an f32 concatenation the GEMM would cast again)."""
@@ -1247,8 +1260,10 @@ class MLPChainFn(torch.autograd.Function):
             if not last:
                 hs.append(h)
         ctx.save_for_backward(*hs, *[p for p in pres if p is not None], *ws)
+        # dx_f32: the input gradient in f32 even for a bf16 input (an input assembled in bf16 whose
+        # parts want f32 gradients: RankerInputFn)
         ctx.meta = (n, acts, [p is not None for p in pres], [wb[2 * i + 1] is not None for i in range(n)], shp,
-                    x.dtype)
+                    torch.float32 if dx_f32 else x.dtype)
         return h.view(*shp[:-1], h.shape[-1])
 
     @staticmethod
@@ -1278,15 +1293,15 @@ class MLPChainFn(torch.autograd.Function):
                 dx = linear_dgrad(gb, ws[0], out_dtype=torch.float32 if xdt == torch.float32 else torch.bfloat16)
         if ctx.k1 is not None:  # the two inputs' parts of dx (x2's cast to its dtype by autograd)
             k1 = ctx.k1
-            return (dx[:, :k1].reshape(*shp[:-1], k1), dx[:, k1:], None, None, *grads)
-        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, None, *grads)
+            return (dx[:, :k1].reshape(*shp[:-1], k1), dx[:, k1:], None, None, None, *grads)
+        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, None, None, *grads)
 
 
-def mlp_chain(x, linears, acts, out_f32=True, x2=None):
+def mlp_chain(x, linears, acts, out_f32=True, x2=None, dx_f32=False):
     wb = []
     for lin in linears:
         wb += [lin.weight, lin.bias]
-    return MLPChainFn.apply(x, x2, tuple(acts), out_f32, *wb)
+    return MLPChainFn.apply(x, x2, tuple(acts), out_f32, bool(dx_f32), *wb)
 
 
 class ActivationFn(torch.autograd.Function):

@@ -38,7 +38,11 @@ class RankerModelConfig(BaseModel):
     n_categorical: int = 64
     cat_vocab: int = 1_000_000
     cat_emb_dim: int = 32
-    cat_gather_bf16: bool = True
+    # K = 1 tables gather from the fp32 master: the same bf16 outputs as a bf16 shadow (bf16(W[row])
+    # either way), and the row-wise step writes no shadow rows: C4 3.65 -> 3.48 ms per step,
+    # sparse AdamW 0.79 -> 0.65 ms, gather unchanged (random rows, not bytes, bound it;
+    # profiles/r06e/c4_g*.log)
+    cat_gather_bf16: bool = False
     gate_sizes: List[int] = [1024, 512]
     out_dim: int = 1
     lr: float = 1e-3

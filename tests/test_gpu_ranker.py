@@ -107,3 +107,42 @@ def test_ranker_c4_shape_step(dev):
     torch.cuda.synchronize()
     assert np.isfinite(float(loss))
     assert not torch.equal(w0, m._model.interaction.model[0].weight.detach())
+
+
+@pytest.mark.parametrize("B,E", [(1000, 16), (4099, 64)])
+def test_tables_into_row_matches_concat(dev, B, E):
+    """TablesIntoRowFn (round 6: the ranker's MLP input built in one bf16 row buffer by the strided
+    K = 1 gather, lthm_kshift_fwd_multi_ld; the tables' gradient read in place by
+    lthm_kshift_bwd_sparse_first_ld) against the concatenation path on the same weights and batch:
+    logits and the dense input's gradient bit-identical (same bf16 operand, same GEMMs); the table
+    gradient rows equal to the f32 input gradient's columns summed per row (the concat path rounds
+    that gradient to bf16 first: within 1e-2 of it)."""
+    from recommendations_amd import kernels as K
+    from recommendations_amd.commons.layers import MLP, TableBatchedKShiftEmbedding, TablesIntoRowFn
+    torch.manual_seed(B)
+    F_, P, D = 4, 997, 32
+    res = []
+    for into in (False, True):
+        torch.manual_seed(B)
+        tab = TableBatchedKShiftEmbedding(F_, P, D, num_shifts=1, normalize_output=False, sparse=True,
+                                          out_dtype=torch.bfloat16).to(dev)
+        mlp = MLP(E + F_ * D, 1, [64, 32]).to(dev)
+        g = torch.Generator().manual_seed(B + 1)
+        dense = torch.randn(B, E, generator=g).to(dev).requires_grad_(True)
+        ids = torch.randint(-(2 ** 62), 2 ** 62, (B, F_), generator=g).to(dev)
+        if into:
+            assert tab.into_row_ok()
+            h = TablesIntoRowFn.apply(dense, ids, tab.weight, tab, tab.gather_weight())
+            y = mlp.forward_input(h)
+        else:
+            y = mlp.forward_concat(dense, tab(ids).reshape(B, -1))
+        y.float().sum().backward()
+        torch.cuda.synchronize()
+        n = int(tab.sparse_count.item())
+        rows = tab.sparse_rows[:n].sort().values
+        res.append((y.detach().float().cpu(), dense.grad.cpu(), rows.cpu(), tab.sparse_grad[rows].cpu()))
+    (y0, d0, r0, g0), (y1, d1, r1, g1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(d0, d1)
+    assert torch.equal(r0, r1)
+    check(f"tables-into-row table gradient vs concat path (bf16-rounded) B={B}", relerr(g1, g0), 1e-2)
