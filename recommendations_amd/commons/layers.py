@@ -242,35 +242,16 @@ def _kshift_fwd_into(mod, ids, gather_w, buf, col0):
          _work=ids.numel() * (8 + D * gather_w.element_size() + D * buf.element_size()), _unit="byte")
 
 
-class TablesIntoRowFn(torch.autograd.Function):
-    """[dense | tables(ids)] as ONE bf16 row buffer [B, E + F D] (the ranker's MLP input, round 6):
-    the dense part cast in, the K = 1 table rows gathered straight into their columns.  The backward
-    reads the tables' gradient rows in place from the input gradient (f32, row stride E + F D) into
-    the first-touch sparse backward, and returns the dense part's columns as its gradient -- no
-    torch.cat forward and no strided-slice copy backward (C4: 0.20 + 0.16 ms per step)."""
-
-    @staticmethod
-    def forward(ctx, dense, ids, weight, mod, gather_w):
-        B, E = dense.shape
-        F_, D = mod._F, gather_w.shape[1]
-        buf = torch.empty((B, E + F_ * D), dtype=torch.bfloat16, device=dense.device)
-        buf[:, :E].copy_(dense)  # round to nearest even, as the chain's operand cast
-        _kshift_fwd_into(mod, ids, gather_w, buf, E)
-        ctx.mod, ctx.E = mod, E
-        ctx.save_for_backward(ids)
-        return buf
-
-    @staticmethod
-    def backward(ctx, g):
-        (ids,) = ctx.saved_tensors
-        mod, E = ctx.mod, ctx.E
-        g = g if g.stride(1) == 1 and g.stride(0) == g.shape[1] else g.contiguous()
-        mod._ensure_sparse_state(ids.numel())
-        K.kshift_bwd_sparse(ids, g[:, E:], None, None, mod._num_embeddings, 1, mod._mode, mod._F, mod.sparse_grad,
-                            mod.sparse_flags, mod.sparse_rows, mod.sparse_count, pending=mod.sparse_pending,
-                            flag_bits=mod.sparse_flag_bits, dy_ld=g.stride(0))
-        mod.sparse_pending += ids.numel()
-        return g[:, :E], None, None, None, None
+def _kshift_bwd_rows(mod, ids, g, col0):
+    """The gradient of _kshift_fwd_into's rows, read in place from g[:, col0:] (row stride
+    g.stride(0), f32 or bf16) into mod's first-touch sparse backward
+    (lthm_kshift_bwd_sparse_first_ld)."""
+    g = g if g.stride(1) == 1 else g.contiguous()
+    mod._ensure_sparse_state(ids.numel())
+    K.kshift_bwd_sparse(ids, g[:, col0:col0 + mod._F * mod.weight.shape[1]], None, None, mod._num_embeddings, 1,
+                        mod._mode, mod._F, mod.sparse_grad, mod.sparse_flags, mod.sparse_rows, mod.sparse_count,
+                        pending=mod.sparse_pending, flag_bits=mod.sparse_flag_bits, dy_ld=g.stride(0))
+    mod.sparse_pending += ids.numel()
 
 
 class _TableShardedFn(torch.autograd.Function):
@@ -343,7 +324,7 @@ class TableBatchedKShiftEmbedding(_SparseRowsMixin, nn.Module):
                         out_dtype=self._out_dtype or self.weight.dtype)
 
     def into_row_ok(self) -> bool:
-        """TablesIntoRowFn serves this module: row-wise trained K = 1 tables on one rank with the
+        """MLP.forward_rows serves this module: row-wise trained K = 1 tables on one rank with the
         first-touch backward (the strided-gradient path), under autograd."""
         return (type(self) is TableBatchedKShiftEmbedding and self.sparse and not self.replicated_dp
                 and self._num_shifts == 1 and self._mode != K.KSHIFT_NORMALIZE and self.weight.requires_grad
@@ -490,12 +471,13 @@ class MLP(nn.Module):
         return K.mlp_chain(x, lins, acts, out_f32=True, x2=x2)
 
     @torch.jit.unused
-    def forward_input(self, h: torch.Tensor) -> torch.Tensor:
-        """forward(h) for an input row buffer assembled in bf16 (TablesIntoRowFn) whose gradient is
-        wanted in f32."""
+    def forward_rows(self, x: torch.Tensor, ids: torch.Tensor, tables) -> torch.Tensor:
+        """forward_concat(x, tables(ids)) with the K = 1 table rows gathered straight into the
+        operand's columns (K.RowsInput, round 6): the same values, no concatenation pass, and the
+        tables' gradient (f32) read in place by their sparse backward."""
         lins = [m for m in self.model if isinstance(m, nn.Linear)]
         acts = [K.ACT_QGELU] * (len(lins) - 1) + [K.ACT_NONE]
-        return K.mlp_chain(h, lins, acts, out_f32=True, dx_f32=True)
+        return K.mlp_chain(x, lins, acts, out_f32=True, x2=K.RowsInput(ids, tables, tables.gather_weight()))
 
     @torch.jit.unused
     def forward_concat(self, x: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:

@@ -987,7 +987,8 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
     Table-batched layout: dW and flags cover all F*P rows; rows_list must hold
     every row that can still be appended (<= F*P, <= pending + ids*K).  flag_bits: flags is
     the touched-row bitmap of the first-touch K = 1 backward (int32 words, >= ceil(F*P / 32))."""
-    require_gpu(ids, gy, out, norms, dW, flags, rows_list, count)
+    # a row-strided gy (dy_ld) is not contiguous by design: its device is checked below
+    require_gpu(ids, gy if dy_ld is None else None, out, norms, dW, flags, rows_list, count)
     D = dW.shape[1]
     if dy_ld is None:
         _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0], gy=gy, out=out, norms=norms)
@@ -995,7 +996,7 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
         # gy: a [B, F * D] view with row stride dy_ld inside a wider gradient row (the first-touch
         # K = 1 path reads it in place: lthm_kshift_bwd_sparse_first_ld)
         _check_kshift(ids, P, K, F, D, table_rows=dW.shape[0])
-        _check(flag_bits and gy.dim() == 2 and gy.shape == (ids.numel() // F, F * D) and gy.stride(1) == 1
+        _check(flag_bits and gy.is_cuda and gy.dim() == 2 and gy.shape == (ids.numel() // F, F * D) and gy.stride(1) == 1
                and gy.stride(0) == dy_ld and gy.data_ptr() % 16 == 0 and dy_ld % 4 == 0,
                "kshift_bwd_sparse(dy_ld): a [B, F*D] row-strided view, first-touch tables only")
     _check(dW.dtype == torch.float32, "dW must be float32")
@@ -1232,16 +1233,28 @@ class MLPChainFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, x2, acts, out_f32, dx_f32, *wb):
+    def forward(ctx, x, x2, acts, out_f32, *wb):
         """x2 (optional, [.., K2]): concatenated after x's features as the first GEMM's operand
         (the ranker's [dense | categorical] input, built once in bf16, the GEMM operand dtype,
-        instead of as an f32 concatenation the GEMM would cast again)."""
+        instead of as an f32 concatenation the GEMM would cast again).  x2 may also be a
+        ``RowsInput`` (round 6): row-wise trained K = 1 tables whose lookups are gathered straight
+        into the operand's columns after x's, and whose gradient the backward hands to their
+        sparse backward in place (no concatenation, no strided-slice copy)."""
         require_gpu(x)
         shp = x.shape
         h = x.contiguous().view(-1, shp[-1])
+        ctx.k1, ctx.rows = None, None
+        if isinstance(x2, RowsInput):
+            B, E = h.shape
+            F_, D = x2.mod._F, x2.gather_w.shape[1]
+            buf = torch.empty((B, E + F_ * D), dtype=torch.bfloat16, device=x.device)
+            buf[:, :E].copy_(h)  # round to nearest even, as the operand cast below
+            x2.gather_into(buf, E)
+            ctx.k1, ctx.rows = E, x2
+            h = buf
+            shp = tuple(shp[:-1]) + (h.shape[1],)
         h = h if h.dtype == torch.bfloat16 else cast(h, torch.bfloat16)
-        ctx.k1 = None
-        if x2 is not None:
+        if x2 is not None and ctx.rows is None:
             ctx.k1 = h.shape[1]
             h = torch.cat([h, x2.reshape(h.shape[0], -1).to(torch.bfloat16)], dim=1)
             shp = tuple(shp[:-1]) + (h.shape[1],)
@@ -1260,10 +1273,8 @@ class MLPChainFn(torch.autograd.Function):
             if not last:
                 hs.append(h)
         ctx.save_for_backward(*hs, *[p for p in pres if p is not None], *ws)
-        # dx_f32: the input gradient in f32 even for a bf16 input (an input assembled in bf16 whose
-        # parts want f32 gradients: RankerInputFn)
         ctx.meta = (n, acts, [p is not None for p in pres], [wb[2 * i + 1] is not None for i in range(n)], shp,
-                    torch.float32 if dx_f32 else x.dtype)
+                    x.dtype)
         return h.view(*shp[:-1], h.shape[-1])
 
     @staticmethod
@@ -1291,17 +1302,38 @@ class MLPChainFn(torch.autograd.Function):
                 gb = linear_dgrad(gb, ws[i], act_grad=ag, aux=pres[i - 1])
             else:
                 dx = linear_dgrad(gb, ws[0], out_dtype=torch.float32 if xdt == torch.float32 else torch.bfloat16)
+        if ctx.rows is not None:  # the tables' columns of dx go to their sparse backward in place
+            k1 = ctx.k1
+            ctx.rows.backward_from(dx, k1)
+            ctx.rows = None
+            return (dx[:, :k1].reshape(*shp[:-1], k1), None, None, None, *grads)
         if ctx.k1 is not None:  # the two inputs' parts of dx (x2's cast to its dtype by autograd)
             k1 = ctx.k1
-            return (dx[:, :k1].reshape(*shp[:-1], k1), dx[:, k1:], None, None, None, *grads)
-        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, None, None, *grads)
+            return (dx[:, :k1].reshape(*shp[:-1], k1), dx[:, k1:], None, None, *grads)
+        return (dx.view(*shp[:-1], dx.shape[-1]), None, None, None, *grads)
 
 
-def mlp_chain(x, linears, acts, out_f32=True, x2=None, dx_f32=False):
+class RowsInput:
+    """Row-wise trained K = 1 tables (``mod``: TableBatchedKShiftEmbedding with ``into_row_ok``)
+    looked up by ``ids`` [B, F] as the second part of MLPChainFn's operand (see there)."""
+
+    def __init__(self, ids, mod, gather_w):
+        self.ids, self.mod, self.gather_w = ids, mod, gather_w
+
+    def gather_into(self, buf, col0):
+        from .commons.layers import _kshift_fwd_into
+        _kshift_fwd_into(self.mod, self.ids, self.gather_w, buf, col0)
+
+    def backward_from(self, dx, col0):
+        from .commons.layers import _kshift_bwd_rows
+        _kshift_bwd_rows(self.mod, self.ids, dx, col0)
+
+
+def mlp_chain(x, linears, acts, out_f32=True, x2=None):
     wb = []
     for lin in linears:
         wb += [lin.weight, lin.bias]
-    return MLPChainFn.apply(x, x2, tuple(acts), out_f32, bool(dx_f32), *wb)
+    return MLPChainFn.apply(x, x2, tuple(acts), out_f32, *wb)
 
 
 class ActivationFn(torch.autograd.Function):

@@ -19,7 +19,7 @@ from ... import kernels as K
 from ...commons.base_model_wrapper import BaseModelWrapper
 import os
 
-from ...commons.layers import MLP, TableBatchedKShiftEmbedding, TablesIntoRowFn
+from ...commons.layers import MLP, TableBatchedKShiftEmbedding
 from ...commons.transformers.layers import DenseMapper
 from ...optim import FusedAdamW, SparseRowAdamW
 
@@ -44,10 +44,8 @@ class RankerModel(nn.Module):
         e_dense = self.dense_mapper.forward_matrix(dense)              # [B, emb_dim] f32
         if _INPUT_ROW and self.cat_tables.into_row_ok():
             # the MLP input [e_dense | table rows] built in one bf16 buffer, the table rows gathered
-            # into their columns (TablesIntoRowFn): the same values as the concatenation below
-            h = TablesIntoRowFn.apply(e_dense, cat.contiguous(), self.cat_tables.weight, self.cat_tables,
-                                      self.cat_tables.gather_weight())
-            return {"logits": self.interaction.forward_input(h)}
+            # into their columns (MLP.forward_rows): the same values as the concatenation below
+            return {"logits": self.interaction.forward_rows(e_dense, cat.contiguous(), self.cat_tables)}
         e_cat = self.cat_tables(cat.contiguous())                      # [B, F, D] bf16
         # the MLP input [e_dense | e_cat] ([B, emb_dim + F*D]) is assembled in bf16 inside the MLP
         # op: the same values the first GEMM reads from an f32 concatenation, without it

@@ -111,15 +111,12 @@ def test_ranker_c4_shape_step(dev):
 
 @pytest.mark.parametrize("B,E", [(1000, 16), (4099, 64)])
 def test_tables_into_row_matches_concat(dev, B, E):
-    """TablesIntoRowFn (round 6: the ranker's MLP input built in one bf16 row buffer by the strided
-    K = 1 gather, lthm_kshift_fwd_multi_ld; the tables' gradient read in place by
+    """MLP.forward_rows (round 6: the ranker's MLP input built in one bf16 row buffer by the strided
+    K = 1 gather, lthm_kshift_fwd_multi_ld; the tables' f32 gradient read in place by
     lthm_kshift_bwd_sparse_first_ld) against the concatenation path on the same weights and batch:
     logits and the dense input's gradient bit-identical (same bf16 operand, same GEMMs); the table
-    gradient rows equal to the f32 input gradient's columns summed per row (the concat path rounds
-    that gradient to bf16 first: within 1e-2 of it)."""
-    from recommendations_amd import kernels as K
-    from recommendations_amd.commons.layers import MLP, TableBatchedKShiftEmbedding, TablesIntoRowFn
-    torch.manual_seed(B)
+    gradient rows within 1e-2 of the concat path's (which rounds that gradient to bf16 first)."""
+    from recommendations_amd.commons.layers import MLP, TableBatchedKShiftEmbedding
     F_, P, D = 4, 997, 32
     res = []
     for into in (False, True):
@@ -132,8 +129,7 @@ def test_tables_into_row_matches_concat(dev, B, E):
         ids = torch.randint(-(2 ** 62), 2 ** 62, (B, F_), generator=g).to(dev)
         if into:
             assert tab.into_row_ok()
-            h = TablesIntoRowFn.apply(dense, ids, tab.weight, tab, tab.gather_weight())
-            y = mlp.forward_input(h)
+            y = mlp.forward_rows(dense, ids, tab)
         else:
             y = mlp.forward_concat(dense, tab(ids).reshape(B, -1))
         y.float().sum().backward()
