@@ -126,6 +126,10 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_k(
 // wave iterations of 64 / LPR items); the next iteration's id load is issued before this
 // iteration's row loads retire.  Same arithmetic as kshift_fwd_k: f32 sum in the order
 // c = 0 .. K - 1, then / sqrt(K) or / max(|v|, 1e-12).
+// LTHM_KS_NT=1 (A/B build): the row loads non-temporal (read-once rows of a table far past the caches)
+#ifndef LTHM_KS_NT
+#define LTHM_KS_NT 0
+#endif
 template <typename TW, typename TO, int KT, int LPR>
 __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_reg_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
                                                            const TW* __restrict__ W, int64_t P, int D, int mode,
@@ -160,7 +164,11 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_reg_k(const int64_t* __re
       const int src = gb + (c % LPR);
       const uint64_t r = ((uint64_t)(uint32_t)__shfl((int)rhi[c / LPR], src, 64) << 32) |
                          (uint32_t)__shfl((int)rlo[c / LPR], src, 64);
+#if LTHM_KS_NT
+      raw[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(colp + (int64_t)r * D));
+#else
       raw[c] = *reinterpret_cast<const u32x4*>(colp + (int64_t)r * D);
+#endif
     }
     float acc[NE];
 #pragma unroll
