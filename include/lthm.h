@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define LTHM_ABI_VERSION 42 /* bumped on any signature / struct layout change */
+#define LTHM_ABI_VERSION 43 /* bumped on any signature / struct layout change */
 
 #define LTHM_F32 0
 #define LTHM_BF16 1
@@ -125,6 +125,26 @@ int lthm_kshift_bwd_sparse_first(const int64_t* ids, int64_t n, int32_t F, const
 int lthm_kshift_bwd_sparse_first_ld(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
                                     int64_t dy_ld, int64_t P, int32_t D, float* dW, int32_t* flags, int64_t* list,
                                     int64_t* count, int64_t* dup_ws, int64_t dup_cap, void* stream);
+
+/* Fused dedup + row-wise Adagrad of a KShift table: lthm_kshift_bwd_sparse followed by
+ * lthm_sparse_adagrad_ex in one call, with no gradient row stored.  For the item-embedding
+ * generator, whose tables step right after their backward with torch.optim.Adagrad and nothing
+ * in between (embedding_module_gen.py:137,151-153 and :97-99,113-115): the pairs (row, item) of
+ * every (item, shift) are radix-sorted by row (stable, so a row's pairs stay in item order), each
+ * row's gradient -- sum over its pairs of the item's pooled-sum gradient (dy / sqrt(K), dy, or the
+ * F.normalize backward, as lthm_kshift_bwd_sparse) -- is summed in that order and the row updated
+ * once, unfused f32:  s = s + g * g;  W = W - (clr * g) / (sqrt(s) + eps).  A row with more than
+ * 256 pairs is summed in chunks of 256 pairs, the chunk sums in 16 contiguous groups, the group
+ * sums in order (oracle/ref.py kshift_adagrad_ref restates the order).  Deterministic.
+ * clr = lr / (1 + (step - 1) * lr_decay) (torch.optim.Adagrad; no weight decay).  ids / dY / out /
+ * norms as lthm_kshift_bwd_sparse ([n, F] ids, item i of table i % F); W, state_sum [F * P, D] f32.
+ * Requires F * P <= 2^32, n * F * K < 2^31, D <= 256, K <= 64; workspace 256-B aligned, >=
+ * lthm_kshift_adagrad_ws_bytes(n * F, K, D) bytes (-1: invalid sizes). */
+int64_t lthm_kshift_adagrad_ws_bytes(int64_t n_items, int32_t K, int32_t D);
+int lthm_kshift_adagrad_fused(const int64_t* ids, int64_t n, int32_t F, const void* dY, int32_t dy_dtype,
+                              const void* out, int32_t out_dtype, const float* norms, int64_t P, int32_t D, int32_t K,
+                              int32_t mode, float* W, float* state_sum, float clr, float eps, void* workspace,
+                              int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* GEMM: every nn.Linear on the path (commons/transformers/layers.py:240-241,   */

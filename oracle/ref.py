@@ -93,6 +93,71 @@ def kshift_bwd_c(ids: np.ndarray, dY: np.ndarray, P: int, K: int, mode: int) -> 
     return acc.astype(np.float32)
 
 
+def kshift_pool_grad(dY: np.ndarray, K: int, mode: int, out: Optional[np.ndarray] = None,
+                     norms: Optional[np.ndarray] = None) -> np.ndarray:
+    """Per-item gradient of the pooled row sum (commons/layers.py:152-172 backward): mode 0
+    (scale) dy / f32(sqrt K), mode 2 (none) dy; mode 1 (normalize) in float64 (the GPU's dot
+    product runs in its own order)."""
+    dY = np.asarray(dY, np.float32)
+    if mode == 0:
+        return dY / np.float32(math.sqrt(K))
+    if mode == 2:
+        return dY.copy()
+    o = np.asarray(out, np.float64)
+    d = dY.astype(np.float64)
+    nrm = np.asarray(norms, np.float64)[:, None]
+    dot = (o * d).sum(-1, keepdims=True)
+    return np.where(nrm > 1e-12, (d - o * dot) / np.maximum(nrm, 1e-12), d / 1e-12).astype(np.float32)
+
+
+def kshift_adagrad_ref(ids: np.ndarray, g_items: np.ndarray, P: int, K: int, F: int, W: np.ndarray,
+                       S: np.ndarray, clr: float, eps: float, ch: int = 256, nw: int = 16):
+    """The KShift table backward followed by torch.optim.Adagrad's step (embedding_module_gen.py
+    :137,151-153 and :97-99: loss.backward(); optim.step(); torch.optim.Adagrad with lr_decay in clr,
+    no weight decay: state_sum += g * g; param -= clr * g / (sqrt(state_sum) + eps)), restated in
+    the summation order of lthm_kshift_adagrad_fused so that the GPU result is bit-identical:
+    the (row, item) pairs of ids [n * F] (item i in table i % F, rows kshift_rows + (i % F) P)
+    stably sorted by row; a row's gradient is the f32 sum, in that order from 0, of its items'
+    g_items rows; a row with more than `ch` pairs sums chunks of `ch` pairs, the chunk sums in `nw`
+    contiguous groups [w m // nw, (w + 1) m // nw), the group sums in order.  Every f32 operation
+    rounds on its own (no fused multiply-add).  Returns (W, S) updated copies."""
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.int64).reshape(-1))
+    n = ids.size
+    rows = kshift_rows(ids, P, K)
+    if F > 1:
+        rows = rows + (np.arange(n, dtype=np.int64) % F)[:, None] * P
+    keys = rows.reshape(-1)
+    order = np.argsort(keys, kind="stable")
+    skeys, items = keys[order], order // K
+    g = np.asarray(g_items, np.float32).reshape(n, -1)
+    W = np.array(W, dtype=np.float32, copy=True)
+    S = np.array(S, dtype=np.float32, copy=True)
+    if n == 0:
+        return W, S
+    D = g.shape[1]
+    zero = np.zeros(D, np.float32)
+
+    def seq(x):  # ((0 + x0) + x1) + ... in f32 (np.add.accumulate runs in order)
+        return np.add.accumulate(x, axis=0, dtype=np.float32)[-1] if len(x) else zero
+
+    heads = np.flatnonzero(np.r_[True, skeys[1:] != skeys[:-1]])
+    ends = np.r_[heads[1:], skeys.size]
+    c32, e32 = np.float32(clr), np.float32(eps)
+    for s0, s1 in zip(heads, ends):
+        cnt = s1 - s0
+        if cnt <= ch:
+            acc = seq(g[items[s0:s1]])
+        else:
+            m = -(-cnt // ch)
+            parts = np.stack([seq(g[items[s0 + c * ch:min(s0 + (c + 1) * ch, s1)]]) for c in range(m)])
+            acc = seq(np.stack([seq(parts[w * m // nw:(w + 1) * m // nw]) for w in range(nw)]))
+        r = skeys[s0]
+        s = S[r] + acc * acc
+        S[r] = s
+        W[r] = W[r] - (c32 * acc) / (np.sqrt(s) + e32)
+    return W, S
+
+
 def kshift_row_idx_torch(x: torch.Tensor, c: int, P: int) -> torch.Tensor:
     """commons/layers.py:174-185, torch form (arithmetic >>, wrapping <<, torch.remainder)."""
     if c != 0:

@@ -31,6 +31,10 @@ class _SparseRowsMixin:
         self.sparse_flag_bits = False
         self.sparse_pending = 0
         self.replicated_dp = False  # set by the trainer when the tables are replicated across DP ranks
+        # set by optim.SparseRowAdagrad(fused=True): the backward records its lookups for the
+        # fused dedup + Adagrad step instead of accumulating a row gradient
+        self.fused_row_step = None
+        self.fused_pending = []
 
     def _ensure_sparse_state(self, max_new_rows: int):
         w = self.weight
@@ -222,6 +226,9 @@ class _SparseKShiftFn(torch.autograd.Function):
             # (1/world-scaled) updates, so the replicas stay identical
             from ..distributed import gather_sparse_grads
             ids, gy, out, norms = gather_sparse_grads(ids, gy, out, norms)
+        if mod.fused_row_step:
+            mod.fused_pending.append((ids, gy, out, norms))  # consumed by the fused Adagrad step
+            return None, None, None, None
         _kshift_bwd_local(mod, ids, gy, out, norms)
         return None, None, None, None
 

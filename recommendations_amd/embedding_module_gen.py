@@ -11,14 +11,17 @@
   encoder consumes (encoder.py:25-29).
 
 The tables train through the touched-row path (``sparse=True``): the KShift
-backward appends the rows a batch touched and ``SparseRowAdagrad`` updates
-only those.  For Adagrad (lr_decay = 0, no weight decay) this is exactly the
+backward records the batch's lookups and ``SparseRowAdagrad(fused=True)`` forms
+each touched row's gradient and updates the row in one call (no gradient row
+stored; ``LTHM_EMBGEN_FUSED=0``: the backward stages the row gradients and the
+row-wise Adagrad updates the touched rows).  For Adagrad (lr_decay = 0, no weight decay) this is exactly the
 reference's dense update: a row with zero gradient keeps its value and its
 state sum.  The MLP uses ``FusedAdagrad``.  Batches are shuffled with a seeded
 numpy Generator (the reference uses the global ``np.random``).
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import numpy as np
@@ -31,6 +34,11 @@ from .commons.layers import MLP, KShiftEmbedding
 from .optim import FusedAdagrad, SparseRowAdagrad
 
 MAX_LONG_VALUE_PLUS_ONE = 2 ** 63
+# the tables step with the fused dedup + Adagrad (lthm_kshift_adagrad_fused): nothing reads or
+# clips their gradients between loss.backward() and optim.step() (:137,151-153 / :97-99,113-115).
+# LTHM_EMBGEN_FUSED=0: the two-pass path (row gradient staged by the backward, then the
+# row-wise Adagrad over the touched rows) for A/B runs
+_FUSED = os.environ.get("LTHM_EMBGEN_FUSED", "1") != "0"
 
 
 class ModelWrapper(nn.Module):
@@ -96,7 +104,7 @@ def train_model(df, expansion_factor: float, k_shift: int, *, num_epochs: int = 
     x = K.l2norm_rows(x.contiguous())  # F.normalize(x, p=2.0, dim=-1)
     model = KShiftEmbedding(int(expansion_factor * x.size(0)), x.size(1), num_shifts=k_shift,
                             normalize_output=True, sparse=True).to(device)
-    optim = SparseRowAdagrad([model], lr=lr)
+    optim = SparseRowAdagrad([model], lr=lr, fused=_FUSED)
     rng = np.random.default_rng(seed)
     losses = _LossLog(log, "Model", num_epochs, log_every)
     for epoch in range(num_epochs):
@@ -124,7 +132,7 @@ def train_mask_model(df, expansion_factor: float, k_shift: int, mask_emb_dim: in
     emb = KShiftEmbedding(int(expansion_factor * n), mask_emb_dim, num_shifts=k_shift, normalize_output=False,
                           sparse=True)
     model = nn.Sequential(emb, MLP(mask_emb_dim, 1, [mask_emb_dim * 16])).to(device)
-    opt_tab = SparseRowAdagrad([emb], lr=lr)
+    opt_tab = SparseRowAdagrad([emb], lr=lr, fused=_FUSED)
     opt_mlp = FusedAdagrad(model[1].parameters(), lr=lr)
     rng = np.random.default_rng(seed)
     g = torch.Generator(device=device).manual_seed(seed)

@@ -1028,6 +1028,38 @@ def kshift_bwd_sparse(ids, gy, out, norms, P, K, mode, F, dW, flags, rows_list, 
          P, D, K, mode, ptr(dW), ptr(flags), ptr(rows_list), ptr(count), stream())
 
 
+# fused dedup + Adagrad workspaces, one per (device, stream) (the kernel counters live in it)
+_kag_ws = {}
+_kag_need = {}
+
+
+def kshift_adagrad_fused(ids, gy, out, norms, P, K, mode, F, W, state, clr, eps):
+    """lthm_kshift_adagrad_fused: the KShift backward of ids [n, F] / gy [n, F, D] and the
+    Adagrad step of the rows it touches in one call (W, state [F * P, D] f32, updated in place;
+    clr = lr / (1 + (step - 1) lr_decay))."""
+    require_gpu(ids, gy, out, norms, W, state)
+    D = W.shape[1]
+    _check_kshift(ids, P, K, F, D, table_rows=W.shape[0], gy=gy, out=out, norms=norms)
+    _check(W.dtype == torch.float32 and state.dtype == torch.float32 and state.shape == W.shape,
+           "kshift_adagrad_fused: W and state are [F * P, D] float32")
+    _check(mode != KSHIFT_NORMALIZE or (out is not None and norms is not None), "normalize mode needs out / norms")
+    n = ids.numel() // F
+    if n == 0:
+        return
+    need = _kag_need.get((n * F, K, D))
+    if need is None:  # (the size query asks the sort for its temporary storage: once per shape)
+        need = _kag_need[(n * F, K, D)] = load().lthm_kshift_adagrad_ws_bytes(n * F, K, D)
+    _check(need > 0,f"kshift_adagrad_fused: unsupported sizes (n * F * K = {n * F * K}, D = {D}, K = {K})")
+    key = (ids.device, torch.cuda.current_stream(ids.device).cuda_stream)
+    ws = _kag_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=ids.device)
+        _kag_ws[key] = ws
+    call("lthm_kshift_adagrad_fused", ptr(ids), n, F, ptr(gy), dcode(gy),
+         ptr(out) if out is not None else None, dcode(out) if out is not None else F32, ptr(norms), P, D, K, mode,
+         ptr(W), ptr(state), clr, eps, ptr(ws), ws.numel(), stream(), _key="lthm_kshift_adagrad_fused")
+
+
 # ----------------------------------------------------------------- optimizers / norms
 def adamw_(p, g, m, v, lr, betas, eps, wd, step, grad_scale=1.0, shadow=None, zero_grad=False):
     for t, nm in ((g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq"), (shadow, "shadow")):

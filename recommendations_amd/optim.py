@@ -158,14 +158,52 @@ class SparseRowAdamW:
 
 
 class SparseRowAdagrad(SparseRowAdamW):
-    def __init__(self, modules: Iterable, lr=1e-2, lr_decay=0.0, eps=1e-10):
+    """Row-wise Adagrad over KShift tables (sparse=True).
+
+    ``fused=True``: the tables' backward only records its lookups and ``step`` runs the fused
+    dedup + Adagrad (lthm_kshift_adagrad_fused): each touched row's gradient is summed and
+    consumed by its update in one call, no gradient row stored and no [F * P, D] gradient buffer
+    allocated.  Valid where nothing reads or rescales the table gradients between backward and
+    step -- the item-embedding generator (embedding_module_gen.py:137,151-153: ``loss.backward();
+    optim.step()`` with torch.optim.Adagrad, no clipping)."""
+
+    def __init__(self, modules: Iterable, lr=1e-2, lr_decay=0.0, eps=1e-10, fused: bool = False):
         super().__init__(modules, lr=lr)
         self.lr_decay, self.eps = lr_decay, eps
+        self.fused = fused
+        if fused:
+            for m in self.modules:
+                m.fused_row_step = True
+                m.fused_pending = []
+
+    @torch.no_grad()
+    def _step_fused(self, m):
+        recs, m.fused_pending = m.fused_pending, []
+        if not recs:
+            return
+        st = self.state.get(id(m))
+        if st is None:
+            st = self.state[id(m)] = K.zeros(m.weight.shape, torch.float32, m.weight.device)
+        if len(recs) == 1:
+            ids, gy, out, norms = recs[0]
+        else:  # several backwards before one step: their lookups in order
+            ids = torch.cat([r[0].reshape(-1, m._F) for r in recs])
+            gy = torch.cat([r[1].reshape(-1, r[1].shape[-1]) for r in recs])
+            out = None if recs[0][2] is None else torch.cat([r[2].reshape(-1, r[2].shape[-1]) for r in recs])
+            norms = None if recs[0][3] is None else torch.cat([r[3].reshape(-1) for r in recs])
+        # torch.optim.Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double, applied as f32
+        clr = self.lr / (1.0 + (self.step_count - 1) * self.lr_decay)
+        K.kshift_adagrad_fused(ids, gy, out, norms, m._num_embeddings, m._num_shifts, m._mode, m._F, m.weight.data,
+                               st, clr, self.eps)
+        m.invalidate_shadow()  # rows rewritten outside torch's version counter
 
     @torch.no_grad()
     def step(self):
         self.step_count += 1
         for m in self.modules:
+            if self.fused:
+                self._step_fused(m)
+                continue
             if m.sparse_count is None or m.sparse_pending == 0:
                 continue
             st = self.state.get(id(m))

@@ -26,8 +26,11 @@ def _df(n, D, seed=0):
                          "embedding": list(g.standard_normal((n, D)).astype(np.float32))})
 
 
-def test_train_model_matches_dense_adagrad(dev):
+@pytest.mark.parametrize("fused", [True, False])  # lthm_kshift_adagrad_fused / the two-pass row path
+def test_train_model_matches_dense_adagrad(dev, fused, monkeypatch):
+    from recommendations_amd import embedding_module_gen
     from recommendations_amd.embedding_module_gen import massage_embeddings, train_model
+    monkeypatch.setattr(embedding_module_gen, "_FUSED", fused)
     df = massage_embeddings(_df(3000, 32))
     torch.manual_seed(5)
     m = train_model(df, 1.15, 16, num_epochs=2, batch_size=1024, device=dev, seed=1, log=None)
@@ -49,8 +52,11 @@ def test_train_model_matches_dense_adagrad(dev):
     check('m.emb.weight, W', relerr(m.emb.weight, W), 1e-5)
 
 
-def test_train_mask_model_matches_dense_adagrad(dev):
+@pytest.mark.parametrize("fused", [True, False])
+def test_train_mask_model_matches_dense_adagrad(dev, fused, monkeypatch):
+    from recommendations_amd import embedding_module_gen
     from recommendations_amd.embedding_module_gen import massage_embeddings, train_mask_model
+    monkeypatch.setattr(embedding_module_gen, "_FUSED", fused)
     df = massage_embeddings(_df(2000, 8, seed=3))
     negs = np.random.default_rng(9).integers(-2 ** 63, 2 ** 63 - 1, size=(8, 1000), dtype=np.int64)
     calls = {"i": 0}

@@ -1,0 +1,132 @@
+"""GPU parity of the fused dedup + Adagrad (lthm_kshift_adagrad_fused, csrc/kshift_adagrad.hip)
+against its CPU restatement (oracle/ref.py kshift_adagrad_ref, itself pinned to
+torch.optim.Adagrad by tests/test_kshift_adagrad_cpu.py):
+
+* scale / plain modes: bit-identical tables and Adagrad state (same pair order, same f32
+  operations), over two steps, short and long (> 256 pairs, chunked) rows, F = 1..3 tables,
+  D from 4 to 200, f32 and bf16 upstream gradients;
+* normalize mode: the per-item F.normalize backward's dot product runs in another order on the
+  GPU (wave reduction vs float64): 1e-5;
+* the module path (KShiftEmbedding + SparseRowAdagrad(fused=True), two backwards before one
+  step) against the two-pass path (row gradients staged, then the row-wise Adagrad): 1e-5;
+* determinism: two runs bit-identical."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(seed, n, F_, P, D, neg_frac=0.5):
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, 2 ** 63 - 1, size=(n, F_), dtype=np.int64)
+    neg = rng.random((n, F_)) < neg_frac
+    ids[neg] = -ids[neg] - 1
+    W0 = rng.standard_normal((F_ * P, D)).astype(np.float32)
+    S0 = np.abs(rng.standard_normal((F_ * P, D))).astype(np.float32) * 0.1
+    return rng, ids, W0, S0
+
+
+@pytest.mark.parametrize("mode,K,F_,D,P,n,gdt", [
+    (0, 16, 1, 32, 1000, 3000, torch.float32),   # heavy row P - 1: ~22k pairs (chunked)
+    (0, 16, 1, 4, 500, 2000, torch.float32),     # the mask model's D
+    (0, 8, 2, 128, 300, 700, torch.bfloat16),
+    (0, 4, 3, 200, 50, 400, torch.float32),      # D > 128: four columns per lane
+    (2, 1, 3, 16, 40, 1500, torch.float32),      # K = 1 plain rows, many long rows
+    (0, 16, 1, 64, 100000, 5000, torch.float32),  # mostly short rows
+])
+def test_fused_adagrad_bit_exact(dev, mode, K, F_, D, P, n, gdt):
+    from recommendations_amd import kernels as KK
+    rng, ids, W0, S0 = _case(7 * K + D, n, F_, P, D)
+    W = torch.from_numpy(W0).to(dev)
+    S = torch.from_numpy(S0).to(dev)
+    Wo, So = W0, S0
+    for step in range(1, 3):
+        dY = rng.standard_normal((n * F_, D)).astype(np.float32)
+        gy = torch.from_numpy(dY).to(dev).to(gdt)
+        clr = 0.5 / (1.0 + (step - 1) * 0.01)
+        KK.kshift_adagrad_fused(torch.from_numpy(ids).to(dev), gy, None, None, P, K, mode, F_, W, S, clr, 1e-10)
+        g = ref.kshift_pool_grad(gy.float().cpu().numpy(), K, mode)
+        Wo, So = ref.kshift_adagrad_ref(ids, g, P, K, F_, Wo, So, clr, 1e-10)
+    torch.cuda.synchronize()
+    assert np.array_equal(W.cpu().numpy(), Wo), np.abs(W.cpu().numpy() - Wo).max()
+    assert np.array_equal(S.cpu().numpy(), So), np.abs(S.cpu().numpy() - So).max()
+    if K > 1:
+        assert (ref.kshift_rows(ids.reshape(-1), P, K) == P - 1).sum() > 256  # the long path ran
+
+
+def test_fused_adagrad_normalize(dev):
+    from recommendations_amd import kernels as KK
+    K, D, P, n = 16, 32, 800, 2500
+    rng, ids, W0, S0 = _case(3, n, 1, P, D)
+    x = ref.kshift_fwd_c(ids[:, 0], W0, K, 2)
+    norms = np.linalg.norm(x.astype(np.float64), axis=-1).astype(np.float32)
+    out = (x / np.maximum(norms, 1e-12)[:, None]).astype(np.float32)
+    dY = rng.standard_normal((n, D)).astype(np.float32)
+    W = torch.from_numpy(W0).to(dev)
+    S = torch.from_numpy(S0).to(dev)
+    KK.kshift_adagrad_fused(torch.from_numpy(ids).to(dev), torch.from_numpy(dY).to(dev), torch.from_numpy(out).to(dev),
+                            torch.from_numpy(norms).to(dev), P, K, KK.KSHIFT_NORMALIZE, 1, W, S, 0.5, 1e-10)
+    Wo, So = ref.kshift_adagrad_ref(ids, ref.kshift_pool_grad(dY, K, 1, out, norms), P, K, 1, W0, S0, 0.5, 1e-10)
+    np.testing.assert_allclose(W.cpu().numpy(), Wo, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(S.cpu().numpy(), So, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_fused_module_step_matches_two_pass(dev, normalize):
+    """KShiftEmbedding(sparse=True) trained by SparseRowAdagrad(fused=True) vs (fused=False):
+    two backwards (two batches) accumulated before each of two steps."""
+    from recommendations_amd.commons.layers import KShiftEmbedding
+    from recommendations_amd.optim import SparseRowAdagrad
+    P, D, K = 5000, 32, 16
+    mods, opts = [], []
+    for fused in (True, False):
+        torch.manual_seed(4)
+        m = KShiftEmbedding(P, D, num_shifts=K, normalize_output=normalize, sparse=True).to(dev)
+        mods.append(m)
+        opts.append(SparseRowAdagrad([m], lr=0.5, lr_decay=0.01, fused=fused))
+    rng = np.random.default_rng(8)
+    for step in range(2):
+        batches = [(torch.from_numpy(rng.integers(-2 ** 63, 2 ** 63 - 1, size=3000, dtype=np.int64)).to(dev),
+                    torch.randn(3000, D, device=dev)) for _ in range(2)]
+        for m, opt in zip(mods, opts):
+            for ids, tgt in batches:
+                ((m(ids) - tgt) ** 2).mean().backward()
+            opt.step()
+    torch.cuda.synchronize()
+    a, b = mods[0].weight.detach(), mods[1].weight.detach()
+    assert torch.isfinite(a).all()
+    assert ((a - b).norm() / b.norm()).item() < 1e-5
+    sa, sb = opts[0].state[id(mods[0])], opts[1].state[id(mods[1])]
+    assert ((sa - sb).norm() / sb.norm()).item() < 1e-5
+    assert mods[0].sparse_grad is None  # the fused path allocates no [P, D] gradient
+
+
+def test_fused_adagrad_deterministic_large(dev):
+    """2^17 items x 16 shifts (2M pairs, about 1M of them on row P - 1: 4k chunks): two runs
+    from the same state are bit-identical."""
+    from recommendations_amd import kernels as KK
+    K, D, P, n = 16, 32, 150000, 1 << 17
+    rng, ids, W0, S0 = _case(11, n, 1, P, D)
+    dY = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(dev)
+    idt = torch.from_numpy(ids).to(dev)
+    res = []
+    for _ in range(2):
+        W = torch.from_numpy(W0).to(dev)
+        S = torch.from_numpy(S0).to(dev)
+        KK.kshift_adagrad_fused(idt, dY, None, None, P, K, KK.KSHIFT_SCALE, 1, W, S, 0.5, 1e-10)
+        res.append((W, S))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.isfinite(res[0][0]).all()
+    # row P - 1 against the float64 sum of its pairs' gradients
+    rows = ref.kshift_rows(ids.reshape(-1), P, K)
+    items = np.nonzero(rows == P - 1)[0] // K
+    g = dY.cpu().numpy().astype(np.float64)[items].sum(0) / math.sqrt(K)
+    s = S0[P - 1].astype(np.float64) + g * g
+    w = W0[P - 1] - 0.5 * g / (np.sqrt(s) + 1e-10)
+    np.testing.assert_allclose(res[0][0][P - 1].cpu().numpy(), w, rtol=1e-4, atol=1e-5)
