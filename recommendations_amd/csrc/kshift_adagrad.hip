@@ -84,46 +84,76 @@ __global__ __launch_bounds__(256) void kag_heads_k(const uint32_t* __restrict__ 
     heads[j] = (j == 0 || skeys[j] != skeys[j - 1]) ? 1 : 0;
 }
 
-// acc[q] += g[item][gl + LG q] for the pairs [j0, j1) in order, four pairs' loads in flight
-template <int LG, int NQ>
+// column slots of a lane: slot q of lane gl covers columns (gl + LG q) CW .. + CW - 1 (CW = 4: one
+// 16-B access, D % 4 == 0), none past D
+template <int CW>
+__device__ __forceinline__ void kag_ld(const float* __restrict__ p, int c0, int D, float* v) {
+  if constexpr (CW == 4) {
+    const f32x4 x = c0 < D ? *reinterpret_cast<const f32x4*>(p + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else {
+    v[0] = c0 < D ? p[c0] : 0.f;
+  }
+}
+template <int CW>
+__device__ __forceinline__ void kag_st(float* __restrict__ p, int c0, int D, const float* v) {
+  if (c0 >= D) return;
+  if constexpr (CW == 4) *reinterpret_cast<f32x4*>(p + c0) = f32x4{v[0], v[1], v[2], v[3]};
+  else p[c0] = v[0];
+}
+
+// acc += g[item] over the lane's column slots for the pairs [j0, j1) in order, four pairs'
+// loads in flight
+template <int LG, int NQ, int CW>
 __device__ __forceinline__ void kag_sum(const uint32_t* __restrict__ svals, const float* __restrict__ g, int D,
-                                        int gl, uint32_t j0, uint32_t j1, float (&acc)[NQ]) {
+                                        int gl, uint32_t j0, uint32_t j1, float (&acc)[NQ * CW]) {
   uint32_t j = j0;
   for (; j + 4 <= j1; j += 4) {
-    float x[4][NQ];
+    float x[4][NQ * CW];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const float* gr = g + (int64_t)svals[j + p] * D;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int d = gl + LG * q;
-        x[p][q] = d < D ? gr[d] : 0.f;
-      }
+      for (int q = 0; q < NQ; ++q) kag_ld<CW>(gr, (gl + LG * q) * CW, D, x[p] + q * CW);
     }
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] = __fadd_rn(acc[q], x[p][q]);
+      for (int e = 0; e < NQ * CW; ++e) acc[e] = __fadd_rn(acc[e], x[p][e]);
   }
   for (; j < j1; ++j) {
     const float* gr = g + (int64_t)svals[j] * D;
+    float x[NQ * CW];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int d = gl + LG * q;
-      acc[q] = __fadd_rn(acc[q], d < D ? gr[d] : 0.f);
-    }
+    for (int q = 0; q < NQ; ++q) kag_ld<CW>(gr, (gl + LG * q) * CW, D, x + q * CW);
+#pragma unroll
+    for (int e = 0; e < NQ * CW; ++e) acc[e] = __fadd_rn(acc[e], x[e]);
   }
 }
 
-// torch.optim.Adagrad's element update (lr_decay in clr, no weight decay), unfused:
-// s = s + g * g ; W = W - (clr * g) / (sqrt(s) + eps)
+// correctly rounded f32 square root: v_sqrt_f32 is within 1 ulp; its neighbours' exact
+// residuals x - s' s (one fma each) pick the rounded root
+__device__ __forceinline__ float kag_sqrt_rn(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float dn = __int_as_float(__float_as_int(s) - 1), up = __int_as_float(__float_as_int(s) + 1);
+  const float vp = __builtin_fmaf(-dn, s, x), vs = __builtin_fmaf(-up, s, x);
+  const float r = vp <= 0.f ? dn : s;
+  return vs > 0.f ? up : r;
+}
+
+// torch.optim.Adagrad's element update (lr_decay in clr, no weight decay), every operation
+// rounded on its own (no contraction into fma): s = s + g * g ; W = W - (clr * g) / (sqrt(s) + eps)
 __device__ __forceinline__ void kag_update(float& w, float& s, float gr, float clr, float eps) {
-  s = __fadd_rn(s, __fmul_rn(gr, gr));
-  w = __fsub_rn(w, __fdiv_rn(__fmul_rn(clr, gr), __fadd_rn(__fsqrt_rn(s), eps)));
+#pragma clang fp contract(off)
+  const float gg = gr * gr;
+  s = s + gg;
+  const float den = kag_sqrt_rn(s) + eps;
+  const float num = clr * gr;
+  w = w - num / den;
 }
 
 // one LG-lane group per segment (grid-stride); segments of more than KAG_CH pairs are listed
-template <int LG, int NQ>
+template <int LG, int NQ, int CW>
 __global__ __launch_bounds__(256) void kag_apply_k(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
                                                    const uint32_t* __restrict__ starts, const int* __restrict__ nseg_p,
                                                    int64_t N, const float* __restrict__ g, int D, float* __restrict__ W,
@@ -141,23 +171,21 @@ __global__ __launch_bounds__(256) void kag_apply_k(const uint32_t* __restrict__ 
     const int64_t row = skeys[s0];
     float* wr = W + row * D;
     float* sr = S + row * D;
-    float w[NQ], s[NQ], acc[NQ];
+    float w[NQ * CW], s[NQ * CW], acc[NQ * CW];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int d = gl + LG * q;
-      w[q] = d < D ? wr[d] : 0.f;
-      s[q] = d < D ? sr[d] : 0.f;
-      acc[q] = 0.f;
+      kag_ld<CW>(wr, (gl + LG * q) * CW, D, w + q * CW);
+      kag_ld<CW>(sr, (gl + LG * q) * CW, D, s + q * CW);
     }
-    kag_sum<LG, NQ>(svals, g, D, gl, s0, s1, acc);
+#pragma unroll
+    for (int e = 0; e < NQ * CW; ++e) acc[e] = 0.f;
+    kag_sum<LG, NQ, CW>(svals, g, D, gl, s0, s1, acc);
+#pragma unroll
+    for (int e = 0; e < NQ * CW; ++e) kag_update(w[e], s[e], acc[e], clr, eps);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int d = gl + LG * q;
-      if (d < D) {
-        kag_update(w[q], s[q], acc[q], clr, eps);
-        sr[d] = s[q];
-        wr[d] = w[q];
-      }
+      kag_st<CW>(sr, (gl + LG * q) * CW, D, s + q * CW);
+      kag_st<CW>(wr, (gl + LG * q) * CW, D, w + q * CW);
     }
   }
 }
@@ -199,7 +227,7 @@ __global__ __launch_bounds__(1024) void kag_long_prep_k(const uint32_t* __restri
 }
 
 // chunk c of the long segments (grid-stride, one LG-lane group per chunk): its pairs' sum
-template <int LG, int NQ>
+template <int LG, int NQ, int CW>
 __global__ __launch_bounds__(256) void kag_chunk_k(const uint32_t* __restrict__ svals, const uint32_t* __restrict__ starts,
                                                    const int* __restrict__ nseg_p, int64_t N,
                                                    const uint32_t* __restrict__ longlist, const int* __restrict__ nlong,
@@ -218,18 +246,15 @@ __global__ __launch_bounds__(256) void kag_chunk_k(const uint32_t* __restrict__ 
       else hi = mid - 1;
     }
     const uint32_t u = longlist[lo];
-    const uint32_t e = (int)u + 1 < nseg ? starts[u + 1] : (uint32_t)N;
+    const uint32_t send = (int)u + 1 < nseg ? starts[u + 1] : (uint32_t)N;
     const uint32_t s0 = starts[u] + ((uint32_t)c - lpref[lo]) * KAG_CH;
-    const uint32_t s1 = min(s0 + (uint32_t)KAG_CH, e);
-    float acc[NQ];
+    const uint32_t s1 = min(s0 + (uint32_t)KAG_CH, send);
+    float acc[NQ * CW];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-    kag_sum<LG, NQ>(svals, g, D, gl, s0, s1, acc);
+    for (int e = 0; e < NQ * CW; ++e) acc[e] = 0.f;
+    kag_sum<LG, NQ, CW>(svals, g, D, gl, s0, s1, acc);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int d = gl + LG * q;
-      if (d < D) part[c * D + d] = acc[q];
-    }
+    for (int q = 0; q < NQ; ++q) kag_st<CW>(part + c * D, (gl + LG * q) * CW, D, acc + q * CW);
   }
 }
 
@@ -344,7 +369,7 @@ static int kag_cu_count() {
   return cus;
 }
 
-template <int LG, int NQ>
+template <int LG, int NQ, int CW>
 static int kag_launch_groups(const KagLayout& L, unsigned char* w, int64_t N, int D, float* W, float* S, float clr,
                              float eps, hipStream_t s) {
   const uint32_t* skeys = (const uint32_t*)(w + L.skeys);
@@ -357,13 +382,13 @@ static int kag_launch_groups(const KagLayout& L, unsigned char* w, int64_t N, in
   float* part = (float*)(w + L.part);
   const int cap = kag_cu_count() * 16;
   const int gpb = 256 / LG;
-  hipLaunchKernelGGL((kag_apply_k<LG, NQ>), dim3(grid_for(N, gpb, cap)), dim3(256), 0, s, skeys, svals, starts, cnt, N,
+  hipLaunchKernelGGL((kag_apply_k<LG, NQ, CW>), dim3(grid_for(N, gpb, cap)), dim3(256), 0, s, skeys, svals, starts, cnt, N,
                      g, D, W, S, clr, eps, longlist, (int*)(cnt + 1));
   LTHM_CHECK_LAUNCH();
   hipLaunchKernelGGL(kag_long_prep_k, dim3(1), dim3(1024), 0, s, starts, cnt, N, (const uint32_t*)longlist, cnt + 1,
                      lpref);
   LTHM_CHECK_LAUNCH();
-  hipLaunchKernelGGL((kag_chunk_k<LG, NQ>), dim3(grid_for(2 * (N / KAG_CH) + 2, gpb, cap)), dim3(256), 0, s, svals,
+  hipLaunchKernelGGL((kag_chunk_k<LG, NQ, CW>), dim3(grid_for(2 * (N / KAG_CH) + 2, gpb, cap)), dim3(256), 0, s, svals,
                      starts, cnt, N, (const uint32_t*)longlist, cnt + 1, (const uint32_t*)lpref, g, D, part);
   LTHM_CHECK_LAUNCH();
   hipLaunchKernelGGL(kag_long_apply_k, dim3(grid_for(N / (KAG_CH + 1) + 1, 1, kag_cu_count() * 2)),
@@ -441,12 +466,22 @@ extern "C" int lthm_kshift_adagrad_fused(const int64_t* ids, int64_t n, int32_t 
                                     (const uint8_t*)heads, (uint32_t*)(w + L.starts), (int*)(w + L.cnt), (int)N,
                                     s) != hipSuccess)
     return (int)hipErrorLaunchFailure;
-  // lane groups sized to the row: D <= LG * NQ, LG a power of two in [4, 64]
-  if (D <= 4) return kag_launch_groups<4, 1>(L, w, N, D, W, state_sum, clr, eps, s);
-  if (D <= 8) return kag_launch_groups<8, 1>(L, w, N, D, W, state_sum, clr, eps, s);
-  if (D <= 16) return kag_launch_groups<16, 1>(L, w, N, D, W, state_sum, clr, eps, s);
-  if (D <= 32) return kag_launch_groups<32, 1>(L, w, N, D, W, state_sum, clr, eps, s);
-  if (D <= 64) return kag_launch_groups<64, 1>(L, w, N, D, W, state_sum, clr, eps, s);
-  if (D <= 128) return kag_launch_groups<64, 2>(L, w, N, D, W, state_sum, clr, eps, s);
-  return kag_launch_groups<64, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+  // lane groups sized to the row: 16-B column slots when D % 4 == 0 (D / 4 lanes rounded up to a
+  // power of two: D = 32 -> 8 lanes, 8 rows per wave in flight), else one column per slot
+  if (D % 4 == 0) {
+    if (D <= 4) return kag_launch_groups<1, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    if (D <= 8) return kag_launch_groups<2, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    if (D <= 16) return kag_launch_groups<4, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    if (D <= 32) return kag_launch_groups<8, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    if (D <= 64) return kag_launch_groups<16, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    if (D <= 128) return kag_launch_groups<32, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+    return kag_launch_groups<64, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
+  }
+  if (D <= 4) return kag_launch_groups<4, 1, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  if (D <= 8) return kag_launch_groups<8, 1, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  if (D <= 16) return kag_launch_groups<16, 1, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  if (D <= 32) return kag_launch_groups<32, 1, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  if (D <= 64) return kag_launch_groups<64, 1, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  if (D <= 128) return kag_launch_groups<64, 2, 1>(L, w, N, D, W, state_sum, clr, eps, s);
+  return kag_launch_groups<64, 4, 1>(L, w, N, D, W, state_sum, clr, eps, s);
 }

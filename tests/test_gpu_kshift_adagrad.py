@@ -38,6 +38,8 @@ def _case(seed, n, F_, P, D, neg_frac=0.5):
     (0, 4, 3, 200, 50, 400, torch.float32),      # D > 128: four columns per lane
     (2, 1, 3, 16, 40, 1500, torch.float32),      # K = 1 plain rows, many long rows
     (0, 16, 1, 64, 100000, 5000, torch.float32),  # mostly short rows
+    (0, 16, 2, 70, 200, 500, torch.float32),     # D % 4 != 0: one column per lane slot
+    (0, 8, 1, 6, 300, 800, torch.bfloat16),
 ])
 def test_fused_adagrad_bit_exact(dev, mode, K, F_, D, P, n, gdt):
     from recommendations_amd import kernels as KK
@@ -124,7 +126,7 @@ def test_fused_adagrad_deterministic_large(dev):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     assert torch.isfinite(res[0][0]).all()
     # row P - 1 against the float64 sum of its pairs' gradients
-    rows = ref.kshift_rows(ids.reshape(-1), P, K)
+    rows = ref.kshift_rows(ids.reshape(-1), P, K).reshape(-1)
     items = np.nonzero(rows == P - 1)[0] // K
     g = dY.cpu().numpy().astype(np.float64)[items].sum(0) / math.sqrt(K)
     s = S0[P - 1].astype(np.float64) + g * g
