@@ -102,24 +102,37 @@ __device__ __forceinline__ void kag_st(float* __restrict__ p, int c0, int D, con
   else p[c0] = v[0];
 }
 
-// acc += g[item] over the lane's column slots for the pairs [j0, j1) in order, four pairs'
-// loads in flight
+// acc += g[item] over the lane's column slots for the pairs [j0, j1) in order: eight pairs' g
+// rows in flight, the next eight pairs' items loaded one batch ahead (a long chunk is then one
+// memory latency per eight pairs, not two per pair group), a tail of < 8 pairs one by one
 template <int LG, int NQ, int CW>
 __device__ __forceinline__ void kag_sum(const uint32_t* __restrict__ svals, const float* __restrict__ g, int D,
                                         int gl, uint32_t j0, uint32_t j1, float (&acc)[NQ * CW]) {
   uint32_t j = j0;
-  for (; j + 4 <= j1; j += 4) {
-    float x[4][NQ * CW];
+  if (j + 8 <= j1) {
+    uint32_t nv[8];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const float* gr = g + (int64_t)svals[j + p] * D;
+    for (int p = 0; p < 8; ++p) nv[p] = svals[j + p];
+    for (; j + 8 <= j1; j += 8) {
+      uint32_t cur[8];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) kag_ld<CW>(gr, (gl + LG * q) * CW, D, x[p] + q * CW);
+      for (int p = 0; p < 8; ++p) cur[p] = nv[p];
+      if (j + 16 <= j1) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) nv[p] = svals[j + 8 + p];
+      }
+      float x[8][NQ * CW];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const float* gr = g + (int64_t)cur[p] * D;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) kag_ld<CW>(gr, (gl + LG * q) * CW, D, x[p] + q * CW);
+      }
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int e = 0; e < NQ * CW; ++e) acc[e] = __fadd_rn(acc[e], x[p][e]);
     }
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int e = 0; e < NQ * CW; ++e) acc[e] = __fadd_rn(acc[e], x[p][e]);
   }
   for (; j < j1; ++j) {
     const float* gr = g + (int64_t)svals[j] * D;

@@ -240,6 +240,33 @@ def test_attention_vs_oracle(dev, B, T, H, E, causal):
             check('got, want', relerr(got, want), 1e-2)
 
 
+def test_attention_persistent_bwd_matches_default(dev, tmp_path):
+    """The persistent double-buffered E = 64 backward (attn_bwd32p_k, opt-in LTHM_ATTN_BWD_P=1,
+    read once by the library: run in a child process, tests/attn_pers_worker.py) against the
+    default one-workgroup-per-(b, h) kernel on the same inputs: each (b, h)'s units run the
+    same arithmetic, so dq / dk / dv are identical; the bias gradient sums the entries per
+    workgroup slot before the cross-slot reduction (f32 order only)."""
+    import os
+    import subprocess
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from attn_pers_worker import run_case
+    cases = [(300, 129, 4, 64, True), (520, 65, 1, 64, False), (600, 100, 2, 64, True)]
+    specs = [",".join(str(int(x)) for x in c) for c in cases]
+    path = str(tmp_path / "pers.npz")
+    env = dict(os.environ, LTHM_ATTN_BWD_P="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run([sys.executable, os.path.join(here, "attn_pers_worker.py"), path] + specs, env=env, check=True,
+                   timeout=300)
+    got = np.load(path)
+    for c, spec in zip(cases, specs):
+        dq, dt = run_case(dev, *c)
+        assert np.array_equal(got[f"{spec}/dqkv"], dq), (spec, np.abs(got[f"{spec}/dqkv"] - dq).max())
+        check(f"dtable persistent vs default {spec}", relerr(torch.from_numpy(got[f"{spec}/dtab"]),
+                                                            torch.from_numpy(dt)), 1e-5)
+
+
 def _cfg(d, H, bias, causal, pos):
     from recommendations_amd.commons.transformers.configs import TransformerConfig
     return TransformerConfig(rotator_config={"ff_mult": 4}, is_causal=causal,
