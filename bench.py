@@ -103,6 +103,40 @@ def pmc_traffic(key, calls_per_step):
     return tot / (calls_per_step * PMC_STEPS)
 
 
+def embedding_generator_step(dev, n_catalogue=2_000_000, B=1 << 18, D=32, K=16, steps=10, warmup=3):
+    """one step of the item-embedding generator's reconstruction model at the
+    reference sizes (embedding_module_gen.py:122-156: KShiftEmbedding(1.15 n, D, K = 16,
+    normalize) -> MSE -> loss.backward(); Adagrad(lr 0.5).step(); batches of 2^18 ids), with the
+    tables stepped by the fused dedup + Adagrad (lthm_kshift_adagrad_fused) and by the two-pass
+    row path, HIP events over `steps` steps after `warmup`."""
+    from recommendations_amd import kernels as K_
+    from recommendations_amd.commons.layers import KShiftEmbedding
+    from recommendations_amd.optim import SparseRowAdagrad
+    g = torch.Generator(device=dev).manual_seed(11)
+    P = int(1.15 * n_catalogue)
+    catalogue = torch.randint(-2 ** 63, 2 ** 63 - 1, (n_catalogue,), device=dev, generator=g, dtype=torch.int64)
+    batches = [catalogue[torch.randint(0, n_catalogue, (B,), device=dev, generator=g)] for _ in range(4)]
+    tgt = K_.l2norm_rows(torch.randn(B, D, device=dev, generator=g))
+    res = {"model": f"KShiftEmbedding(P={P}, D={D}, K={K}, normalize) + MSE + Adagrad", "ids_per_step": B}
+    for fused in (True, False):
+        torch.manual_seed(0)
+        emb = KShiftEmbedding(P, D, num_shifts=K, normalize_output=True, sparse=True).to(dev)
+        opt = SparseRowAdagrad([emb], lr=0.5, fused=fused)
+        for i in range(warmup + steps):
+            if i == warmup:
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            K_.mse_loss(emb(batches[i % 4]), tgt).backward()
+            opt.step()
+        e1.record()
+        torch.cuda.synchronize()
+        res["fused_ms_per_step" if fused else "two_pass_ms_per_step"] = round(e0.elapsed_time(e1) / steps, 4)
+        del emb, opt
+    torch.cuda.empty_cache()
+    return res
+
+
 def embedding_gather_hbm(dev, P=16_000_000, D=128, K=16, n=524_288, iters=50):
     """SURVEY §8(d) embedding roofline: KShift gather + pool forward on a table far past
     the 256 MiB Infinity Cache (P x D bf16 = 4.1 GB), algorithmic bytes per lookup
@@ -358,6 +392,8 @@ def main():
                     help="CPU-baseline sample (sequences); default per BASELINE.md: C2 256, C5 16, C1 the batch")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-hbm-gather", action="store_true", help="skip the 1 GB-table embedding roofline")
+    ap.add_argument("--no-generator", action="store_true",
+                    help="skip the item-embedding generator step (fused vs two-pass Adagrad)")
     ap.add_argument("--check-launch", action="store_true",
                     help="form the process group, print the world size it reports and exit (launcher test)")
     args = ap.parse_args()
@@ -654,6 +690,8 @@ def main():
                                           "frac": round(g["work"] / (g["ms"] / 1000) / 1e9 / HBM_PEAK_GBS, 4)}
         if rank == 0 and not args.no_hbm_gather:
             res["embedding_gather"] = embedding_gather_hbm(dev)
+        if rank == 0 and not args.no_generator and args.config == "c2":
+            res["embedding_generator"] = embedding_generator_step(dev)
         res["kernels"] = kern
         res["kernels_source"] = (f"{PROF_STEPS} untimed profiling steps after warm-up (HIP events around every "
                                  f"entry point; share = fraction of the summed kernel time); the roofline kernel "
