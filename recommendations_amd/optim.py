@@ -197,6 +197,13 @@ class SparseRowAdagrad(SparseRowAdamW):
                                st, clr, self.eps)
         m.invalidate_shadow()  # rows rewritten outside torch's version counter
 
+    def zero_grad(self, set_to_none: bool = True):
+        """fused: the recorded lookups are the tables' pending gradient -- dropped, as
+        torch's zero_grad drops .grad (the two-pass form keeps its row-wise semantics)."""
+        if self.fused:
+            for m in self.modules:
+                m.fused_pending = []
+
     @torch.no_grad()
     def step(self):
         self.step_count += 1
