@@ -32,20 +32,24 @@ namespace lthm {
 constexpr int KAG_CH = 256;  // pairs per chunk; rows with more pairs take the long path
 constexpr int KAG_LW = 16;   // waves of the long-row combine workgroup
 
-// per item (one wave each, grid-stride): g_i and the item's K (row, item) pairs
-template <typename TY, typename TO>
+// per item (LPI lanes each, 64 / LPI items per wave, grid-stride): g_i and the item's K (row,
+// item) pairs; LPI >= K and D <= 4 LPI (column d = lane + LPI q)
+template <typename TY, typename TO, int LPI>
 __global__ __launch_bounds__(256) void kag_prep_k(const int64_t* __restrict__ ids, int64_t n_items, int F,
                                                   const TY* __restrict__ dY, const TO* __restrict__ out,
                                                   const float* __restrict__ norms, int64_t P, int D, int K, int mode,
                                                   float scale, float* __restrict__ g, uint32_t* __restrict__ keys,
                                                   uint32_t* __restrict__ vals) {
-  const int lane = threadIdx.x & 63;
+  constexpr int IPW = 64 / LPI;
+  const int l = threadIdx.x % LPI, slot = (threadIdx.x & 63) / LPI;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < n_items; it += nw) {
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * IPW; base < n_items; base += nw * IPW) {
+    const int64_t it = base + slot;
+    if (it >= n_items) continue;  // a whole lane group: its shuffles stay inside the group
     float v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int d = lane + 64 * q;
+      const int d = l + LPI * q;
       const float dy = d < D ? Elem<TY>::ld(dY + it * D + d) : 0.f;
       v[q] = mode == LTHM_KSHIFT_SCALE ? dy / scale : dy;
     }
@@ -54,26 +58,26 @@ __global__ __launch_bounds__(256) void kag_prep_k(const int64_t* __restrict__ id
       float dot = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int d = lane + 64 * q;
+        const int d = l + LPI * q;
         if (d < D) dot += Elem<TO>::ld(out + it * D + d) * v[q];
       }
-      dot = wave_sum(dot);
+      dot = group_sum<LPI>(dot);
       const float nrm = norms[it];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int d = lane + 64 * q;
+        const int d = l + LPI * q;
         if (d < D) v[q] = nrm > 1e-12f ? (v[q] - Elem<TO>::ld(out + it * D + d) * dot) / nrm : v[q] / 1e-12f;
       }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int d = lane + 64 * q;
+      const int d = l + LPI * q;
       if (d < D) g[it * D + d] = v[q];
     }
-    if (lane < K) {
-      const int64_t row = (F > 1 ? (it % F) * P : 0) + kshift_row(ids[it], lane, P);
-      keys[it * K + lane] = (uint32_t)row;
-      vals[it * K + lane] = (uint32_t)it;
+    if (l < K) {
+      const int64_t row = (F > 1 ? (it % F) * P : 0) + kshift_row(ids[it], l, P);
+      keys[it * K + l] = (uint32_t)row;
+      vals[it * K + l] = (uint32_t)it;
     }
   }
 }
@@ -452,10 +456,19 @@ extern "C" int lthm_kshift_adagrad_fused(const int64_t* ids, int64_t n, int32_t 
   float* g = (float*)(w + L.g);
   uint32_t* keys = (uint32_t*)(w + L.keys);
   uint32_t* vals = (uint32_t*)(w + L.vals);
-  const int pg = grid_for(items, 4, kag_cu_count() * 16);
-#define KAG_PREP(TY, TO)                                                                                        \
-  hipLaunchKernelGGL((kag_prep_k<TY, TO>), dim3(pg), dim3(256), 0, s, ids, items, F, (const TY*)dY, (const TO*)out, \
-                     norms, P, D, K, mode, scale, g, keys, vals)
+  // lanes per item: >= K and >= D / 4, a power of two in [16, 64]
+  const int need = K > (D + 3) / 4 ? K : (D + 3) / 4;
+  const int lpi = need <= 16 ? 16 : need <= 32 ? 32 : 64;
+  const int pg = grid_for(items, 4 * (64 / lpi), kag_cu_count() * 16);
+#define KAG_PREP_L(TY, TO, LPI)                                                                                   \
+  hipLaunchKernelGGL((kag_prep_k<TY, TO, LPI>), dim3(pg), dim3(256), 0, s, ids, items, F, (const TY*)dY,           \
+                     (const TO*)out, norms, P, D, K, mode, scale, g, keys, vals)
+#define KAG_PREP(TY, TO)                      \
+  do {                                        \
+    if (lpi == 16) KAG_PREP_L(TY, TO, 16);    \
+    else if (lpi == 32) KAG_PREP_L(TY, TO, 32); \
+    else KAG_PREP_L(TY, TO, 64);              \
+  } while (0)
   const int od = out ? out_dtype : LTHM_F32;
   if (dy_dtype == LTHM_F32 && od == LTHM_F32) KAG_PREP(float, float);
   else if (dy_dtype == LTHM_F32 && od == LTHM_BF16) KAG_PREP(float, bf16_t);
@@ -463,6 +476,7 @@ extern "C" int lthm_kshift_adagrad_fused(const int64_t* ids, int64_t n, int32_t 
   else if (dy_dtype == LTHM_BF16 && od == LTHM_BF16) KAG_PREP(bf16_t, bf16_t);
   else return (int)hipErrorInvalidValue;
 #undef KAG_PREP
+#undef KAG_PREP_L
   LTHM_CHECK_LAUNCH();
   uint32_t* skeys = (uint32_t*)(w + L.skeys);
   uint32_t* svals = (uint32_t*)(w + L.svals);
