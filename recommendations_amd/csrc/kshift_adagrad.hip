@@ -25,6 +25,8 @@
 // atomic on the table: each row is written by exactly one lane group.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace lthm {
@@ -397,7 +399,11 @@ static int kag_launch_groups(const KagLayout& L, unsigned char* w, int64_t N, in
   uint32_t* longlist = (uint32_t*)(w + L.longlist);
   uint32_t* lpref = (uint32_t*)(w + L.lpref);
   float* part = (float*)(w + L.part);
-  const int cap = kag_cu_count() * 16;
+  // workgroups per CU of the row / chunk passes (latency-bound: more groups in flight);
+  // LTHM_KAG_BPC overrides (A/B, profiles/r06p/: 8 / 16 / 32 per CU -> 0.658 / 0.602 / 0.592 ms per
+  // generator step)
+  static const int bpc = getenv("LTHM_KAG_BPC") ? atoi(getenv("LTHM_KAG_BPC")) : 32;
+  const int cap = kag_cu_count() * (bpc > 0 ? bpc : 32);
   const int gpb = 256 / LG;
   hipLaunchKernelGGL((kag_apply_k<LG, NQ, CW>), dim3(grid_for(N, gpb, cap)), dim3(256), 0, s, skeys, svals, starts, cnt, N,
                      g, D, W, S, clr, eps, longlist, (int*)(cnt + 1));
