@@ -338,9 +338,24 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
         }
         atomicAdd(dW + row * D + d, acc);
       }
-      if (flags != nullptr && gl == 0) {
-        if (atomicExch(flags + row, 1) == 0) s_new[atomicAdd(&s_nnew, 1)] = row;
+    }
+    // touched-row flags: every segment's first-touch test with its returning atomic issued side
+    // by side (up to KB_NP / 256 per thread in flight), not one per lane group inside the segment
+    // loop above, where each waited for its return before the group's next segment
+    if (flags != nullptr) {
+      constexpr int FQ = KB_NP / 256;
+      int64_t rr[FQ];
+      int old[FQ];
+#pragma unroll
+      for (int q = 0; q < FQ; ++q) {
+        const int s = tid + 256 * q;
+        rr[q] = s < nseg ? (int64_t)(keys[segs[s]] >> 12) : -1;
       }
+#pragma unroll
+      for (int q = 0; q < FQ; ++q) old[q] = rr[q] >= 0 ? atomicExch(flags + rr[q], 1) : 1;
+#pragma unroll
+      for (int q = 0; q < FQ; ++q)
+        if (old[q] == 0) s_new[atomicAdd(&s_nnew, 1)] = rr[q];
     }
     __syncthreads();
     if (flags != nullptr) {
