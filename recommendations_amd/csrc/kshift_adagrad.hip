@@ -181,8 +181,21 @@ __global__ __launch_bounds__(256) void kag_apply_k(const uint32_t* __restrict__ 
   const int nseg = *nseg_p;
   const int gl = threadIdx.x % LG;
   const int64_t ngrp = (int64_t)gridDim.x * (256 / LG);
-  for (int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LG; u < nseg; u += ngrp) {
-    const uint32_t s0 = starts[u], s1 = u + 1 < nseg ? starts[u + 1] : (uint32_t)N;
+  int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LG;
+  // the next segment's bounds are loaded one iteration ahead (the grid-stride loop is a chain
+  // of dependent loads: bounds -> row and items -> W / state / gradients)
+  uint32_t n0 = 0, n1 = 0;
+  if (u < nseg) {
+    n0 = starts[u];
+    n1 = u + 1 < nseg ? starts[u + 1] : (uint32_t)N;
+  }
+  for (; u < nseg; u += ngrp) {
+    const uint32_t s0 = n0, s1 = n1;
+    const int64_t un = u + ngrp;
+    if (un < nseg) {
+      n0 = starts[un];
+      n1 = un + 1 < nseg ? starts[un + 1] : (uint32_t)N;
+    }
     if (s1 - s0 > (uint32_t)KAG_CH) {
       if (gl == 0) longlist[atomicAdd(nlong, 1)] = (uint32_t)u;
       continue;
