@@ -212,6 +212,9 @@ __global__ __launch_bounds__(KS_BLOCK) void kshift_fwd_reg_k(const int64_t* __re
 // Backward: LDS-staged dedup + wave-segmented reduction + one f32 add per
 // unique row per workgroup.
 // ---------------------------------------------------------------------------
+#ifndef LTHM_KSB_X
+#define LTHM_KSB_X 0  // cost-ladder builds of kshift_bwd_dense_k (tools/build_variant.sh; wrong results)
+#endif
 constexpr int KB_NP = 2048;            // max (row, item) pairs per workgroup
 constexpr int KB_G_FLOATS = 16384;     // LDS budget for per-item gradients (64 KiB)
 
@@ -274,8 +277,8 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
       keys[p] = key;
     }
     __syncthreads();
-    // 3) bitonic sort of NP2 keys in LDS
-    for (int k = 2; k <= NP2; k <<= 1) {
+    // 3) bitonic sort of NP2 keys in LDS (LTHM_KSB_X=1 cost-ladder build: skipped, timing only)
+    for (int k = 2; k <= (LTHM_KSB_X == 1 ? 1 : NP2); k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
         for (int t = tid; t < NP2 / 2; t += 256) {
           const int i0 = 2 * t - (t & (j - 1));
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(256) void kshift_bwd_dense_k(
           const int it = (int)(keys[p] & 0xfff) / K;
           acc += g[it * D + d];
         }
-        atomicAdd(dW + row * D + d, acc);
+        if (LTHM_KSB_X != 2) atomicAdd(dW + row * D + d, acc);  // LTHM_KSB_X=2: no row adds (timing only)
       }
     }
     // touched-row flags: every segment's first-touch test with its returning atomic issued side
