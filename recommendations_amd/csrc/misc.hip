@@ -155,8 +155,10 @@ __global__ __launch_bounds__(256) void logq_apply_k(LogqArgs p) {
     const uint32_t key = p.keys[s];
     if (key == LQ_EMPTY) continue;
     float b = p.bt[key], a = p.at[key];
-    p.b0[s] = b;
-    p.a0[s] = a;
+    if (p.out) {  // the pre-call state: only logq_out_k's replays read it
+      p.b0[s] = b;
+      p.a0[s] = a;
+    }
     for (int w = 0; w < p.n_w; ++w) {
       uint32_t m = p.bits[s * p.n_w + w];
       while (m) {
