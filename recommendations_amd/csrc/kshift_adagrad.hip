@@ -512,9 +512,10 @@ extern "C" int lthm_kshift_adagrad_fused(const int64_t* ids, int64_t n, int32_t 
                                     (const uint8_t*)heads, (uint32_t*)(w + L.starts), (int*)(w + L.cnt), (int)N,
                                     s) != hipSuccess)
     return (int)hipErrorLaunchFailure;
-  // lane groups sized to the row: 16-B column slots when D % 4 == 0 (D / 4 lanes rounded up to a
-  // power of two: D = 32 -> 8 lanes, 8 rows per wave in flight), else one column per slot
-  if (D % 4 == 0) {
+  // lane groups sized to the row: 16-B column slots when D % 4 == 0 and W / state_sum are 16-B
+  // aligned (D / 4 lanes rounded up to a power of two: D = 32 -> 8 lanes, 8 rows per wave in
+  // flight), else one column per slot
+  if (D % 4 == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)state_sum % 16) == 0) {
     if (D <= 4) return kag_launch_groups<1, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
     if (D <= 8) return kag_launch_groups<2, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);
     if (D <= 16) return kag_launch_groups<4, 1, 4>(L, w, N, D, W, state_sum, clr, eps, s);

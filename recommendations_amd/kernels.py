@@ -1042,6 +1042,7 @@ def kshift_adagrad_fused(ids, gy, out, norms, P, K, mode, F, W, state, clr, eps)
     _check_kshift(ids, P, K, F, D, table_rows=W.shape[0], gy=gy, out=out, norms=norms)
     _check(W.dtype == torch.float32 and state.dtype == torch.float32 and state.shape == W.shape,
            "kshift_adagrad_fused: W and state are [F * P, D] float32")
+    _check(W.is_contiguous() and state.is_contiguous(), "kshift_adagrad_fused: W and state contiguous")
     _check(mode != KSHIFT_NORMALIZE or (out is not None and norms is not None), "normalize mode needs out / norms")
     n = ids.numel() // F
     if n == 0:
@@ -1049,7 +1050,7 @@ def kshift_adagrad_fused(ids, gy, out, norms, P, K, mode, F, W, state, clr, eps)
     need = _kag_need.get((n * F, K, D))
     if need is None:  # (the size query asks the sort for its temporary storage: once per shape)
         need = _kag_need[(n * F, K, D)] = load().lthm_kshift_adagrad_ws_bytes(n * F, K, D)
-    _check(need > 0,f"kshift_adagrad_fused: unsupported sizes (n * F * K = {n * F * K}, D = {D}, K = {K})")
+    _check(need > 0, f"kshift_adagrad_fused: unsupported sizes (n * F * K = {n * F * K}, D = {D}, K = {K})")
     key = (ids.device, torch.cuda.current_stream(ids.device).cuda_stream)
     ws = _kag_ws.get(key)
     if ws is None or ws.numel() < need:

@@ -61,6 +61,24 @@ def test_fused_adagrad_bit_exact(dev, mode, K, F_, D, P, n, gdt):
         assert (ref.kshift_rows(ids.reshape(-1), P, K) == P - 1).sum() > 256  # the long path ran
 
 
+def test_fused_adagrad_unaligned_tables(dev):
+    """W / state views 4 bytes off a 16-B boundary (D % 4 == 0): the scalar column slots, same bits."""
+    from recommendations_amd import kernels as KK
+    K, F_, D, P, n = 8, 1, 32, 400, 900
+    rng, ids, W0, S0 = _case(11, n, F_, P, D)
+    Wb = torch.empty(F_ * P * D + 1, device=dev)
+    Sb = torch.empty(F_ * P * D + 1, device=dev)
+    W, S = Wb[1:].view(F_ * P, D), Sb[1:].view(F_ * P, D)
+    W.copy_(torch.from_numpy(W0))
+    S.copy_(torch.from_numpy(S0))
+    dY = rng.standard_normal((n * F_, D)).astype(np.float32)
+    KK.kshift_adagrad_fused(torch.from_numpy(ids).to(dev), torch.from_numpy(dY).to(dev), None, None, P, K, 0, F_, W, S,
+                            0.5, 1e-10)
+    Wo, So = ref.kshift_adagrad_ref(ids, ref.kshift_pool_grad(dY, K, 0), P, K, F_, W0, S0, 0.5, 1e-10)
+    torch.cuda.synchronize()
+    assert np.array_equal(W.cpu().numpy(), Wo) and np.array_equal(S.cpu().numpy(), So)
+
+
 def test_fused_adagrad_normalize(dev):
     from recommendations_amd import kernels as KK
     K, D, P, n = 16, 32, 800, 2500
