@@ -169,3 +169,32 @@ def test_fused_zero_grad_drops_pending(dev):
     m(ids).square().sum().backward()
     opt.step()
     assert not torch.equal(m.weight.detach(), w0)
+
+
+@pytest.mark.parametrize("K,D", [(64, 256), (64, 1), (1, 256)])
+def test_fused_adagrad_size_limits(dev, K, D):
+    """The largest K (64 lanes per item) and D (four 16-B column slots per lane), and D = 1:
+    bit-identical to the restatement."""
+    from recommendations_amd import kernels as KK
+    P, n = 300, 400
+    rng, ids, W0, S0 = _case(5 + K + D, n, 1, P, D)
+    W = torch.from_numpy(W0).to(dev)
+    S = torch.from_numpy(S0).to(dev)
+    dY = rng.standard_normal((n, D)).astype(np.float32)
+    KK.kshift_adagrad_fused(torch.from_numpy(ids).to(dev), torch.from_numpy(dY).to(dev), None, None, P, K, 0, 1, W, S,
+                            0.5, 1e-10)
+    Wo, So = ref.kshift_adagrad_ref(ids, ref.kshift_pool_grad(dY, K, 0), P, K, 1, W0, S0, 0.5, 1e-10)
+    torch.cuda.synchronize()
+    assert np.array_equal(W.cpu().numpy(), Wo) and np.array_equal(S.cpu().numpy(), So)
+
+
+def test_fused_adagrad_empty_batch(dev):
+    """No ids: nothing launched, the table and state unchanged."""
+    from recommendations_amd import kernels as KK
+    W = torch.randn(64, 8, device=dev)
+    S = torch.rand(64, 8, device=dev)
+    w0, s0 = W.clone(), S.clone()
+    KK.kshift_adagrad_fused(torch.empty(0, 1, dtype=torch.int64, device=dev), torch.empty(0, 8, device=dev), None, None,
+                            64, 4, 0, 1, W, S, 0.5, 1e-10)
+    torch.cuda.synchronize()
+    assert torch.equal(W, w0) and torch.equal(S, s0)
