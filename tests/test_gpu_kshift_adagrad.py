@@ -4,7 +4,8 @@ torch.optim.Adagrad by tests/test_kshift_adagrad_cpu.py):
 
 * scale / plain modes: bit-identical tables and Adagrad state (same pair order, same f32
   operations), over two steps, short and long (> 256 pairs, chunked) rows, F = 1..3 tables,
-  D from 4 to 200, f32 and bf16 upstream gradients;
+  D from 1 to 256, K up to 64, tables off a 16-B boundary, an empty batch, f32 and bf16 upstream
+  gradients;
 * normalize mode: the per-item F.normalize backward's dot product runs in another order on the
   GPU (wave reduction vs float64): 1e-5;
 * the module path (KShiftEmbedding + SparseRowAdagrad(fused=True), two backwards before one
